@@ -1,0 +1,118 @@
+/*
+ * dmx.h — C-ABI of the MI355X-native two-round barcode demultiplexer (libdmx.so).
+ *
+ * Drop-in boundary.  In the reference the hot path is a PROCESS boundary: bash calls the
+ * `cutadapt` executable (scripts/02_cutadapt_loop.sh:64-72 round 1, :91-103 round 2;
+ * scripts/04_cleaning_primers.sh:371-388 linked primers).  Our drop-in `cutadapt` CLI
+ * (nanopore-barcoding-orc_amd/bin/cutadapt, Python) keeps that surface and calls this library
+ * through ctypes.  Each entry point below names the cutadapt-side interface whose work it
+ * replaces (upstream cutadapt 4.9 is not vendored in /root/reference).
+ *
+ * Conventions: plain pointers and sizes, no torch types.  Host buffers are caller-owned, device
+ * buffers library-owned.  Status 0 = OK, negative = error (message via dmx_last_error).
+ * One context per device; a context is not thread-safe (one host thread per context).
+ */
+#ifndef DMX_H
+#define DMX_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DMX_ABI_VERSION 1
+
+/* Panel flags (dmx_set_panel.flags). */
+#define DMX_FRONT 0x01  /* -g ADAPTER: 5' adapter, Where.FRONT (prefix of adapter may be skipped at read start) */
+#define DMX_BACK 0x02   /* -a ADAPTER: 3' adapter, Where.BACK  (suffix may be skipped at read end)          */
+#define DMX_RC 0x10     /* --rc: also try the reverse complement; use it iff its score is strictly greater  */
+
+/* Run modes (dmx_set_mode). */
+#define DMX_MODE_SINGLE 0    /* one cutadapt invocation: round 0 panel only                                   */
+#define DMX_MODE_TWO_ROUND 1 /* 02_cutadapt_loop.sh fused: round 0 on the read, round 1 on the round-0-trimmed */
+#define DMX_MODE_LINKED 2    /* -g F...R linked pairs: round 0 = fronts, round 1 = backs (pair i <-> i)        */
+
+/* Error codes. */
+#define DMX_OK 0
+#define DMX_E_INVALID -1
+#define DMX_E_HIP -2
+#define DMX_E_NOMEM -3
+#define DMX_E_UNSUPPORTED -4
+#define DMX_E_STATE -5
+
+/* One adapter match (cutadapt Match: astart/astop on the adapter, rstart/rstop on the read view
+ * that round was run on, i.e. already reverse-complemented when rc == 1). */
+typedef struct dmx_match {
+    int32_t rstart, rstop;
+    int16_t astart, astop;
+    int16_t score, errors;
+} dmx_match;
+
+/* Per-read result (caller-owned array, one entry per read).
+ * bin = adapter index in the panel (file order), -1 = no match ("unknown").
+ * TWO_ROUND: m2 coordinates are on the round-1 output (trimmed, oriented) sequence.
+ * LINKED: bin1 = bin2 = pair index; m1 = front part on the read, m2 = back part on
+ *         read[m1.rstop:]. */
+typedef struct dmx_result {
+    int16_t bin1, bin2;
+    uint8_t rc1, rc2;
+    uint8_t flags, _pad;
+    dmx_match m1, m2;
+} dmx_result;
+
+typedef struct dmx_ctx dmx_ctx;
+
+/* Replaces: process start-up of `cutadapt -j N` (cli.main).  Opens HIP device `device`. */
+int dmx_open(int device, dmx_ctx** out);
+/* Replaces: cutadapt's exit. */
+void dmx_close(dmx_ctx* ctx);
+const char* dmx_last_error(dmx_ctx* ctx);
+int dmx_abi_version(void);
+
+/* Replaces: parser.py adapter parsing of `-g file:` / `-a file:` / `-g F...R` (one call per panel).
+ * seqs: uppercase IUPAC (U already mapped to T), lens <= 64.  max_errors: -e value (< 1 rate,
+ * >= 1 absolute count).  min_overlap: -O (cutadapt default 3).  Adapter wildcards are enabled for
+ * an adapter iff it has a non-ACGT character (cutadapt default). */
+int dmx_set_panel(dmx_ctx* ctx, int round, const char* const* seqs, const int* lens,
+                  int n_adapters, double max_errors, int min_overlap, int flags);
+int dmx_set_mode(dmx_ctx* ctx, int mode);
+
+/* Host-side packer (no GPU needed): ASCII reads -> 2-bit codes (A=0,C=1,G=2,T=3, 16 nt per
+ * little-endian u32 word) + 1-bit "no-match" mask (any non-ACGT byte, e.g. N).  Reads are laid
+ * out back to back starting at nt offset DMX_PACK_PAD; out_offsets[i] is read i's first nt.
+ * Required words for both outputs: dmx_pack_words(total_nt). */
+#define DMX_PACK_PAD 64
+size_t dmx_pack_words(uint64_t total_nt, size_t n_reads);
+int dmx_pack(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens, size_t n_reads,
+             uint32_t* out_seq2b, uint32_t* out_nmask, uint64_t* out_offsets);
+
+/* Replaces: the per-read hot loop of one or more cutadapt runs (ReverseComplementer ->
+ * AdapterCutter.best_match -> Adapter.match_to -> Aligner.locate, for every read) for the whole
+ * input.  Synchronous: uploads, runs both rounds on the GPU, downloads `out`. */
+int dmx_run(dmx_ctx* ctx, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
+            const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out);
+
+/* Device-resident form (benchmarks / pipelined hosts): dmx_load copies a packed batch to HBM
+ * once; dmx_exec enqueues the full pipeline on the context's stream (asynchronous); dmx_sync
+ * waits; dmx_fetch copies results of the last exec to the host. */
+int dmx_load(dmx_ctx* ctx, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
+             const uint32_t* lens, size_t n_words, size_t n_reads);
+int dmx_exec(dmx_ctx* ctx);
+int dmx_sync(dmx_ctx* ctx);
+int dmx_fetch(dmx_ctx* ctx, dmx_result* out);
+
+/* Replaces: cutadapt's per-adapter match statistics (report.py).  counts has
+ * (A0+1)*(A1+1) entries: index (bin1+1)*(A1+1) + (bin2+1) (A1 = 0 in SINGLE mode), then
+ * two more entries: number of reads that used the reverse complement in round 0 / round 1. */
+int dmx_counts(dmx_ctx* ctx, uint64_t* out_counts, size_t n_out);
+
+/* Diagnostics of the last dmx_exec: per-stage device time in ms measured with HIP events on the
+ * context's stream (order: scan0, resolve0, finalize0, scan1, resolve1, finalize1), the number of
+ * candidate clusters per round, and overflow / window-violation flags (must be 0). */
+int dmx_stats(dmx_ctx* ctx, float* stage_ms, int n_stage, uint64_t* clusters, int* flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DMX_H */

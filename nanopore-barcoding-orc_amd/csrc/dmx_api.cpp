@@ -1,0 +1,492 @@
+// dmx_api.cpp — C-ABI of libdmx (include/dmx.h): context, panels, packing, batch execution.
+//
+// Panel rules restate cutadapt 4.9 adapter construction (parser.py / adapters.py, not vendored
+// in /root/reference): name/sequence come from the FASTA, sequences are
+// uppercase with U->T, adapter wildcards are enabled iff a non-ACGT character is present,
+// k = int(max_error_rate * m), acceptance `cost <= effective_length * max_error_rate` in IEEE
+// double with effective length excluding adapter N's, minimum overlap -O (default 3).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "dmx_internal.h"
+
+using namespace dmx;
+
+#define CK(call)                                                                        \
+    do {                                                                                \
+        hipError_t e_ = (call);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            c->err = std::string(#call) + ": " + hipGetErrorString(e_);                 \
+            return DMX_E_HIP;                                                           \
+        }                                                                               \
+    } while (0)
+
+namespace {
+
+constexpr int kPackAlign = 32;   // every read starts on a 32-nt (one nmask word) boundary
+
+uint8_t iupac_mask(char ch) {
+    switch (ch) {
+        case 'A': return 1;
+        case 'C': return 2;
+        case 'G': return 4;
+        case 'T': return 8;
+        case 'R': return 5;
+        case 'Y': return 10;
+        case 'S': return 6;
+        case 'W': return 9;
+        case 'K': return 12;
+        case 'M': return 3;
+        case 'B': return 14;
+        case 'D': return 13;
+        case 'H': return 11;
+        case 'V': return 7;
+        case 'N': return 15;
+        default: return 0;
+    }
+}
+
+template <typename T>
+int dev_alloc(Ctx* c, T** p, size_t count) {
+    if (*p) {
+        hipFree(*p);
+        *p = nullptr;
+    }
+    if (count == 0) count = 1;
+    CK(hipMalloc((void**)p, count * sizeof(T)));
+    return DMX_OK;
+}
+
+struct PackTables {
+    uint8_t code[256];
+    uint8_t nflag[256];
+    PackTables() {
+        for (int i = 0; i < 256; ++i) {
+            code[i] = 0;
+            nflag[i] = 1;
+        }
+        const char* s = "ACGT";
+        for (int k = 0; k < 4; ++k) {
+            code[(uint8_t)s[k]] = code[(uint8_t)(s[k] + 32)] = (uint8_t)k;
+            nflag[(uint8_t)s[k]] = nflag[(uint8_t)(s[k] + 32)] = 0;
+        }
+    }
+};
+const PackTables kTables;
+
+void pack_range(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens, size_t lo,
+                size_t hi, const uint64_t* out_offsets, uint32_t* seq, uint32_t* nmask) {
+    for (size_t r = lo; r < hi; ++r) {
+        const uint8_t* src = ascii + offsets[r];
+        const uint32_t n = lens[r];
+        const uint64_t g0 = out_offsets[r];   // multiple of 32
+        uint32_t* sw = seq + g0 / 16;
+        uint32_t* nw = nmask + g0 / 32;
+        for (uint32_t x = 0; x < n; x += 32) {
+            const uint32_t cnt = std::min<uint32_t>(32u, n - x);
+            uint32_t w0 = 0, w1 = 0, nb = 0;
+            for (uint32_t y = 0; y < cnt; ++y) {
+                const uint8_t ch = src[x + y];
+                const uint32_t cd = kTables.code[ch];
+                if (y < 16) w0 |= cd << (2 * y);
+                else w1 |= cd << (2 * (y - 16));
+                nb |= (uint32_t)kTables.nflag[ch] << y;
+            }
+            sw[x / 16] = w0;
+            if (cnt > 16) sw[x / 16 + 1] = w1;
+            nw[x / 32] = nb;
+        }
+    }
+}
+
+int ensure_pipeline(Ctx* c) {
+    const size_t n = c->n_reads;
+    const bool linked = c->mode == DMX_MODE_LINKED;
+    const size_t slots0 = linked ? n * (size_t)std::max(1, c->panel[0].n) : n;
+    const size_t items = linked ? slots0 : n;
+    if (c->slot_cap < std::max(slots0, items) || !c->d_res || c->cap_reads < n) {
+        const size_t s = std::max(slots0, items);
+        int rc;
+        if ((rc = dev_alloc(c, &c->d_res, n))) return rc;
+        for (int r = 0; r < 2; ++r) {
+            if ((rc = dev_alloc(c, &c->d_winner[r], s))) return rc;
+            if ((rc = dev_alloc(c, &c->d_origin[r], s))) return rc;
+        }
+        if ((rc = dev_alloc(c, &c->d_items, items))) return rc;
+        c->slot_cap = s;
+        c->item_cap = items;
+        c->cap_reads = n;
+    }
+    c->item_cap = items;
+    const size_t want_cl = 4 * std::max(slots0, n) + 65536;
+    if (c->cl_cap < want_cl) {
+        int rc;
+        for (int r = 0; r < 2; ++r) {
+            if ((rc = dev_alloc(c, &c->d_cl[r], want_cl))) return rc;
+            if ((rc = dev_alloc(c, &c->d_outc[r], want_cl))) return rc;
+        }
+        c->cl_cap = want_cl;
+    }
+    const size_t a1 = c->mode == DMX_MODE_SINGLE ? 0 : (size_t)c->panel[1].n;
+    const size_t nc = ((size_t)c->panel[0].n + 1) * (a1 + 1) + 2;
+    if (c->n_counts != nc) {
+        int rc;
+        if ((rc = dev_alloc(c, &c->d_counts, nc))) return rc;
+        c->n_counts = nc;
+    }
+    return DMX_OK;
+}
+
+int grow_clusters(Ctx* c) {
+    const size_t want = c->cl_cap * 2;
+    int rc;
+    for (int r = 0; r < 2; ++r) {
+        if ((rc = dev_alloc(c, &c->d_cl[r], want))) return rc;
+        if ((rc = dev_alloc(c, &c->d_outc[r], want))) return rc;
+    }
+    c->cl_cap = want;
+    return DMX_OK;
+}
+
+}  // namespace
+
+struct dmx_ctx : Ctx {};
+
+extern "C" {
+
+int dmx_abi_version(void) { return DMX_ABI_VERSION; }
+
+int dmx_open(int device, dmx_ctx** out) {
+    if (!out) return DMX_E_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return DMX_E_HIP;
+    dmx_ctx* c = new dmx_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return DMX_E_HIP;
+    }
+    for (auto& e : c->ev) hipEventCreate(&e);
+    for (int r = 0; r < 2; ++r) hipMalloc((void**)&c->d_panel[r], sizeof(DevPanel));
+    hipMalloc((void**)&c->d_counters, 16 * sizeof(uint32_t));
+    *out = c;
+    return DMX_OK;
+}
+
+void dmx_close(dmx_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    void* bufs[] = {c->d_seq,       c->d_nmask,     c->d_offs,     c->d_lens,      c->d_res,
+                    c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_cl[0],
+                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items,     c->d_counters,
+                    c->d_counts,    c->d_panel[0],  c->d_panel[1]};
+    for (void* b : bufs)
+        if (b) hipFree(b);
+    for (auto& e : c->ev)
+        if (e) hipEventDestroy(e);
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* dmx_last_error(dmx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int dmx_set_mode(dmx_ctx* c, int mode) {
+    if (!c) return DMX_E_INVALID;
+    if (mode != DMX_MODE_SINGLE && mode != DMX_MODE_TWO_ROUND && mode != DMX_MODE_LINKED) {
+        c->err = "unknown mode";
+        return DMX_E_INVALID;
+    }
+    if (mode == DMX_MODE_LINKED) {
+        c->err = "linked mode is not implemented on the GPU path yet";
+        return DMX_E_UNSUPPORTED;
+    }
+    c->mode = mode;
+    return DMX_OK;
+}
+
+int dmx_set_panel(dmx_ctx* c, int round, const char* const* seqs, const int* lens, int n,
+                  double max_errors, int min_overlap, int flags) {
+    if (!c || round < 0 || round > 1 || !seqs || !lens) return DMX_E_INVALID;
+    if (n <= 0 || n > kMaxAdapters) {
+        c->err = "panel must hold 1..64 adapters";
+        return DMX_E_INVALID;
+    }
+    if (!(flags & (DMX_FRONT | DMX_BACK)) || ((flags & DMX_FRONT) && (flags & DMX_BACK))) {
+        c->err = "panel flags need exactly one of DMX_FRONT / DMX_BACK";
+        return DMX_E_INVALID;
+    }
+    if (!(max_errors >= 0.0)) {
+        c->err = "max_errors must be >= 0";
+        return DMX_E_INVALID;
+    }
+    HostPanel hp;
+    hp.n = n;
+    hp.n_orient = (flags & DMX_RC) ? 2 : 1;
+    for (int a = 0; a < n; ++a) {
+        const int m = lens[a];
+        if (m <= 0 || m > kMaxLen) {
+            c->err = "adapter length must be 1..64 (one 64-bit Myers word)";
+            return DMX_E_UNSUPPORTED;
+        }
+        DevAdapter& ad = hp.ad[a];
+        memset(&ad, 0, sizeof(ad));
+        bool wild = false;
+        for (int i = 0; i < m; ++i) {
+            const char ch = seqs[a][i];
+            if (!iupac_mask(ch)) {
+                c->err = std::string("adapter character not IUPAC uppercase: ") + ch;
+                return DMX_E_INVALID;
+            }
+            if (ch != 'A' && ch != 'C' && ch != 'G' && ch != 'T') wild = true;
+        }
+        const double rate = max_errors >= 1.0 ? max_errors / (double)m : max_errors;
+        const int k = (int)(rate * m);
+        if (m + k + 2 > kRing) {
+            c->err = "error rate too high for the resolve window (m + k + 2 > 128)";
+            return DMX_E_UNSUPPORTED;
+        }
+        int ncount[kMaxLen + 1];
+        int nc = 0;
+        for (int i = 0; i < m; ++i) {
+            ncount[i] = nc;
+            if (seqs[a][i] == 'N') ++nc;
+        }
+        ncount[m] = nc;
+        const int eff_len = wild ? m - nc : m;
+        if (eff_len == 0) {
+            c->err = "adapter consists only of N wildcards";
+            return DMX_E_INVALID;
+        }
+        for (int i = 0; i < m; ++i) {
+            // Adapter wildcards: IUPAC mask vs read base; otherwise ASCII equality. Read codes
+            // 4..7 (any non-ACGT byte) match nothing in either mode.
+            const uint8_t mask = wild ? iupac_mask(seqs[a][i]) : iupac_mask(seqs[a][i]);
+            for (int code = 0; code < 4; ++code)
+                if (mask & (1u << code)) ad.peq[code] |= 1ull << i;
+        }
+        int kk = -1;
+        for (int L = 0; L < 72; ++L) {
+            int allow = -1;
+            if (L <= m && L >= min_overlap) {
+                const int eff = wild ? (L < m ? L - ncount[L] : eff_len) : L;
+                const double lim = (double)eff * rate;
+                for (int cst = 0; cst <= 127 && (double)cst <= lim; ++cst) allow = cst;
+            }
+            ad.acc[L] = (int8_t)allow;
+            kk = std::max(kk, allow);
+        }
+        ad.m = (uint8_t)m;
+        ad.k = (uint8_t)k;
+        ad.kk = (int8_t)std::min(kk, k);
+        ad.where = (flags & DMX_FRONT) ? kFront : kBack;
+    }
+    hp.set = true;
+    c->panel[round] = hp;
+    DevPanel dp;
+    memset(&dp, 0, sizeof(dp));
+    dp.n_adapters = hp.n;
+    dp.n_orient = hp.n_orient;
+    for (int a = 0; a < n; ++a) dp.ad[a] = hp.ad[a];
+    CK(hipSetDevice(c->device));
+    CK(hipMemcpy(c->d_panel[round], &dp, sizeof(dp), hipMemcpyHostToDevice));
+    return DMX_OK;
+}
+
+size_t dmx_pack_words(uint64_t total_nt, size_t n_reads) {
+    const uint64_t nt = 2 * (uint64_t)DMX_PACK_PAD + total_nt + (uint64_t)kPackAlign * n_reads;
+    return (size_t)((nt + 31) / 32 * 2 + 4);
+}
+
+int dmx_pack(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens, size_t n_reads,
+             uint32_t* out_seq2b, uint32_t* out_nmask, uint64_t* out_offsets) {
+    if ((!ascii && n_reads) || !out_seq2b || !out_nmask || !out_offsets) return DMX_E_INVALID;
+    uint64_t g = DMX_PACK_PAD;
+    uint64_t total = 0;
+    for (size_t r = 0; r < n_reads; ++r) {
+        out_offsets[r] = g;
+        g += ((uint64_t)lens[r] + kPackAlign - 1) / kPackAlign * kPackAlign;
+        total += lens[r];
+    }
+    const size_t words = dmx_pack_words(total, n_reads);
+    memset(out_seq2b, 0, words * sizeof(uint32_t));
+    memset(out_nmask, 0, words * sizeof(uint32_t));
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t nth = n_reads < 4096 ? 1 : hw;
+    if (nth == 1) {
+        pack_range(ascii, offsets, lens, 0, n_reads, out_offsets, out_seq2b, out_nmask);
+    } else {
+        std::vector<std::thread> th;
+        const size_t per = (n_reads + nth - 1) / nth;
+        for (size_t t = 0; t < nth; ++t) {
+            const size_t lo = t * per, hi = std::min(n_reads, lo + per);
+            if (lo >= hi) break;
+            th.emplace_back(pack_range, ascii, offsets, lens, lo, hi, out_offsets, out_seq2b,
+                            out_nmask);
+        }
+        for (auto& t : th) t.join();
+    }
+    return DMX_OK;
+}
+
+int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
+             const uint32_t* lens, size_t n_words, size_t n_reads) {
+    if (!c || (n_reads && (!seq2b || !nmask || !offsets || !lens))) return DMX_E_INVALID;
+    if (n_reads >= (1ull << 31)) {
+        c->err = "too many reads in one batch";
+        return DMX_E_UNSUPPORTED;
+    }
+    for (size_t r = 0; r < n_reads; ++r) {
+        if (offsets[r] < 16 || (offsets[r] + lens[r] + 64) > (uint64_t)n_words * 16 ||
+            lens[r] >= (1u << 30)) {
+            c->err = "read offsets/lengths do not fit the packed buffer (use dmx_pack)";
+            return DMX_E_INVALID;
+        }
+    }
+    CK(hipSetDevice(c->device));
+    int rc;
+    if (c->cap_words < n_words) {
+        if ((rc = dev_alloc(c, &c->d_seq, n_words))) return rc;
+        if ((rc = dev_alloc(c, &c->d_nmask, n_words))) return rc;
+        c->cap_words = n_words;
+    }
+    if (!c->d_offs || c->cap_reads < n_reads) {
+        if ((rc = dev_alloc(c, &c->d_offs, n_reads))) return rc;
+        if ((rc = dev_alloc(c, &c->d_lens, n_reads))) return rc;
+        c->cap_reads = 0;   // force pipeline re-allocation
+    }
+    c->n_reads = n_reads;
+    c->n_words = n_words;
+    CK(hipMemcpyAsync(c->d_seq, seq2b, n_words * 4, hipMemcpyHostToDevice, c->stream));
+    CK(hipMemcpyAsync(c->d_nmask, nmask, n_words * 4, hipMemcpyHostToDevice, c->stream));
+    if (n_reads) {
+        CK(hipMemcpyAsync(c->d_offs, offsets, n_reads * 8, hipMemcpyHostToDevice, c->stream));
+        CK(hipMemcpyAsync(c->d_lens, lens, n_reads * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    CK(hipStreamSynchronize(c->stream));
+    c->executed = false;
+    return DMX_OK;
+}
+
+int dmx_exec(dmx_ctx* c) {
+    if (!c) return DMX_E_INVALID;
+    if (!c->panel[0].set || (c->mode != DMX_MODE_SINGLE && !c->panel[1].set)) {
+        c->err = "panels not set for this mode";
+        return DMX_E_STATE;
+    }
+    CK(hipSetDevice(c->device));
+    int rc = ensure_pipeline(c);
+    if (rc) return rc;
+    hipStream_t st = c->stream;
+    CK(hipEventRecord(c->ev[8], st));
+    CK(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(uint32_t), st));
+    CK(hipMemsetAsync(c->d_counts, 0, c->n_counts * sizeof(unsigned long long), st));
+    CK(hipMemsetAsync(c->d_winner[0], 0xFF, c->n_reads * sizeof(unsigned long long), st));
+    if ((rc = launch_round(c, 0, st))) return rc;
+    if ((rc = launch_finalize(c, 0, st))) return rc;
+    if (c->mode == DMX_MODE_TWO_ROUND) {
+        CK(hipMemsetAsync(c->d_winner[1], 0xFF, c->n_reads * sizeof(unsigned long long), st));
+        if ((rc = launch_round(c, 1, st))) return rc;
+        if ((rc = launch_finalize(c, 1, st))) return rc;
+    }
+    c->executed = true;
+    return DMX_OK;
+}
+
+int dmx_sync(dmx_ctx* c) {
+    if (!c) return DMX_E_INVALID;
+    CK(hipStreamSynchronize(c->stream));
+    return DMX_OK;
+}
+
+int dmx_fetch(dmx_ctx* c, dmx_result* out) {
+    if (!c || (!out && c->n_reads)) return DMX_E_INVALID;
+    if (!c->executed) {
+        c->err = "dmx_fetch before dmx_exec";
+        return DMX_E_STATE;
+    }
+    CK(hipSetDevice(c->device));
+    if (c->n_reads)
+        CK(hipMemcpyAsync(out, c->d_res, c->n_reads * sizeof(dmx_result), hipMemcpyDeviceToHost,
+                          c->stream));
+    CK(hipStreamSynchronize(c->stream));
+    return DMX_OK;
+}
+
+int dmx_counts(dmx_ctx* c, uint64_t* out, size_t n_out) {
+    if (!c || !out) return DMX_E_INVALID;
+    if (!c->executed) {
+        c->err = "dmx_counts before dmx_exec";
+        return DMX_E_STATE;
+    }
+    if (n_out < c->n_counts) {
+        c->err = "counts buffer too small";
+        return DMX_E_INVALID;
+    }
+    CK(hipSetDevice(c->device));
+    CK(hipMemcpyAsync(out, c->d_counts, c->n_counts * 8, hipMemcpyDeviceToHost, c->stream));
+    CK(hipStreamSynchronize(c->stream));
+    return (int)c->n_counts;
+}
+
+int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* clusters, int* flags) {
+    if (!c) return DMX_E_INVALID;
+    if (!c->executed) {
+        c->err = "dmx_stats before dmx_exec";
+        return DMX_E_STATE;
+    }
+    CK(hipSetDevice(c->device));
+    CK(hipStreamSynchronize(c->stream));
+    const int rounds = c->mode == DMX_MODE_SINGLE ? 1 : 2;
+    float t[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < rounds; ++r) {
+        hipEventElapsedTime(&t[3 * r + 0], c->ev[3 * r + 0], c->ev[3 * r + 1]);
+        hipEventElapsedTime(&t[3 * r + 1], c->ev[3 * r + 1], c->ev[3 * r + 2]);
+        hipEventElapsedTime(&t[3 * r + 2], c->ev[3 * r + 2], c->ev[6 + r]);
+    }
+    hipEventElapsedTime(&t[6], c->ev[8], c->ev[6 + rounds - 1]);
+    for (int i = 0; i < n_stage && i < 7; ++i) stage_ms[i] = t[i];
+    uint32_t cnt[4];
+    CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
+    if (clusters) {
+        clusters[0] = cnt[0];
+        clusters[1] = cnt[1];
+    }
+    if (flags) {
+        int f = (int)cnt[3];
+        if (cnt[0] > c->cl_cap || cnt[1] > c->cl_cap) f |= 1;
+        *flags = f;
+    }
+    return DMX_OK;
+}
+
+int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
+            const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out) {
+    int rc = dmx_load(c, seq2b, nmask, offsets, lens, n_words, n_reads);
+    if (rc) return rc;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        if ((rc = dmx_exec(c))) return rc;
+        uint64_t cl[2];
+        int flags = 0;
+        float ms[7];
+        if ((rc = dmx_stats(c, ms, 7, cl, &flags))) return rc;
+        if (flags & 2) {
+            c->err = "internal: traceback left the exact window (please report)";
+            return DMX_E_STATE;
+        }
+        if (!(flags & 1)) return dmx_fetch(c, out);
+        if ((rc = grow_clusters(c))) return rc;   // candidate overflow: retry, never truncate
+    }
+    c->err = "candidate cluster buffer overflow";
+    return DMX_E_NOMEM;
+}
+
+}  // extern "C"

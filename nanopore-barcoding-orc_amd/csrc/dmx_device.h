@@ -1,0 +1,151 @@
+// dmx_device.h — device-side data layout and primitives of the demultiplexer (gfx950 / CDNA4).
+//
+// What the kernels compute is cutadapt 4.9's Aligner.locate (upstream cutadapt/_align.pyx;
+// restated in oracle/cutadapt_oracle.c) for every (read, adapter, orientation) of a round, then
+// AdapterCutter.best_match + ReverseComplementer selection.  Reference call sites:
+// scripts/02_cutadapt_loop.sh:64-72 (round 1, -g file:SP5 --rc), :91-103 (round 2, -a file:SP27rc
+// --rc); scripts/04_cleaning_primers.sh:371-388 (linked primers).
+//
+// Algorithm:
+//   scan    — one lane per (read, orientation, adapter) runs a Myers/Hyyro bit-vector over the
+//             whole read: one 64-bit word per adapter (m <= 64), giving the exact unit-cost DP
+//             last-row cost D(m, j) of every column.  Columns with D <= k form candidate
+//             clusters (plus the final column for 3' adapters).
+//   resolve — one lane per cluster re-runs Myers from column j1-m-k-1 (restricted start; exact
+//             for every cell of cost <= k, proof in DESIGN.md), keeps the last 128 columns of
+//             (Pv, Mv) in LDS, and walks cutadapt's tie-broken pointer chain back from each
+//             candidate cell to recover (origin, score) exactly; keeps cutadapt's best cell.
+//   select/finalize — 64-bit packed keys make "best over adapters and orientations" one
+//             atomicMin per read.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dmx {
+
+constexpr int kMaxAdapters = 64;
+constexpr int kMaxLen = 64;       // adapter length limit: one 64-bit Myers word
+constexpr int kRing = 128;        // resolve ring (must be >= m + k + 2)
+constexpr int kScanBlock = 256;
+constexpr int kResolveBlock = 64;
+
+enum : uint8_t { kFront = 1, kBack = 2 };
+
+// One adapter of a panel as the kernels see it.
+struct DevAdapter {
+    uint64_t peq[8];    // match bit-vectors per read code: 0..3 = A,C,G,T; 4..7 = non-ACGT (0)
+    int8_t acc[72];     // acc[L]: max accepted cost for an alignment covering L adapter chars,
+                        // -1 if never (L < min_overlap).  Precomputed on the host in IEEE double
+                        // exactly as `cost <= effective_length * max_error_rate` (_align.pyx).
+    uint8_t m;          // adapter length
+    uint8_t k;          // int(max_error_rate * m): band used to size the resolve window
+    uint8_t where;      // kFront / kBack
+    int8_t kk;          // max_L acc[L]: no cell with a larger cost can ever be accepted
+    uint8_t pad[4];
+};
+static_assert(sizeof(DevAdapter) == 144, "DevAdapter layout");
+
+struct DevPanel {
+    int32_t n_adapters;
+    int32_t n_orient;    // 2 with --rc, else 1
+    int32_t pad[2];
+    DevAdapter ad[kMaxAdapters];
+};
+
+// A view of a read: strand 0 = the read as given, strand 1 = its reverse complement; the view
+// is positions [start, start+len) of that strand.
+struct ItemView {
+    uint32_t read;
+    uint32_t start;
+    uint32_t len;
+    uint8_t strand;
+    uint8_t pad;
+    int16_t only_adapter;   // linked mode: the pair index, else -1
+};
+
+struct Cluster {      // candidate columns [j1, j2] of one task (item, orientation, adapter)
+    uint32_t item;
+    uint16_t sub;     // o * A + a (or a in linked mode)
+    uint8_t lastcol;  // 3' adapter: final column holds cells with cost <= k
+    uint8_t pad;
+    uint32_t j1, j2;
+};
+
+struct Outcome {      // best cell found by the resolve lane of a cluster
+    uint64_t key;     // ~0 = none
+    int32_t origin;
+    int32_t pad;
+};
+
+// 64-bit ordering key, smaller = better, matching cutadapt's selection order:
+//   score desc (Aligner.locate / best_match / ReverseComplementer), forward before RC on equal
+//   score, fewer errors, earlier adapter (file order), earlier cell in locate's scan order.
+__host__ __device__ inline uint64_t make_key(int score, int o, int cost, int a, uint64_t t) {
+    return ((uint64_t)(127 - score) << 57) | ((uint64_t)o << 56) | ((uint64_t)cost << 49) |
+           ((uint64_t)a << 41) | (t & ((1ull << 41) - 1));
+}
+__host__ __device__ inline int key_score(uint64_t k) { return 127 - (int)(k >> 57); }
+__host__ __device__ inline int key_orient(uint64_t k) { return (int)((k >> 56) & 1); }
+__host__ __device__ inline int key_cost(uint64_t k) { return (int)((k >> 49) & 127); }
+__host__ __device__ inline int key_adapter(uint64_t k) { return (int)((k >> 41) & 255); }
+__host__ __device__ inline uint64_t key_t(uint64_t k) { return k & ((1ull << 41) - 1); }
+
+// ---------------------------------------------------------------------------------------------
+// Packed read streams.  seq: 2 bits per nt (16 nt / u32, nt x at bits 2(x%16)); nmask: 1 bit per
+// nt (1 = not ACGT, never matches).  Buffers carry DMX_PACK_PAD (64) nt of padding on both ends
+// so a 32-bit window starting up to 16 nt before a read or ending past it stays in bounds.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t window32(const uint32_t* __restrict__ w, uint64_t bitpos) {
+    const uint64_t q = bitpos >> 5;
+    const uint32_t sh = (uint32_t)bitpos & 31u;
+    const uint64_t v = ((uint64_t)w[q + 1] << 32) | (uint64_t)w[q];
+    return (uint32_t)(v >> sh);
+}
+
+// Reverse the order of the 16 2-bit fields of w.
+__device__ __forceinline__ uint32_t rev_pairs(uint32_t w) {
+    const uint32_t v = __brev(w);
+    return ((v >> 1) & 0x55555555u) | ((v << 1) & 0xAAAAAAAAu);
+}
+
+// 16 consecutive view positions starting at view position p: 2-bit codes (complemented on the
+// reverse strand) and the no-match bits.  `off`/`n`: the read's first nt and length; view
+// (strand, start).
+__device__ __forceinline__ void fetch16(const uint32_t* __restrict__ seq,
+                                        const uint32_t* __restrict__ nmask, uint64_t off,
+                                        uint32_t n, uint32_t strand, uint32_t start, uint32_t p,
+                                        uint32_t& codes, uint32_t& nbits) {
+    if (strand == 0) {
+        const uint64_t g = off + start + p;
+        codes = window32(seq, 2 * g);
+        nbits = window32(nmask, g) & 0xFFFFu;
+    } else {
+        const uint64_t b = off + (uint64_t)n - 1 - start - p - 15;   // lowest nt of the window
+        codes = ~rev_pairs(window32(seq, 2 * b));                    // complement = 3 - c
+        nbits = __brev(window32(nmask, b)) >> 16;
+    }
+}
+
+// One Myers/Hyyro column step for semi-global matching with a free start in the read
+// (D(0, j) = 0 for all j, so the row-0 horizontal delta shifted in is 0).
+// Bit i-1 of Pv/Mv: vertical delta D(i, j) - D(i-1, j) is +1 / -1.
+__device__ __forceinline__ void myers_step(uint64_t eq, uint64_t& pv, uint64_t& mv, int& d,
+                                           uint32_t hbit) {
+    const uint64_t xv = eq | mv;
+    const uint64_t xh = (((eq & pv) + pv) ^ pv) | eq;
+    uint64_t ph = mv | ~(xh | pv);
+    uint64_t mh = pv & xh;
+    d += (int)((ph >> hbit) & 1u) - (int)((mh >> hbit) & 1u);
+    ph <<= 1;
+    mh <<= 1;
+    pv = mh | ~(xv | ph);
+    mv = ph & xv;
+}
+
+// D(i, j) from column j's vertical-delta vectors (row 0 is 0).
+__device__ __forceinline__ int col_cost(uint64_t pv, uint64_t mv, int i) {
+    const uint64_t mask = i >= 64 ? ~0ull : ((1ull << i) - 1ull);
+    return __popcll(pv & mask) - __popcll(mv & mask);
+}
+
+}  // namespace dmx

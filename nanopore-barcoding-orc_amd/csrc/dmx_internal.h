@@ -1,0 +1,56 @@
+// dmx_internal.h — host-side context of libdmx (not part of the public ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/dmx.h"
+#include "dmx_device.h"
+
+namespace dmx {
+
+struct HostPanel {
+    int n = 0;
+    int n_orient = 1;
+    bool set = false;
+    DevAdapter ad[kMaxAdapters];
+};
+
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int mode = DMX_MODE_SINGLE;
+    HostPanel panel[2];
+    DevPanel* d_panel[2] = {nullptr, nullptr};
+
+    // resident batch
+    size_t n_reads = 0, n_words = 0;
+    size_t cap_reads = 0, cap_words = 0;
+    uint32_t* d_seq = nullptr;
+    uint32_t* d_nmask = nullptr;
+    uint64_t* d_offs = nullptr;
+    uint32_t* d_lens = nullptr;
+
+    // pipeline state
+    dmx_result* d_res = nullptr;
+    unsigned long long* d_winner[2] = {nullptr, nullptr};
+    int32_t* d_origin[2] = {nullptr, nullptr};
+    size_t slot_cap = 0;
+    Cluster* d_cl[2] = {nullptr, nullptr};
+    Outcome* d_outc[2] = {nullptr, nullptr};
+    size_t cl_cap = 0;
+    ItemView* d_items = nullptr;
+    size_t item_cap = 0;
+    uint32_t* d_counters = nullptr;   // [0..1] clusters per round, [2] items, [3] flags
+    unsigned long long* d_counts = nullptr;
+    size_t n_counts = 0;
+    hipEvent_t ev[9] = {};
+    bool executed = false;
+};
+
+int launch_round(Ctx* c, int round, hipStream_t st);
+int launch_finalize(Ctx* c, int round, hipStream_t st);
+
+}  // namespace dmx

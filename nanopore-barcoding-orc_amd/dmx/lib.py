@@ -1,0 +1,196 @@
+"""ctypes binding of libdmx.so (the C-ABI declared in include/dmx.h).
+
+The product path has exactly one compute backend: the HIP kernels in libdmx.so.  If the
+library is missing or no GPU is visible, the calls raise — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdmx.so")
+
+DMX_FRONT, DMX_BACK, DMX_RC = 0x01, 0x02, 0x10
+MODE_SINGLE, MODE_TWO_ROUND, MODE_LINKED = 0, 1, 2
+PACK_PAD = 64
+
+MATCH_FIELDS = [("rstart", "<i4"), ("rstop", "<i4"), ("astart", "<i2"), ("astop", "<i2"),
+                ("score", "<i2"), ("errors", "<i2")]
+RESULT_DTYPE = np.dtype([("bin1", "<i2"), ("bin2", "<i2"), ("rc1", "u1"), ("rc2", "u1"),
+                         ("flags", "u1"), ("pad", "u1")]
+                        + [("m1_" + n, t) for n, t in MATCH_FIELDS]
+                        + [("m2_" + n, t) for n, t in MATCH_FIELDS])
+assert RESULT_DTYPE.itemsize == 40
+
+EXPORTS = ["dmx_abi_version", "dmx_open", "dmx_close", "dmx_last_error", "dmx_set_panel",
+           "dmx_set_mode", "dmx_pack_words", "dmx_pack", "dmx_run", "dmx_load", "dmx_exec",
+           "dmx_sync", "dmx_fetch", "dmx_counts", "dmx_stats"]
+
+
+class DmxError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libdmx.so (built by `make -C nanopore-barcoding-orc_amd`); raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DmxError(f"{LIB_PATH} not built: run `make -C nanopore-barcoding-orc_amd` "
+                       "(the HIP extension is required; there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, c_int, c_size, c_u64p = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
+    L.dmx_abi_version.restype = c_int
+    L.dmx_open.argtypes = [c_int, ctypes.POINTER(P)]
+    L.dmx_close.argtypes = [P]
+    L.dmx_close.restype = None
+    L.dmx_last_error.argtypes = [P]
+    L.dmx_last_error.restype = ctypes.c_char_p
+    L.dmx_set_panel.argtypes = [P, c_int, ctypes.POINTER(ctypes.c_char_p),
+                                ctypes.POINTER(c_int), c_int, ctypes.c_double, c_int, c_int]
+    L.dmx_set_mode.argtypes = [P, c_int]
+    L.dmx_pack_words.argtypes = [ctypes.c_uint64, c_size]
+    L.dmx_pack_words.restype = c_size
+    L.dmx_pack.argtypes = [P, c_u64p, P, c_size, P, P, c_u64p]
+    L.dmx_run.argtypes = [P, P, P, c_u64p, P, c_size, c_size, P]
+    L.dmx_load.argtypes = [P, P, P, c_u64p, P, c_size, c_size]
+    L.dmx_exec.argtypes = [P]
+    L.dmx_sync.argtypes = [P]
+    L.dmx_fetch.argtypes = [P, P]
+    L.dmx_counts.argtypes = [P, c_u64p, c_size]
+    L.dmx_stats.argtypes = [P, ctypes.POINTER(ctypes.c_float), c_int, c_u64p,
+                            ctypes.POINTER(c_int)]
+    if L.dmx_abi_version() != 1:
+        raise DmxError("libdmx ABI mismatch")
+    _lib = L
+    return L
+
+
+class Packed:
+    """A batch of reads in the device layout: 2-bit codes + no-match mask (see include/dmx.h)."""
+
+    def __init__(self, seq2b: np.ndarray, nmask: np.ndarray, offsets: np.ndarray,
+                 lengths: np.ndarray):
+        self.seq2b, self.nmask, self.offsets, self.lengths = seq2b, nmask, offsets, lengths
+
+    @property
+    def n_reads(self) -> int:
+        return int(len(self.lengths))
+
+    @property
+    def n_words(self) -> int:
+        return int(len(self.seq2b))
+
+
+def pack(ascii_blob: np.ndarray, offsets: np.ndarray, lengths: np.ndarray) -> Packed:
+    """Pack ASCII reads (uint8 blob + per-read offset/length) with the library's host packer."""
+    L = load()
+    blob = np.ascontiguousarray(ascii_blob, dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(lengths, dtype=np.uint32)
+    n = len(lens)
+    words = L.dmx_pack_words(int(lens.sum(dtype=np.uint64)), n)
+    seq = np.empty(words, dtype=np.uint32)
+    nm = np.empty(words, dtype=np.uint32)
+    out_offs = np.empty(n, dtype=np.uint64)
+    rc = L.dmx_pack(blob.ctypes.data if len(blob) else None, offs.ctypes.data, lens.ctypes.data,
+                    n, seq.ctypes.data, nm.ctypes.data, out_offs.ctypes.data)
+    if rc != 0:
+        raise DmxError(f"dmx_pack failed ({rc})")
+    return Packed(seq, nm, out_offs, lens)
+
+
+class Context:
+    """One device context (include/dmx.h: one per GPU, one host thread per context)."""
+
+    def __init__(self, device: int = 0):
+        self._L = load()
+        h = ctypes.c_void_p()
+        rc = self._L.dmx_open(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise DmxError(f"dmx_open(device={device}) failed ({rc}): no usable HIP device")
+        self._h = h
+        self.device = device
+        self.panel_sizes = [0, 0]
+        self.mode = MODE_SINGLE
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.dmx_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int, what: str) -> int:
+        if rc < 0:
+            msg = self._L.dmx_last_error(self._h)
+            raise DmxError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+        return rc
+
+    def set_panel(self, rnd: int, seqs, flags: int, max_errors: float = 0.1,
+                  min_overlap: int = 3):
+        arr = (ctypes.c_char_p * len(seqs))(*[s.encode("ascii") for s in seqs])
+        lens = (ctypes.c_int * len(seqs))(*[len(s) for s in seqs])
+        self._check(self._L.dmx_set_panel(self._h, rnd, arr, lens, len(seqs), float(max_errors),
+                                          int(min_overlap), int(flags)), "dmx_set_panel")
+        self.panel_sizes[rnd] = len(seqs)
+
+    def set_mode(self, mode: int):
+        self._check(self._L.dmx_set_mode(self._h, mode), "dmx_set_mode")
+        self.mode = mode
+
+    def run(self, p: Packed) -> np.ndarray:
+        out = np.zeros(p.n_reads, dtype=RESULT_DTYPE)
+        self._check(self._L.dmx_run(self._h, p.seq2b.ctypes.data, p.nmask.ctypes.data,
+                                    p.offsets.ctypes.data, p.lengths.ctypes.data, p.n_words,
+                                    p.n_reads, out.ctypes.data), "dmx_run")
+        return out
+
+    def load(self, p: Packed):
+        self._check(self._L.dmx_load(self._h, p.seq2b.ctypes.data, p.nmask.ctypes.data,
+                                     p.offsets.ctypes.data, p.lengths.ctypes.data, p.n_words,
+                                     p.n_reads), "dmx_load")
+        self._n_loaded = p.n_reads
+
+    def exec(self):
+        self._check(self._L.dmx_exec(self._h), "dmx_exec")
+
+    def sync(self):
+        self._check(self._L.dmx_sync(self._h), "dmx_sync")
+
+    def fetch(self) -> np.ndarray:
+        out = np.zeros(self._n_loaded, dtype=RESULT_DTYPE)
+        self._check(self._L.dmx_fetch(self._h, out.ctypes.data), "dmx_fetch")
+        return out
+
+    def n_counts(self) -> int:
+        a1 = 0 if self.mode == MODE_SINGLE else self.panel_sizes[1]
+        return (self.panel_sizes[0] + 1) * (a1 + 1) + 2
+
+    def counts(self) -> np.ndarray:
+        out = np.zeros(self.n_counts(), dtype=np.uint64)
+        self._check(self._L.dmx_counts(self._h, out.ctypes.data, len(out)), "dmx_counts")
+        return out
+
+    def stats(self):
+        ms = (ctypes.c_float * 7)()
+        cl = np.zeros(2, dtype=np.uint64)
+        fl = ctypes.c_int()
+        self._check(self._L.dmx_stats(self._h, ms, 7, cl.ctypes.data, ctypes.byref(fl)),
+                    "dmx_stats")
+        names = ["scan0", "resolve0", "finalize0", "scan1", "resolve1", "finalize1", "total"]
+        return {"ms": dict(zip(names, list(ms))), "clusters": cl.tolist(), "flags": fl.value}

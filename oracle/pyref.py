@@ -1,0 +1,137 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (pure-Python, small cases).
+
+A second, independent CPU restatement of cutadapt 4.9's ``Aligner.locate`` semantics
+(upstream ``cutadapt/_align.pyx``; call sites in the reference:
+``scripts/02_cutadapt_loop.sh:64-72,91-103``, ``scripts/04_cleaning_primers.sh:371-388``).
+
+Unlike ``cutadapt_oracle.c`` (a literal one-column DP with Ukkonen's cut-off and its stale
+cells), this keeps the FULL (m+1) x (n+1) matrix and evaluates every cell, then scans the
+candidates in cutadapt's order.  Agreement of the two formulations is the evidence that the
+cut-off never changes an accepted result ("Why a full-column scan is exact").
+
+PARITY UNPINNED: the reference holds no fixtures for this path.
+Only for small inputs (pure Python loops).
+"""
+from __future__ import annotations
+
+REF_START, QUERY_START, REF_END, QUERY_STOP = 1, 2, 4, 8
+FRONT = QUERY_START | QUERY_STOP | REF_START
+BACK = QUERY_START | QUERY_STOP | REF_END
+
+_IUPAC = {"A": 1, "C": 2, "G": 4, "T": 8, "U": 8, "R": 5, "Y": 10, "S": 6, "W": 9, "K": 12,
+          "M": 3, "B": 14, "D": 13, "H": 11, "V": 7, "N": 15}
+_COMP = str.maketrans("ACGTUMRWSYKVHDBNacgtumrwsykvhdbn", "TGCAAKYWSRMBDHVNtgcaakywsrmbdhvn")
+
+
+def revcomp(s: str) -> str:
+    return s.translate(_COMP)[::-1]
+
+
+def _acgt(c: str) -> int:
+    v = _IUPAC.get(c.upper(), 0)
+    return v if v in (1, 2, 4, 8) else 0
+
+
+def locate(ref: str, query: str, max_error_rate: float, flags: int, min_overlap: int = 3):
+    """Full-matrix restatement. Returns (ref_start, ref_stop, q_start, q_stop, score, errors)."""
+    m, n = len(ref), len(query)
+    wildcard_ref = not set(ref) <= set("ACGT")
+    if wildcard_ref:
+        r = [_IUPAC.get(c, 0) for c in ref]
+        q = [_acgt(c) for c in query]
+        eq = lambda a, b: (a & b) != 0  # noqa: E731
+    else:
+        r = list(ref)
+        q = list(query.upper())
+        eq = lambda a, b: a == b  # noqa: E731
+    n_counts = [0] * (m + 1)
+    nc = 0
+    for i in range(m):
+        n_counts[i] = nc
+        nc += ref[i] in "Nn"
+    n_counts[m] = nc
+    eff_len = m - nc if wildcard_ref else m
+    start_ref, start_q = bool(flags & REF_START), bool(flags & QUERY_START)
+    stop_ref, stop_q = bool(flags & REF_END), bool(flags & QUERY_STOP)
+    assert start_q and stop_q, "only FRONT/BACK-style flags are restated here"
+    # cell = (cost, score, origin)
+    C = [[None] * (n + 1) for _ in range(m + 1)]
+    for i in range(m + 1):
+        C[i][0] = (0, 0, -i) if start_ref else (i, -2 * i, 0)
+    for j in range(1, n + 1):
+        C[0][j] = (0, 0, j)
+        for i in range(1, m + 1):
+            d, up, left = C[i - 1][j - 1], C[i - 1][j], C[i][j - 1]
+            if eq(r[i - 1], q[j - 1]):
+                C[i][j] = (d[0], d[1] + 1, d[2])
+            elif d[0] + 1 <= left[0] + 1 and d[0] + 1 <= up[0] + 1:
+                C[i][j] = (d[0] + 1, d[1] - 1, d[2])
+            elif up[0] + 1 <= left[0] + 1:
+                C[i][j] = (up[0] + 1, up[1] - 2, up[2])
+            else:
+                C[i][j] = (left[0] + 1, left[1] - 2, left[2])
+
+    def acceptable(i, cell):
+        length = i + min(cell[2], 0)
+        eff = length
+        if wildcard_ref:
+            eff = length - n_counts[length] if length < m else eff_len
+        return length >= min_overlap and cell[0] <= eff * max_error_rate
+
+    best = None  # (score, cost, origin, ref_stop, q_stop)
+    for j in range(1, n + 1):
+        cell = C[m][j]
+        if acceptable(m, cell) and (best is None or cell[1] > best[0]
+                                    or (cell[1] == best[0] and cell[0] < best[1])):
+            best = (cell[1], cell[0], cell[2], m, j)
+    for i in range(0 if stop_ref else m, m + 1):
+        cell = C[i][n]
+        if acceptable(i, cell) and (best is None or cell[1] > best[0]
+                                    or (cell[1] == best[0] and cell[0] < best[1])):
+            best = (cell[1], cell[0], cell[2], i, n)
+    if best is None:
+        return None
+    score, cost, origin, rstop, qstop = best
+    if origin >= 0:
+        return (0, rstop, origin, qstop, score, cost)
+    return (-origin, rstop, 0, qstop, score, cost)
+
+
+def best_match(adapters, where, seq, e=0.1, min_overlap=3):
+    """modifiers.AdapterCutter.best_match: (index, match) or (-1, None)."""
+    best, bm = -1, None
+    for a, ad in enumerate(adapters):
+        rate = e / len(ad) if e >= 1 else e
+        mt = locate(ad, seq, rate, where[a], min_overlap)
+        if mt is None:
+            continue
+        if bm is None or mt[4] > bm[4] or (mt[4] == bm[4] and mt[5] < bm[5]):
+            best, bm = a, mt
+    return best, bm
+
+
+def demux_round(adapters, where, seq, use_rc=True, e=0.1):
+    """ReverseComplementer: returns (index, is_rc, match, trimmed_seq)."""
+    af, mf = best_match(adapters, where, seq, e)
+    ar, mr = (-1, None)
+    rc = revcomp(seq)
+    if use_rc:
+        ar, mr = best_match(adapters, where, rc, e)
+    fs = mf[4] if mf else 0
+    rs = mr[4] if mr else 0
+    if use_rc and rs > fs:
+        a, mt, src, is_rc = ar, mr, rc, True
+    else:
+        a, mt, src, is_rc = af, mf, seq, False
+    if a < 0:
+        return -1, False, None, seq
+    trimmed = src[mt[3]:] if where[a] == FRONT else src[:mt[2]]
+    return a, is_rc, mt, trimmed
+
+
+def two_round(sp5, sp27, seq, use_rc=True, e=0.1):
+    a, rc1, m1, t1 = demux_round(sp5, [FRONT] * len(sp5), seq, use_rc, e)
+    if a < 0:
+        return (a, rc1, m1, -1, False, None, None)
+    b, rc2, m2, t2 = demux_round(sp27, [BACK] * len(sp27), t1, use_rc, e)
+    return (a, rc1, m1, b, rc2, m2, t2 if b >= 0 else None)
