@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""Benchmark: two-round SP5 x SP27 demultiplexing throughput on MI355X (BASELINE.json metric).
+
+One "step" = the complete two-round demux (round 1: 5' SP5 adapters with --rc; round 2: 3'
+SP27rc adapters with --rc on every round-1-matched read; bins, trim coordinates, per-bin counts)
+of one resident batch of synthetic reads — the work of scripts/02_cutadapt_loop.sh:64-103.
+Workload (default, BASELINE.json configs[1]): 10M synthetic ONT reads per GPU, lognormal
+length mean 1.2 kb, synthetic 24 x 24 M13 panel, -e 0.1, --rc.
+
+Multi-GPU (torchrun): one process per GPU, reads sharded by contiguous range (rank r processes
+reads [r*N, (r+1)*N) of one seeded generation: weak scaling), one RCCL all-reduce of the
+per-bin counts per step (the only exchange the path has).
+
+Prints ONE JSON line on rank 0 (see README "Benchmark contract").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "nanopore-barcoding-orc_amd"))
+
+METRIC = "Mreads/s two-round SP5×SP27 demux; % HBM roofline; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CUs x 4 SIMD32 x 2.4 GHz, 32-bit lane-ops
+
+
+def scan_algorithmic_bytes(lengths: np.ndarray, n_clusters: int) -> float:
+    """Algorithmic HBM bytes of one scan launch over these views: the 2-bit
+    packed read once (L/4 B), its 1-bit no-match mask (L/8 B), offset + length (12 B), plus the
+    16-B candidate-cluster records it writes."""
+    L = lengths.astype(np.float64)
+    return float(np.sum(np.ceil(L / 4) + np.ceil(L / 8) + 12.0) + 16.0 * n_clusters)
+
+
+def cpu_baseline(workload: str, threads: int, target_s: float = 12.0):
+    """Oracle (CPU restatement of cutadapt 4.9, C, pthreads) on a bounded sample of the same
+    workload.  rank 0, N=1 only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: timed CPU baseline only
+    from dmx import synth
+    pilot = synth.generate(workload, n=400 * threads, seed=99)
+    p1 = oracle.Panel(pilot["sp5"], oracle.FRONT)
+    p2 = oracle.Panel(pilot["sp27"], oracle.BACK)
+    t = time.perf_counter()
+    oracle.run_batch(p1, p2, pilot["blob"], pilot["offsets"], pilot["lengths"], 1, True, threads)
+    rate = len(pilot["lengths"]) / (time.perf_counter() - t)
+    n = int(max(1000, min(2_000_000, rate * target_s)))
+    d = synth.generate(workload, n=n, seed=98)
+    t = time.perf_counter()
+    oracle.run_batch(p1, p2, d["blob"], d["offsets"], d["lengths"], 1, True, threads)
+    dt = time.perf_counter() - t
+    return {"value": n / dt / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "port",
+            "sample": f"{n} reads of workload {workload} (seed 98), two rounds, --rc, -e 0.1, "
+                      f"{dt:.1f} s wall on {threads} host threads (oracle/cutadapt_oracle.c, "
+                      "a C restatement of cutadapt 4.9's Ukkonen-banded DP; cutadapt itself is "
+                      "not installed)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="c2x24", choices=["c2x24", "c2", "c4", "c1"])
+    ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")   # RCCL over xGMI
+        dist = tdist
+
+    from dmx import lib, synth
+    gen_threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    t0 = time.perf_counter()
+    d = synth.generate(args.workload, n=args.reads, first=rank * args.reads,
+                       threads=gen_threads)
+    packed = lib.pack(d["blob"], d["offsets"], d["lengths"])
+    lengths = d["lengths"].copy()
+    del d["blob"]
+    gen_s = time.perf_counter() - t0
+
+    ctx = lib.Context(local_rank if world > 1 else 0)
+    ctx.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC, 0.1)
+    ctx.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC, 0.1)
+    ctx.set_mode(lib.MODE_TWO_ROUND)
+    ctx.load(packed)
+    del packed
+
+    def allreduce_counts():
+        c = ctx.counts()
+        if dist is not None:
+            import torch
+            t = torch.from_numpy(c.astype(np.int64)).cuda()
+            dist.all_reduce(t)
+            c = t.cpu().numpy()
+        return c
+
+    def barrier_sync():
+        ctx.sync()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        ctx.exec()
+        ctx.sync()
+        allreduce_counts()
+
+    stage = {k: 0.0 for k in ("scan0", "resolve0", "finalize0", "scan1", "resolve1",
+                              "finalize1", "total")}
+    clusters = np.zeros(2)
+    windows = np.zeros(2)
+    barrier_sync()
+    t = time.perf_counter()
+    counts = None
+    flags = 0
+    for _ in range(args.steps):
+        ctx.exec()
+        ctx.sync()
+        st = ctx.stats()
+        for k in stage:
+            stage[k] += st["ms"][k]
+        clusters += np.array(st["clusters"], dtype=np.float64)
+        windows += np.array(st["windows"], dtype=np.float64)
+        flags |= st["flags"]
+        counts = allreduce_counts()
+    barrier_sync()
+    elapsed = time.perf_counter() - t
+    if flags:
+        raise SystemExit(f"pipeline flags {flags}: cluster overflow or window violation")
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    K = args.steps
+    total_reads = args.reads * world * K
+    value = total_reads / elapsed / 1e6
+    # roofline of the dominant kernel (scan; two launches per step: round 1 and round 2)
+    scan_ms = (stage["scan0"] + stage["scan1"]) / (2 * K)
+    res = ctx.fetch()
+    n2 = int((res["bin1"] >= 0).sum())
+    len2 = (lengths[res["bin1"] >= 0] - res["m1_rstop"][res["bin1"] >= 0]).astype(np.int64)
+    bytes0 = scan_algorithmic_bytes(lengths, int(clusters[0] / K))
+    bytes1 = scan_algorithmic_bytes(len2, int(clusters[1] / K))
+    achieved = (bytes0 + bytes1) / 2 / (scan_ms / 1e3) / 1e9
+    A0, A1 = ctx.panel_sizes
+    steps_r0 = float(lengths.sum()) * A0 * 2
+    steps_r1 = float(len2.sum()) * A1 * 2
+    word_steps_per_s = (steps_r0 + steps_r1) / ((stage["scan0"] + stage["scan1"]) / K / 1e3)
+
+    out = {
+        "metric": METRIC, "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
+        "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic",
+        "config": {"workload": f"{args.workload}: {args.reads} synthetic ONT reads per GPU "
+                               "(SURVEY.md §8d), two-round SP5 x SP27 demux, -e 0.1 --rc, "
+                               "inputs resident in HBM",
+                   "panel": f"{A0}x{A1}", "reads_per_gpu": args.reads,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "kernel": "dmx::scan_kernel", "avg_launch_ms": round(scan_ms, 3),
+                     "note": "integer bit-vector scan is VALU-bound by construction "
+                             "(DESIGN.md §5); see 'valu'"},
+        "valu": {"word_steps_per_s": word_steps_per_s,
+                 "peak_lane_ops_per_s": VALU_PEAK_TOPS * 1e12},
+        "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
+        "clusters_per_step": (clusters / K).tolist(),
+        "filter_windows_per_step": (windows / K).tolist(),
+        "reads_round2_per_gpu": n2,
+        "unknown_round1": int(counts[0]) if counts is not None else None,
+        "gen_s": round(gen_s, 1),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -108,8 +108,9 @@ int dmx_fetch(dmx_ctx* ctx, dmx_result* out);
 int dmx_counts(dmx_ctx* ctx, uint64_t* out_counts, size_t n_out);
 
 /* Diagnostics of the last dmx_exec: per-stage device time in ms measured with HIP events on the
- * context's stream (order: scan0, resolve0, finalize0, scan1, resolve1, finalize1), the number of
- * candidate clusters per round, and overflow / window-violation flags (must be 0). */
+ * context's stream (order: scan0, resolve0, finalize0, scan1, resolve1, finalize1, total), and
+ * counts[4] = {candidate clusters round 0, round 1, filter windows round 0, round 1}, and flags
+ * (bit0 cluster overflow, bit1 window violation, bit2 filter-window overflow; must be 0). */
 int dmx_stats(dmx_ctx* ctx, float* stage_ms, int n_stage, uint64_t* clusters, int* flags);
 
 #ifdef __cplusplus

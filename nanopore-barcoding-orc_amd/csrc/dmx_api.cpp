@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <thread>
@@ -29,6 +30,7 @@ using namespace dmx;
 namespace {
 
 constexpr int kPackAlign = 32;   // every read starts on a 32-nt (one nmask word) boundary
+constexpr int kMinFilterLen = 10; // shortest shared suffix worth a filter pass
 
 uint8_t iupac_mask(char ch) {
     switch (ch) {
@@ -116,6 +118,7 @@ int ensure_pipeline(Ctx* c) {
         for (int r = 0; r < 2; ++r) {
             if ((rc = dev_alloc(c, &c->d_winner[r], s))) return rc;
             if ((rc = dev_alloc(c, &c->d_origin[r], s))) return rc;
+            if ((rc = dev_alloc(c, &c->d_lb[r], s))) return rc;
         }
         if ((rc = dev_alloc(c, &c->d_items, items))) return rc;
         c->slot_cap = s;
@@ -132,6 +135,12 @@ int ensure_pipeline(Ctx* c) {
         }
         c->cl_cap = want_cl;
     }
+    const size_t want_win = 4 * 2 * std::max(slots0, n) + 65536;
+    if (c->win_cap < want_win) {
+        int rc;
+        if ((rc = dev_alloc(c, &c->d_win, want_win))) return rc;
+        c->win_cap = want_win;
+    }
     const size_t a1 = c->mode == DMX_MODE_SINGLE ? 0 : (size_t)c->panel[1].n;
     const size_t nc = ((size_t)c->panel[0].n + 1) * (a1 + 1) + 2;
     if (c->n_counts != nc) {
@@ -139,6 +148,14 @@ int ensure_pipeline(Ctx* c) {
         if ((rc = dev_alloc(c, &c->d_counts, nc))) return rc;
         c->n_counts = nc;
     }
+    return DMX_OK;
+}
+
+int grow_windows(Ctx* c) {
+    const size_t want = c->win_cap * 2;
+    int rc;
+    if ((rc = dev_alloc(c, &c->d_win, want))) return rc;
+    c->win_cap = want;
     return DMX_OK;
 }
 
@@ -169,6 +186,8 @@ int dmx_open(int device, dmx_ctx** out) {
         return DMX_E_HIP;
     dmx_ctx* c = new dmx_ctx();
     c->device = device;
+    const char* nf = std::getenv("DMX_NO_FILTER");
+    c->no_filter = nf && nf[0] == '1';
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -186,8 +205,8 @@ void dmx_close(dmx_ctx* c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_seq,       c->d_nmask,     c->d_offs,     c->d_lens,      c->d_res,
-                    c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_cl[0],
-                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items,     c->d_counters,
+                    c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
+                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_counters,
                     c->d_counts,    c->d_panel[0],  c->d_panel[1]};
     for (void* b : bufs)
         if (b) hipFree(b);
@@ -250,7 +269,8 @@ int dmx_set_panel(dmx_ctx* c, int round, const char* const* seqs, const int* len
         }
         const double rate = max_errors >= 1.0 ? max_errors / (double)m : max_errors;
         const int k = (int)(rate * m);
-        if (m + k + 2 > kRing) {
+        if (m + k + 2 > kRingSmall) hp.ring_small = false;
+        if (m + k + 2 > kRingLarge) {
             c->err = "error rate too high for the resolve window (m + k + 2 > 128)";
             return DMX_E_UNSUPPORTED;
         }
@@ -283,6 +303,7 @@ int dmx_set_panel(dmx_ctx* c, int round, const char* const* seqs, const int* len
             }
             ad.acc[L] = (int8_t)allow;
             kk = std::max(kk, allow);
+            ad.pacc[L] = (int8_t)kk;
         }
         ad.m = (uint8_t)m;
         ad.k = (uint8_t)k;
@@ -290,11 +311,44 @@ int dmx_set_panel(dmx_ctx* c, int round, const char* const* seqs, const int* len
         ad.where = (flags & DMX_FRONT) ? kFront : kBack;
     }
     hp.set = true;
-    c->panel[round] = hp;
     DevPanel dp;
     memset(&dp, 0, sizeof(dp));
     dp.n_adapters = hp.n;
     dp.n_orient = hp.n_orient;
+    dp.where = hp.ad[0].where;
+    // Shared-suffix filter block: the longest suffix common to every adapter (<= 32 chars).
+    int common = lens[0];
+    for (int a = 1; a < n; ++a) {
+        int l = 0;
+        while (l < common && l < lens[a] &&
+               seqs[a][lens[a] - 1 - l] == seqs[0][lens[0] - 1 - l])
+            ++l;
+        common = l;
+    }
+    const int flen = std::min(common, 32);
+    bool uniform = true;
+    for (int a = 1; a < n; ++a) uniform &= hp.ad[a].where == hp.ad[0].where;
+    hp.filter = uniform && flen >= kMinFilterLen && !(c->no_filter);
+    if (hp.filter) {
+        dp.filter_len = flen;
+        const char* blk = seqs[0] + lens[0] - flen;
+        for (int i = 0; i < flen; ++i) {
+            const uint8_t mask = iupac_mask(blk[i]);
+            for (int code = 0; code < 4; ++code)
+                if (mask & (1u << code)) dp.filter_peq[code] |= 1u << i;
+        }
+        int kf = -1, mk = 0;
+        for (int L = 0; L < 72; ++L) dp.pf[L] = -1;
+        for (int a = 0; a < n; ++a) {
+            kf = std::max(kf, (int)hp.ad[a].kk);
+            mk = std::max(mk, (int)hp.ad[a].m + (int)hp.ad[a].k + 1);
+            for (int L = 0; L < 72; ++L) dp.pf[L] = std::max(dp.pf[L], hp.ad[a].pacc[L]);
+        }
+        dp.kf = kf;
+        dp.max_mk = mk;
+    }
+    c->panel[round] = hp;
+    c->ring_small[round] = hp.ring_small;
     for (int a = 0; a < n; ++a) dp.ad[a] = hp.ad[a];
     CK(hipSetDevice(c->device));
     CK(hipMemcpy(c->d_panel[round], &dp, sizeof(dp), hipMemcpyHostToDevice));
@@ -454,15 +508,18 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* clusters, int*
     }
     hipEventElapsedTime(&t[6], c->ev[8], c->ev[6 + rounds - 1]);
     for (int i = 0; i < n_stage && i < 7; ++i) stage_ms[i] = t[i];
-    uint32_t cnt[4];
+    uint32_t cnt[6];
     CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
     if (clusters) {
         clusters[0] = cnt[0];
         clusters[1] = cnt[1];
+        clusters[2] = cnt[4];
+        clusters[3] = cnt[5];
     }
     if (flags) {
         int f = (int)cnt[3];
         if (cnt[0] > c->cl_cap || cnt[1] > c->cl_cap) f |= 1;
+        if (cnt[4] > c->win_cap || cnt[5] > c->win_cap) f |= 4;
         *flags = f;
     }
     return DMX_OK;
@@ -474,7 +531,7 @@ int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint
     if (rc) return rc;
     for (int attempt = 0; attempt < 8; ++attempt) {
         if ((rc = dmx_exec(c))) return rc;
-        uint64_t cl[2];
+        uint64_t cl[4];
         int flags = 0;
         float ms[7];
         if ((rc = dmx_stats(c, ms, 7, cl, &flags))) return rc;
@@ -482,8 +539,10 @@ int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint
             c->err = "internal: traceback left the exact window (please report)";
             return DMX_E_STATE;
         }
-        if (!(flags & 1)) return dmx_fetch(c, out);
-        if ((rc = grow_clusters(c))) return rc;   // candidate overflow: retry, never truncate
+        if (!(flags & 5)) return dmx_fetch(c, out);
+        // candidate overflow: retry with more room, never truncate
+        if ((flags & 1) && (rc = grow_clusters(c))) return rc;
+        if ((flags & 4) && (rc = grow_windows(c))) return rc;
     }
     c->err = "candidate cluster buffer overflow";
     return DMX_E_NOMEM;

@@ -25,7 +25,8 @@ namespace dmx {
 
 constexpr int kMaxAdapters = 64;
 constexpr int kMaxLen = 64;       // adapter length limit: one 64-bit Myers word
-constexpr int kRing = 128;        // resolve ring (must be >= m + k + 2)
+constexpr int kRingSmall = 68;    // resolve ring when every adapter has m + k + 2 <= 68
+constexpr int kRingLarge = 128;   // otherwise (one 64-lane block per CU)
 constexpr int kScanBlock = 256;
 constexpr int kResolveBlock = 64;
 
@@ -37,19 +38,40 @@ struct DevAdapter {
     int8_t acc[72];     // acc[L]: max accepted cost for an alignment covering L adapter chars,
                         // -1 if never (L < min_overlap).  Precomputed on the host in IEEE double
                         // exactly as `cost <= effective_length * max_error_rate` (_align.pyx).
+    int8_t pacc[72];    // prefix maximum of acc: a last-row cell (m, j) of cost d can only be
+                        // accepted if d <= pacc[min(m, j + d)] (its aligned adapter length is
+                        // at most min(m, j + d)); prunes the always-cheap cells near column 0.
     uint8_t m;          // adapter length
     uint8_t k;          // int(max_error_rate * m): band used to size the resolve window
     uint8_t where;      // kFront / kBack
     int8_t kk;          // max_L acc[L]: no cell with a larger cost can ever be accepted
     uint8_t pad[4];
 };
-static_assert(sizeof(DevAdapter) == 144, "DevAdapter layout");
+static_assert(sizeof(DevAdapter) == 216, "DevAdapter layout");
 
 struct DevPanel {
     int32_t n_adapters;
     int32_t n_orient;    // 2 with --rc, else 1
-    int32_t pad[2];
+    int32_t where;       // kFront / kBack when uniform, else 0
+    // Shared-suffix filter (0 = disabled): the last `filter_len` (<= 32) characters are common
+    // to every adapter of the panel, so any acceptable last-row cell (m, j) of any adapter has a
+    // block cost b(j) <= its own cost.  One 32-bit Myers scan per read view
+    // finds all columns where some adapter may end; per-adapter scans run only there.
+    int32_t filter_len;
+    int32_t kf;          // max over adapters of kk
+    int32_t max_mk;      // max over adapters of m + k + 1
+    uint32_t filter_peq[8];
+    int8_t pf[72];       // max over adapters of pacc[L]
     DevAdapter ad[kMaxAdapters];
+};
+
+// A column range of one (item, orientation) that the per-adapter window scan must cover.
+struct Window {
+    uint32_t item;
+    uint8_t o;
+    uint8_t lastcol;     // 3' panel: window ends at the final column (last-column cells)
+    uint16_t pad;
+    uint32_t j1, j2;     // candidate end columns [j1, j2]
 };
 
 // A view of a read: strand 0 = the read as given, strand 1 = its reverse complement; the view
@@ -67,7 +89,7 @@ struct Cluster {      // candidate columns [j1, j2] of one task (item, orientati
     uint32_t item;
     uint16_t sub;     // o * A + a (or a in linked mode)
     uint8_t lastcol;  // 3' adapter: final column holds cells with cost <= k
-    uint8_t pad;
+    int8_t ub;        // upper bound of the score of any cell of the cluster
     uint32_t j1, j2;
 };
 
@@ -135,6 +157,20 @@ __device__ __forceinline__ void myers_step(uint64_t eq, uint64_t& pv, uint64_t& 
     const uint64_t xh = (((eq & pv) + pv) ^ pv) | eq;
     uint64_t ph = mv | ~(xh | pv);
     uint64_t mh = pv & xh;
+    d += (int)((ph >> hbit) & 1u) - (int)((mh >> hbit) & 1u);
+    ph <<= 1;
+    mh <<= 1;
+    pv = mh | ~(xv | ph);
+    mv = ph & xv;
+}
+
+// 32-bit variant for the shared-suffix filter block.
+__device__ __forceinline__ void myers_step32(uint32_t eq, uint32_t& pv, uint32_t& mv, int& d,
+                                             uint32_t hbit) {
+    const uint32_t xv = eq | mv;
+    const uint32_t xh = (((eq & pv) + pv) ^ pv) | eq;
+    uint32_t ph = mv | ~(xh | pv);
+    uint32_t mh = pv & xh;
     d += (int)((ph >> hbit) & 1u) - (int)((mh >> hbit) & 1u);
     ph <<= 1;
     mh <<= 1;

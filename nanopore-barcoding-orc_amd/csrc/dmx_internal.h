@@ -14,6 +14,8 @@ struct HostPanel {
     int n = 0;
     int n_orient = 1;
     bool set = false;
+    bool ring_small = true;
+    bool filter = false;
     DevAdapter ad[kMaxAdapters];
 };
 
@@ -22,6 +24,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     std::string err;
     int mode = DMX_MODE_SINGLE;
+    bool no_filter = false;   // DMX_NO_FILTER=1: always full scans (A/B testing)
     HostPanel panel[2];
     DevPanel* d_panel[2] = {nullptr, nullptr};
 
@@ -37,13 +40,17 @@ struct Ctx {
     dmx_result* d_res = nullptr;
     unsigned long long* d_winner[2] = {nullptr, nullptr};
     int32_t* d_origin[2] = {nullptr, nullptr};
+    int32_t* d_lb[2] = {nullptr, nullptr};
+    bool ring_small[2] = {true, true};
     size_t slot_cap = 0;
     Cluster* d_cl[2] = {nullptr, nullptr};
     Outcome* d_outc[2] = {nullptr, nullptr};
     size_t cl_cap = 0;
+    Window* d_win = nullptr;
+    size_t win_cap = 0;
     ItemView* d_items = nullptr;
     size_t item_cap = 0;
-    uint32_t* d_counters = nullptr;   // [0..1] clusters per round, [2] items, [3] flags
+    uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows
     unsigned long long* d_counts = nullptr;
     size_t n_counts = 0;
     hipEvent_t ev[9] = {};

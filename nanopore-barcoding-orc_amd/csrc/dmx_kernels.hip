@@ -32,6 +32,10 @@ struct RoundArgs {
     uint32_t* flags;             // bit0 cluster overflow, bit1 window violation
     unsigned long long* winner;  // per slot, ~0 = none
     int32_t* origin;             // per slot
+    int32_t* lb;                 // per slot: lower bound of the best accepted score (0 = none)
+    Window* win;
+    uint32_t* win_count;
+    uint32_t win_cap;
 };
 
 struct TaskView {
@@ -80,27 +84,40 @@ __device__ __forceinline__ uint32_t slot_of(const RoundArgs& R, uint32_t item, i
     return R.per_task_slot ? item * (uint32_t)R.T + (uint32_t)sub : item;
 }
 
-__device__ __forceinline__ void load_panel_lds(const DevPanel* P, uint64_t* s_peq, int8_t* s_acc) {
+__device__ __forceinline__ void load_panel_lds(const DevPanel* P, uint64_t* s_peq, int8_t* s_acc,
+                                               int8_t* s_pacc) {
     const int A = P->n_adapters;
     for (int x = threadIdx.x; x < 8 * A; x += blockDim.x) {
         const int c = x / A, a = x % A;
         s_peq[x] = P->ad[a].peq[c];   // code-major: lanes of one read hit consecutive words
     }
-    for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
+    for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) {
+        s_acc[x] = P->ad[x / 72].acc[x % 72];
+        s_pacc[x] = P->ad[x / 72].pacc[x % 72];
+    }
+}
+
+// Can last-row cell (m, j) with cost d be accepted at all? (aligned adapter length <= j + d)
+__device__ __forceinline__ bool row_candidate(const int8_t* pacc, int m, uint32_t j, int d) {
+    const uint32_t L = min((uint32_t)m, j + (uint32_t)d);
+    return d <= (int)pacc[L];
 }
 
 // ---------------------------------------------------------------------------------------------
 // scan: one lane per (item, orientation, adapter); full-read Myers; emits candidate clusters.
+// Besides the clusters each lane publishes a lower bound of the slot's final best score (from
+// cells that are certainly accepted with the whole adapter aligned: score >= m - 3 * cost), so
+// the resolve stage can drop clusters whose score upper bound is below it.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ void emit_cluster(const RoundArgs& R, uint32_t item, int sub,
-                                             uint32_t j1, uint32_t j2, int lastcol) {
+                                             uint32_t j1, uint32_t j2, int lastcol, int ub) {
     const uint32_t idx = atomicAdd(R.cl_count, 1u);
     if (idx < R.cl_cap) {
         Cluster c;
         c.item = item;
         c.sub = (uint16_t)sub;
         c.lastcol = (uint8_t)lastcol;
-        c.pad = 0;
+        c.ub = (int8_t)max(-128, min(127, ub));
         c.j1 = j1;
         c.j2 = j2;
         R.cl[idx] = c;
@@ -109,10 +126,101 @@ __device__ __forceinline__ void emit_cluster(const RoundArgs& R, uint32_t item, 
     }
 }
 
+// One task's Myers scan over view columns (js, jhi]; last-row candidates are reported for
+// columns in [jlo, jhi] only.  js == 0 with `real` uses cutadapt's column-0 initialisation;
+// otherwise the restricted start D'(i, js) = i, exact for every cell of cost <= k at column
+// >= js + m + k + 1.  Emits clusters; returns this task's score lower bound.
+__device__ __forceinline__ int scan_task(const RoundArgs& R, const TaskView& tv, uint32_t item,
+                                         int sub, const uint64_t* peq, int A,
+                                         const DevAdapter& ad, const int8_t* acc,
+                                         const int8_t* pacc, uint32_t js, bool real,
+                                         uint32_t jlo, uint32_t jhi, bool lastcol) {
+    const int m = ad.m;
+    const int kk = ad.kk;
+    const bool front = ad.where == kFront;
+    const uint32_t hbit = (uint32_t)(m - 1);
+    const uint32_t gap = (uint32_t)(m + ad.k + 1);
+    // FRONT cells beyond this column cannot start in column 0 (that would cost > k)
+    const uint32_t full_from = front ? (uint32_t)(m + ad.k + 1) : 0u;
+    const int acc_m = acc[m];
+
+    uint64_t pv = (front && real) ? 0ull : ~0ull, mv = 0ull;
+    int d = (front && real) ? 0 : m;
+    bool have = false;
+    uint32_t cj1 = 0, cj2 = 0;
+    int cub = -128, lb = 0;
+
+#define DMX_SCAN_STEP(q)                                                                  \
+    {                                                                                     \
+        const uint32_t code = ((codes >> (2 * (q))) & 3u) | (((nb >> (q)) & 1u) << 2);    \
+        myers_step(peq[code * A], pv, mv, d, hbit);                                       \
+        if (d <= kk) {                                                                    \
+            const uint32_t j = p0 + (q) + 1;                                              \
+            const int lr = min(m, (int)j + d);                                            \
+            if (j >= jlo && d <= (int)pacc[lr]) {                                         \
+                const int ubc = lr - 2 * d;                                               \
+                if (j >= full_from && d <= acc_m) lb = max(lb, m - 3 * d);                \
+                if (have && j - cj2 <= gap) {                                             \
+                    cj2 = j;                                                              \
+                    cub = max(cub, ubc);                                                  \
+                } else {                                                                  \
+                    if (have) emit_cluster(R, item, sub, cj1, cj2, 0, cub);               \
+                    have = true;                                                          \
+                    cj1 = cj2 = j;                                                        \
+                    cub = ubc;                                                            \
+                }                                                                         \
+            }                                                                             \
+        }                                                                                 \
+    }
+
+    uint32_t p0 = js;
+    for (; p0 + 16 <= jhi; p0 += 16) {
+        uint32_t codes, nb;
+        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) DMX_SCAN_STEP(q)
+    }
+    if (p0 < jhi) {
+        uint32_t codes, nb;
+        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
+        const int cnt = (int)(jhi - p0);
+        for (int q = 0; q < cnt; ++q) DMX_SCAN_STEP(q)
+    }
+#undef DMX_SCAN_STEP
+
+    // 3' adapters: cutadapt also scans the last column (cells (i, n), i < m: adapter prefix
+    // aligned at the read end).  Flag it if any such cell would be accepted.
+    const uint32_t len = tv.len;
+    if (lastcol && !front && len > 0) {
+        int dd = 0;
+        int ubl = -128;
+        for (int i = 1; i < m; ++i) {
+            dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
+            if (dd <= (int)acc[i]) {              // accepted for sure (aligned length is i)
+                ubl = max(ubl, i - 2 * dd);
+                lb = max(lb, i - 3 * dd);
+            }
+        }
+        if (ubl > -128) {
+            if (have && len - cj2 <= gap) {
+                emit_cluster(R, item, sub, cj1, len, 1, max(cub, ubl));
+            } else {
+                if (have) emit_cluster(R, item, sub, cj1, cj2, 0, cub);
+                emit_cluster(R, item, sub, len, len, 1, ubl);
+            }
+            have = false;
+        }
+    }
+    if (have) emit_cluster(R, item, sub, cj1, cj2, 0, cub);
+    return lb;
+}
+
+// Full scan (panels without a usable shared suffix): one lane per (item, orientation, adapter).
 __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kMaxAdapters];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
-    load_panel_lds(R.panel, s_peq, s_acc);
+    __shared__ int8_t s_pacc[72 * kMaxAdapters];
+    load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
     __syncthreads();
 
     const int A = R.panel->n_adapters;
@@ -127,31 +235,74 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
 
     TaskView tv;
     task_view(R, item, sub, A, tv);
-    const DevAdapter& ad = R.panel->ad[tv.a];
-    const int m = ad.m;
-    const int kk = ad.kk;
-    const bool front = ad.where == kFront;
-    const uint32_t hbit = (uint32_t)(m - 1);
-    const uint32_t gap = (uint32_t)(m + ad.k + 1);
-    const uint64_t* peq = s_peq + tv.a;   // peq[code * A]
+    const int lb = scan_task(R, tv, item, sub, s_peq + tv.a, A, R.panel->ad[tv.a],
+                             s_acc + 72 * tv.a, s_pacc + 72 * tv.a, 0, true, 1, tv.len, true);
+    if (lb > 0) atomicMax(&R.lb[slot_of(R, item, sub)], lb);
+}
 
-    uint64_t pv = front ? 0ull : ~0ull, mv = 0ull;
-    int d = front ? 0 : m;
+// ---------------------------------------------------------------------------------------------
+// filter: one lane per (item, orientation); 32-bit Myers of the panel's shared suffix block.
+// Hit columns (b(j) <= min(kf, pf[min(71, j + kf)])) are grouped into windows.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void emit_window(const RoundArgs& R, uint32_t item, int o, uint32_t j1,
+                                            uint32_t j2, int lastcol) {
+    const uint32_t idx = atomicAdd(R.win_count, 1u);
+    if (idx < R.win_cap) {
+        Window w;
+        w.item = item;
+        w.o = (uint8_t)o;
+        w.lastcol = (uint8_t)lastcol;
+        w.pad = 0;
+        w.j1 = j1;
+        w.j2 = j2;
+        R.win[idx] = w;
+    } else {
+        atomicOr(R.flags, 4u);
+    }
+}
+
+__global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
+    __shared__ uint32_t s_fpeq[8];
+    __shared__ int8_t s_pf[72];
+    const DevPanel* P = R.panel;
+    if (threadIdx.x < 8) s_fpeq[threadIdx.x] = P->filter_peq[threadIdx.x];
+    if (threadIdx.x < 72) s_pf[threadIdx.x] = P->pf[threadIdx.x];
+    __syncthreads();
+
+    const int no = P->n_orient;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t item = t / (uint32_t)no;
+    const int o = (int)(t % (uint32_t)no);
+    const uint32_t n_items = R.items ? *R.n_items_dev : R.n_items;
+    if (item >= n_items) return;
+
+    TaskView tv;
+    task_view(R, item, o * P->n_adapters, P->n_adapters, tv);
+    const bool front = P->where == kFront;
+    const int L = P->filter_len;
+    const uint32_t hbit = (uint32_t)(L - 1);
+    const int kf = P->kf;
+    const int kf_far = min(kf, (int)s_pf[71]);
+    const uint32_t gap = (uint32_t)P->max_mk;
+    uint32_t pv = front ? 0u : ~0u, mv = 0u;
+    int b = front ? 0 : L;
     bool have = false;
-    uint32_t cj1 = 0, cj2 = 0;
+    uint32_t w1 = 0, w2 = 0;
 
-#define DMX_SCAN_STEP(q)                                                                  \
+#define DMX_FILTER_STEP(q)                                                                \
     {                                                                                     \
         const uint32_t code = ((codes >> (2 * (q))) & 3u) | (((nb >> (q)) & 1u) << 2);    \
-        myers_step(peq[code * A], pv, mv, d, hbit);                                       \
-        if (d <= kk) {                                                                    \
+        myers_step32(s_fpeq[code], pv, mv, b, hbit);                                      \
+        if (b <= kf_far) {                                                                \
             const uint32_t j = p0 + (q) + 1;                                              \
-            if (have && j - cj2 <= gap) {                                                 \
-                cj2 = j;                                                                  \
-            } else {                                                                      \
-                if (have) emit_cluster(R, item, sub, cj1, cj2, 0);                        \
-                have = true;                                                              \
-                cj1 = cj2 = j;                                                            \
+            if (j + (uint32_t)kf >= 71u || b <= (int)s_pf[j + kf]) {                      \
+                if (have && j - w2 <= gap) {                                              \
+                    w2 = j;                                                               \
+                } else {                                                                  \
+                    if (have) emit_window(R, item, o, w1, w2, 0);                         \
+                    have = true;                                                          \
+                    w1 = w2 = j;                                                          \
+                }                                                                         \
             }                                                                             \
         }                                                                                 \
     }
@@ -162,53 +313,72 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
         uint32_t codes, nb;
         fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) DMX_SCAN_STEP(q)
+        for (int q = 0; q < 16; ++q) DMX_FILTER_STEP(q)
     }
     if (p0 < len) {
         uint32_t codes, nb;
         fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
         const int cnt = (int)(len - p0);
-        for (int q = 0; q < cnt; ++q) DMX_SCAN_STEP(q)
+        for (int q = 0; q < cnt; ++q) DMX_FILTER_STEP(q)
     }
-#undef DMX_SCAN_STEP
-
-    // 3' adapters: cutadapt also scans the last column (cells (i, n), i < m: adapter suffix
-    // hanging off the read end).  Flag it if any such cell could be accepted.
+#undef DMX_FILTER_STEP
+    // 3' panels: the last column (adapter prefix hanging off the read end) is always checked.
     if (!front && len > 0) {
-        int dd = 0;
-        bool any = false;
-        const int8_t* acc = s_acc + 72 * tv.a;
-        for (int i = 1; i < m; ++i) {
-            dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
-            any |= dd <= (int)acc[i];
+        if (have && len - w2 <= gap) {
+            emit_window(R, item, o, w1, len, 1);
+        } else {
+            if (have) emit_window(R, item, o, w1, w2, 0);
+            emit_window(R, item, o, len, len, 1);
         }
-        if (any) {
-            if (have && len - cj2 <= gap) {
-                emit_cluster(R, item, sub, cj1, len, 1);
-            } else {
-                if (have) emit_cluster(R, item, sub, cj1, cj2, 0);
-                emit_cluster(R, item, sub, len, len, 1);
-            }
-            have = false;
-        }
+        have = false;
     }
-    if (have) emit_cluster(R, item, sub, cj1, cj2, 0);
+    if (have) emit_window(R, item, o, w1, w2, 0);
+}
+
+// Window scan: one lane per (window, adapter), grid-stride over the device-side window count.
+__global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
+    __shared__ uint64_t s_peq[8 * kMaxAdapters];
+    __shared__ int8_t s_acc[72 * kMaxAdapters];
+    __shared__ int8_t s_pacc[72 * kMaxAdapters];
+    load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
+    __syncthreads();
+
+    const int A = R.panel->n_adapters;
+    const uint64_t total = (uint64_t)min(*R.win_count, R.win_cap) * (uint64_t)A;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const Window w = R.win[t / A];
+        const int a = (int)(t % A);
+        const int sub = w.o * A + a;
+        TaskView tv;
+        task_view(R, w.item, sub, A, tv);
+        const DevAdapter& ad = R.panel->ad[a];
+        int js = (int)w.j1 - (int)ad.m - (int)ad.k - 1;
+        const bool real = js <= 0;
+        if (real) js = 0;
+        const int lb = scan_task(R, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
+                                 s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2,
+                                 w.lastcol != 0);
+        if (lb > 0) atomicMax(&R.lb[slot_of(R, w.item, sub)], lb);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
 // resolve: one lane per cluster; restricted Myers window + cutadapt tie-broken traceback.
+// The last RING columns of (Pv, Mv) and the read codes live in LDS, lane-interleaved.
 // ---------------------------------------------------------------------------------------------
+template <int RING>
 struct Walker {
-    const uint32_t* seq;
-    const uint32_t* nmask;
     uint32_t* flags;
-    TaskView tv;
     const uint64_t* peq;    // LDS, + adapter, stride A
     int A;
-    const uint64_t* rp;     // LDS ring (P), lane-interleaved: rp[(j % kRing) * 64]
+    const uint64_t* rp;     // LDS ring (P): rp[slot * 64]
     const uint64_t* rm;
+    const uint8_t* rc;      // LDS ring of read codes: code of view position j-1 at slot(j)
     int js;
     bool real, front;
+
+    __device__ __forceinline__ int slot(int j) const { return (j - js) % RING; }
 
     // Walk cutadapt's DP pointers from cell (i, j) back to the alignment start.
     // Pointer rule (_align.pyx locate): equal characters -> diagonal; else mismatch if
@@ -216,6 +386,7 @@ struct Walker {
     // else deletion (left).  Scores: +1 match, -1 mismatch, -2 indel.
     __device__ void trace(int i, int j, int& origin, int& score) const {
         score = 0;
+        int s0 = slot(j);
         while (i > 0) {
             if (j == js) {
                 if (real) {
@@ -226,50 +397,54 @@ struct Walker {
                         origin = 0;
                     }
                 } else {
-                    atomicOr(flags, 2u);    // unreachable for cost <= k
+                    atomicOr(flags, 2u);       // unreachable for cost <= k
                     score -= 2 * i;
                     origin = js;
                 }
                 return;
             }
-            uint32_t codes, nb;
-            fetch16(seq, nmask, tv.off, tv.n, tv.strand, tv.start, (uint32_t)(j - 1),
-                    codes, nb);
-            const uint32_t code = (codes & 3u) | ((nb & 1u) << 2);
+            const int s1 = s0 == 0 ? RING - 1 : s0 - 1;
+            const uint32_t code = rc[s0 * 64];
             if ((peq[code * A] >> (i - 1)) & 1ull) {
                 --i;
                 --j;
                 ++score;
+                s0 = s1;
                 continue;
             }
-            const int s1 = ((j - 1) & (kRing - 1)) * 64;
-            const int s0 = (j & (kRing - 1)) * 64;
-            const uint64_t p1 = rp[s1], m1 = rm[s1];
+            const uint64_t p1 = rp[s1 * 64], m1 = rm[s1 * 64];
             const int cdel = col_cost(p1, m1, i);                                   // D(i, j-1)
             const int cd = cdel - (int)((p1 >> (i - 1)) & 1ull) + (int)((m1 >> (i - 1)) & 1ull);
-            const int cins = col_cost(rp[s0], rm[s0], i - 1);                       // D(i-1, j)
+            const int cins = col_cost(rp[s0 * 64], rm[s0 * 64], i - 1);             // D(i-1, j)
             if (cd <= cdel && cd <= cins) {
                 --i;
                 --j;
                 score -= 1;
+                s0 = s1;
             } else if (cins <= cdel) {
                 --i;
                 score -= 2;
             } else {
                 --j;
                 score -= 2;
+                s0 = s1;
             }
         }
         origin = j;
     }
 };
 
+template <int RING>
 __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kMaxAdapters];
-    __shared__ int8_t s_acc[72 * kMaxAdapters];
-    __shared__ uint64_t s_rp[kRing * kResolveBlock];
-    __shared__ uint64_t s_rm[kRing * kResolveBlock];
-    load_panel_lds(R.panel, s_peq, s_acc);
+    __shared__ uint64_t s_rp[RING * kResolveBlock];
+    __shared__ uint64_t s_rm[RING * kResolveBlock];
+    __shared__ uint8_t s_rc[RING * kResolveBlock];
+    {
+        const int A = R.panel->n_adapters;
+        for (int x = threadIdx.x; x < 8 * A; x += blockDim.x)
+            s_peq[x] = R.panel->ad[x % A].peq[x / A];
+    }
     __syncthreads();
 
     const int A = R.panel->n_adapters;
@@ -277,45 +452,52 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
     const int lane = threadIdx.x;
     uint64_t* rp = s_rp + lane;
     uint64_t* rm = s_rm + lane;
+    uint8_t* rcode = s_rc + lane;
 
     for (uint32_t ci = blockIdx.x * kResolveBlock + lane; ci < total;
          ci += gridDim.x * kResolveBlock) {
         const Cluster c = R.cl[ci];
+        const uint32_t slot = slot_of(R, c.item, c.sub);
+        const int lbr = R.lb[slot];
+        Outcome out;
+        out.key = ~0ull;
+        out.origin = 0;
+        out.pad = 0;
+        if ((int)c.ub < lbr) {            // cannot reach the slot's guaranteed best score
+            R.outc[ci] = out;
+            continue;
+        }
         TaskView tv;
         task_view(R, c.item, c.sub, A, tv);
         const DevAdapter& ad = R.panel->ad[tv.a];
         const int m = ad.m, k = ad.k, kk = ad.kk;
         const bool front = ad.where == kFront;
-        const uint32_t slot = slot_of(R, c.item, c.sub);
         const uint64_t snapshot = R.winner[slot];
-        const int8_t* acc = s_acc + 72 * tv.a;
+        const int8_t* acc = ad.acc;       // global (L1/L2); rare-path reads only
+        const int8_t* pacc = ad.pacc;
 
         int js = (int)c.j1 - m - k - 1;
         const bool real = js <= 0;
         if (real) js = 0;
         uint64_t pv = (front && real) ? 0ull : ~0ull, mv = 0ull;
         int d = (front && real) ? 0 : m;
-        rp[(js & (kRing - 1)) * 64] = pv;
-        rm[(js & (kRing - 1)) * 64] = mv;
+        rp[0] = pv;                       // slot(js) = 0
+        rm[0] = mv;
 
-        Walker W{R.seq, R.nmask, R.flags, tv, s_peq + tv.a, A, rp, rm, js, real, front};
+        Walker<RING> W{R.flags, s_peq + tv.a, A, rp, rm, rcode, js, real, front};
         bool found = false;
         int bs = 0, bc = 0, bo = 0;
         uint64_t bt = 0;
 
         auto consider = [&](int iend, int j, int cost, uint64_t t) {
-            const int ub = iend - 2 * cost;   // score <= aligned adapter length - 2 * cost
+            const int ub = min(iend, j + cost) - 2 * cost;   // score <= aligned length - 2 cost
+            if (ub < lbr) return;
             if (found && (ub < bs || (ub == bs && cost >= bc))) return;
             if (make_key(ub, tv.o, cost, tv.a, t) > snapshot) return;
             int origin, score;
             if (cost == 0) {                  // exact: the pointer chain is the pure diagonal
-                if (j >= iend) {
-                    origin = j - iend;
-                    score = iend;
-                } else {
-                    origin = j - iend;        // FRONT only: reaches column 0 at row iend - j
-                    score = j;
-                }
+                origin = j - iend;            // (FRONT only when j < iend: reaches column 0)
+                score = j >= iend ? iend : j;
             } else {
                 W.trace(iend, j, origin, score);
             }
@@ -332,6 +514,7 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
 
         const uint32_t hbit = (uint32_t)(m - 1);
         const uint64_t* peq = s_peq + tv.a;
+        int sl = 0;
         for (uint32_t p0 = (uint32_t)js; p0 < c.j2; p0 += 16) {
             uint32_t codes, nb;
             fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
@@ -340,9 +523,14 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
                 const uint32_t code = ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
                 myers_step(peq[code * A], pv, mv, d, hbit);
                 const uint32_t j = p0 + q + 1;
-                rp[(j & (kRing - 1)) * 64] = pv;
-                rm[(j & (kRing - 1)) * 64] = mv;
-                if (j >= c.j1 && d <= kk) consider(m, (int)j, d, j);
+                sl = sl == RING - 1 ? 0 : sl + 1;
+                rp[sl * 64] = pv;
+                rm[sl * 64] = mv;
+                rcode[sl * 64] = (uint8_t)code;
+                if (j >= c.j1 && d <= kk) {
+                    const int lr = min(m, (int)j + d);
+                    if (d <= (int)pacc[lr]) consider(m, (int)j, d, j);
+                }
             }
         }
         if (c.lastcol && !front) {
@@ -352,10 +540,6 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
                 if (dd <= (int)acc[i]) consider(i, (int)tv.len, dd, (uint64_t)tv.len + 1 + i);
             }
         }
-        Outcome out;
-        out.key = ~0ull;
-        out.origin = 0;
-        out.pad = 0;
         if (found) {
             out.key = make_key(bs, tv.o, bc, tv.a, bt);
             out.origin = bo;
@@ -547,14 +731,31 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     R.flags = c->d_counters + 3;
     R.winner = c->d_winner[round];
     R.origin = c->d_origin[round];
+    R.lb = c->d_lb[round];
     if (R.T > kScanBlock) return DMX_E_UNSUPPORTED;
+    hipMemsetAsync(R.lb, 0, sizeof(int32_t) * (round == 0 ? c->slot_cap : c->item_cap), st);
 
     const uint32_t rpb = kScanBlock / R.T;
     const uint32_t grid = (uint32_t)((R.n_items + rpb - 1) / rpb);
+    R.win = c->d_win;
+    R.win_count = c->d_counters + 4 + round;
+    R.win_cap = (uint32_t)c->win_cap;
     hipEventRecord(c->ev[round * 3 + 0], st);
-    if (grid > 0) hipLaunchKernelGGL(scan_kernel, dim3(grid), dim3(kScanBlock), 0, st, R);
+    if (hp.filter) {
+        const uint32_t nthreads = R.n_items * (uint32_t)hp.n_orient;
+        const uint32_t fgrid = (nthreads + kScanBlock - 1) / kScanBlock;
+        if (fgrid > 0) hipLaunchKernelGGL(filter_kernel, dim3(fgrid), dim3(kScanBlock), 0, st, R);
+        hipLaunchKernelGGL(wscan_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
+    } else if (grid > 0) {
+        hipLaunchKernelGGL(scan_kernel, dim3(grid), dim3(kScanBlock), 0, st, R);
+    }
     hipEventRecord(c->ev[round * 3 + 1], st);
-    hipLaunchKernelGGL(resolve_kernel, dim3(resolve_grid(c)), dim3(kResolveBlock), 0, st, R);
+    if (c->ring_small[round])
+        hipLaunchKernelGGL(resolve_kernel<kRingSmall>, dim3(resolve_grid(c)), dim3(kResolveBlock),
+                           0, st, R);
+    else
+        hipLaunchKernelGGL(resolve_kernel<kRingLarge>, dim3(resolve_grid(c)), dim3(kResolveBlock),
+                           0, st, R);
     hipLaunchKernelGGL(select_kernel, dim3(1024), dim3(256), 0, st, R);
     hipEventRecord(c->ev[round * 3 + 2], st);
     return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;

@@ -188,9 +188,10 @@ class Context:
 
     def stats(self):
         ms = (ctypes.c_float * 7)()
-        cl = np.zeros(2, dtype=np.uint64)
+        cl = np.zeros(4, dtype=np.uint64)
         fl = ctypes.c_int()
         self._check(self._L.dmx_stats(self._h, ms, 7, cl.ctypes.data, ctypes.byref(fl)),
                     "dmx_stats")
         names = ["scan0", "resolve0", "finalize0", "scan1", "resolve1", "finalize1", "total"]
-        return {"ms": dict(zip(names, list(ms))), "clusters": cl.tolist(), "flags": fl.value}
+        return {"ms": dict(zip(names, list(ms))), "clusters": cl[:2].tolist(),
+                "windows": cl[2:].tolist(), "flags": fl.value}

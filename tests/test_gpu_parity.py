@@ -43,3 +43,90 @@ def test_two_round_matches_oracle(ctx, config, n):
     for f in ("bin1", "rc1", "bin2", "rc2"):
         assert np.array_equal(got_v[f], exp[f]), f
     _assert_same(got, exp)
+
+
+def _random_panel(rng, n, lo, hi, wildcard=0.0):
+    out = []
+    for _ in range(n):
+        L = int(rng.integers(lo, hi + 1))
+        s = "".join(rng.choice(list("ACGT"), size=L))
+        if wildcard:
+            s = "".join(c if rng.random() > wildcard else rng.choice(list("NRYSWKMBDHV"))
+                        for c in s)
+        out.append(s)
+    return out
+
+
+def _reads_with(rng, panel, n, L=(0, 400), err=0.06):
+    seqs = []
+    for _ in range(n):
+        Ln = int(rng.integers(L[0], L[1] + 1))
+        s = "".join(rng.choice(list("ACGTN"), size=Ln, p=[0.249, 0.249, 0.249, 0.249, 0.004]))
+        if panel and rng.random() < 0.8:
+            a = panel[int(rng.integers(len(panel)))]
+            a = "".join(c if c in "ACGT" else "ACGT"[int(rng.integers(4))] for c in a)
+            frag = []
+            for c in a:
+                r = rng.random()
+                if r < err * 0.6:
+                    frag.append("ACGT"[int(rng.integers(4))])
+                elif r < err * 0.8:
+                    pass
+                elif r < err:
+                    frag += [c, "ACGT"[int(rng.integers(4))]]
+                else:
+                    frag.append(c)
+            frag = "".join(frag)
+            if rng.random() < 0.2:   # partial at either end
+                cut = int(rng.integers(1, max(2, len(frag))))
+                frag = frag[cut:] if rng.random() < 0.5 else frag[:cut]
+            p = int(rng.integers(0, len(s) + 1))
+            s = s[:p] + frag + s[p:]
+        if rng.random() < 0.3:
+            s = oracle_rc(s)
+        seqs.append(s)
+    return seqs
+
+
+def oracle_rc(s):
+    import pyref
+    return pyref.revcomp(s)
+
+
+@pytest.mark.parametrize("where", ["front", "back"])
+@pytest.mark.parametrize("wild", [0.0, 0.15])
+@pytest.mark.parametrize("rc", [True, False])
+def test_single_round_random_panels(ctx, where, wild, rc):
+    """Full-scan path (no shared suffix), mixed adapter lengths 3..64, IUPAC wildcards, N in
+    reads, empty and short reads, partial adapters at both read ends."""
+    rng = np.random.default_rng(11 + (where == "back") * 3 + int(wild * 100) + rc)
+    panel = _random_panel(rng, 9, 3, 64, wild)
+    seqs = _reads_with(rng, panel, 1500) + ["", "A", "ACG", panel[0][:5], panel[1][-4:]]
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    ow = oracle.FRONT if where == "front" else oracle.BACK
+    exp = oracle.run_batch(oracle.Panel(panel, ow), None, blob, offs, lens, mode=0, use_rc=rc,
+                           threads=8)
+    f = (lib.DMX_FRONT if where == "front" else lib.DMX_BACK) | (lib.DMX_RC if rc else 0)
+    ctx.set_panel(0, panel, f)
+    ctx.set_mode(lib.MODE_SINGLE)
+    got = ctx.run(lib.pack(blob, offs, lens))
+    _assert_same(got, exp)
+
+
+@pytest.mark.parametrize("e", [0.1, 0.2, 2])
+def test_error_rates_and_filter_toggle(ctx, e, monkeypatch):
+    """-e as a rate and as an absolute count; shared-suffix filter on vs off agree."""
+    d = synth.generate("c4", n=3000, seed=5)
+    p1 = oracle.Panel(d["sp5"], oracle.FRONT, max_errors=e)
+    p2 = oracle.Panel(d["sp27"], oracle.BACK, max_errors=e)
+    exp = oracle.run_batch(p1, p2, d["blob"], d["offsets"], d["lengths"], mode=1, threads=8)
+    ctx.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC, e)
+    ctx.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC, e)
+    ctx.set_mode(lib.MODE_TWO_ROUND)
+    _assert_same(ctx.run(lib.pack(d["blob"], d["offsets"], d["lengths"])), exp)
+    monkeypatch.setenv("DMX_NO_FILTER", "1")
+    with lib.Context(0) as c2:
+        c2.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC, e)
+        c2.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC, e)
+        c2.set_mode(lib.MODE_TWO_ROUND)
+        _assert_same(c2.run(lib.pack(d["blob"], d["offsets"], d["lengths"])), exp)
