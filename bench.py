@@ -128,6 +128,8 @@ def main():
                               "finalize1", "total")}
     clusters = np.zeros(2)
     windows = np.zeros(2)
+    resolved = np.zeros(2)
+    traces = np.zeros(2)
     barrier_sync()
     t = time.perf_counter()
     counts = None
@@ -140,6 +142,8 @@ def main():
             stage[k] += st["ms"][k]
         clusters += np.array(st["clusters"], dtype=np.float64)
         windows += np.array(st["windows"], dtype=np.float64)
+        resolved += np.array(st["resolved"], dtype=np.float64)
+        traces += np.array(st["traces"], dtype=np.float64)
         flags |= st["flags"]
         counts = allreduce_counts()
     barrier_sync()
@@ -188,6 +192,8 @@ def main():
         "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
         "clusters_per_step": (clusters / K).tolist(),
         "filter_windows_per_step": (windows / K).tolist(),
+        "resolved_clusters_per_step": (resolved / K).tolist(),
+        "tracebacks_per_step": (traces / K).tolist(),
         "reads_round2_per_gpu": n2,
         "unknown_round1": int(counts[0]) if counts is not None else None,
         "gen_s": round(gen_s, 1),

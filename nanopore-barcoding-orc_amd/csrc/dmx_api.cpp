@@ -508,13 +508,17 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* clusters, int*
     }
     hipEventElapsedTime(&t[6], c->ev[8], c->ev[6 + rounds - 1]);
     for (int i = 0; i < n_stage && i < 7; ++i) stage_ms[i] = t[i];
-    uint32_t cnt[6];
+    uint32_t cnt[12];
     CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
     if (clusters) {
         clusters[0] = cnt[0];
         clusters[1] = cnt[1];
         clusters[2] = cnt[4];
         clusters[3] = cnt[5];
+        clusters[4] = cnt[8];
+        clusters[5] = cnt[10];
+        clusters[6] = cnt[9];
+        clusters[7] = cnt[11];
     }
     if (flags) {
         int f = (int)cnt[3];
@@ -531,7 +535,7 @@ int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint
     if (rc) return rc;
     for (int attempt = 0; attempt < 8; ++attempt) {
         if ((rc = dmx_exec(c))) return rc;
-        uint64_t cl[4];
+        uint64_t cl[8];
         int flags = 0;
         float ms[7];
         if ((rc = dmx_stats(c, ms, 7, cl, &flags))) return rc;

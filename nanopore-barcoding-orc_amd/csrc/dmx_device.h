@@ -70,8 +70,55 @@ struct Window {
     uint32_t item;
     uint8_t o;
     uint8_t lastcol;     // 3' panel: window ends at the final column (last-column cells)
-    uint16_t pad;
+    uint8_t strand;      // oriented view of the item (copied so the window scan needs no
+    uint8_t pad;         // dependent loads): strand, start, len, read length n, first nt off
     uint32_t j1, j2;     // candidate end columns [j1, j2]
+    uint32_t n, start, len, pad2;
+    uint64_t off;
+};
+static_assert(sizeof(Window) == 40, "Window layout");
+
+constexpr int kStageCap = 256;    // LDS staging of emitted records per block
+
+// Block-level staging of appended records: lanes append to LDS (LDS atomics), the block then
+// reserves its range of the global list with ONE global atomic.  A single global counter
+// hammered by every lane serialises at the memory side (MI355X_MICROARCH.md, 'fanin').
+template <typename Rec>
+struct Stage {
+    Rec* buf;              // LDS [kStageCap]
+    uint32_t* cnt;         // LDS
+    uint32_t* base;        // LDS scratch
+    Rec* g;
+    uint32_t* gcount;
+    uint32_t gcap;
+    uint32_t* flags;
+    uint32_t ovf;
+
+    __device__ __forceinline__ void push(const Rec& r) const {
+        const uint32_t i = atomicAdd(cnt, 1u);
+        if (i < (uint32_t)kStageCap) {
+            buf[i] = r;
+            return;
+        }
+        const uint32_t gi = atomicAdd(gcount, 1u);   // LDS full: direct (rare)
+        if (gi < gcap) g[gi] = r;
+        else atomicOr(flags, ovf);
+    }
+    // Every thread of the block must call flush().
+    __device__ __forceinline__ void flush() const {
+        __syncthreads();
+        const uint32_t n = min(*cnt, (uint32_t)kStageCap);
+        if (threadIdx.x == 0) *base = n ? atomicAdd(gcount, n) : 0u;
+        __syncthreads();
+        const uint32_t b = *base;
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+            if (b + i < gcap) g[b + i] = buf[i];
+            else atomicOr(flags, ovf);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) *cnt = 0;
+        __syncthreads();
+    }
 };
 
 // A view of a read: strand 0 = the read as given, strand 1 = its reverse complement; the view

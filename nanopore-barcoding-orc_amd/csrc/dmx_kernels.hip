@@ -36,6 +36,7 @@ struct RoundArgs {
     Window* win;
     uint32_t* win_count;
     uint32_t win_cap;
+    uint32_t* diag;              // [0] resolved clusters, [1] tracebacks
 };
 
 struct TaskView {
@@ -104,37 +105,32 @@ __device__ __forceinline__ bool row_candidate(const int8_t* pacc, int m, uint32_
 }
 
 // ---------------------------------------------------------------------------------------------
-// scan: one lane per (item, orientation, adapter); full-read Myers; emits candidate clusters.
-// Besides the clusters each lane publishes a lower bound of the slot's final best score (from
+// scan: per (item, orientation, adapter) Myers over a column range; emits candidate clusters.
+// Besides the clusters each task publishes a lower bound of the slot's final best score (from
 // cells that are certainly accepted with the whole adapter aligned: score >= m - 3 * cost), so
 // the resolve stage can drop clusters whose score upper bound is below it.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void emit_cluster(const RoundArgs& R, uint32_t item, int sub,
-                                             uint32_t j1, uint32_t j2, int lastcol, int ub) {
-    const uint32_t idx = atomicAdd(R.cl_count, 1u);
-    if (idx < R.cl_cap) {
-        Cluster c;
-        c.item = item;
-        c.sub = (uint16_t)sub;
-        c.lastcol = (uint8_t)lastcol;
-        c.ub = (int8_t)max(-128, min(127, ub));
-        c.j1 = j1;
-        c.j2 = j2;
-        R.cl[idx] = c;
-    } else {
-        atomicOr(R.flags, 1u);
-    }
+__device__ __forceinline__ Cluster make_cluster(uint32_t item, int sub, uint32_t j1, uint32_t j2,
+                                                int lastcol, int ub) {
+    Cluster c;
+    c.item = item;
+    c.sub = (uint16_t)sub;
+    c.lastcol = (uint8_t)lastcol;
+    c.ub = (int8_t)max(-128, min(127, ub));
+    c.j1 = j1;
+    c.j2 = j2;
+    return c;
 }
 
 // One task's Myers scan over view columns (js, jhi]; last-row candidates are reported for
 // columns in [jlo, jhi] only.  js == 0 with `real` uses cutadapt's column-0 initialisation;
 // otherwise the restricted start D'(i, js) = i, exact for every cell of cost <= k at column
 // >= js + m + k + 1.  Emits clusters; returns this task's score lower bound.
-__device__ __forceinline__ int scan_task(const RoundArgs& R, const TaskView& tv, uint32_t item,
-                                         int sub, const uint64_t* peq, int A,
-                                         const DevAdapter& ad, const int8_t* acc,
-                                         const int8_t* pacc, uint32_t js, bool real,
-                                         uint32_t jlo, uint32_t jhi, bool lastcol) {
+__device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster>& st,
+                                         const TaskView& tv, uint32_t item, int sub,
+                                         const uint64_t* peq, int A, const DevAdapter& ad,
+                                         const int8_t* acc, const int8_t* pacc, uint32_t js,
+                                         bool real, uint32_t jlo, uint32_t jhi, bool lastcol) {
     const int m = ad.m;
     const int kk = ad.kk;
     const bool front = ad.where == kFront;
@@ -164,7 +160,7 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const TaskView& tv,
                     cj2 = j;                                                              \
                     cub = max(cub, ubc);                                                  \
                 } else {                                                                  \
-                    if (have) emit_cluster(R, item, sub, cj1, cj2, 0, cub);               \
+                    if (have) st.push(make_cluster(item, sub, cj1, cj2, 0, cub));         \
                     have = true;                                                          \
                     cj1 = cj2 = j;                                                        \
                     cub = ubc;                                                            \
@@ -203,23 +199,31 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const TaskView& tv,
         }
         if (ubl > -128) {
             if (have && len - cj2 <= gap) {
-                emit_cluster(R, item, sub, cj1, len, 1, max(cub, ubl));
+                st.push(make_cluster(item, sub, cj1, len, 1, max(cub, ubl)));
             } else {
-                if (have) emit_cluster(R, item, sub, cj1, cj2, 0, cub);
-                emit_cluster(R, item, sub, len, len, 1, ubl);
+                if (have) st.push(make_cluster(item, sub, cj1, cj2, 0, cub));
+                st.push(make_cluster(item, sub, len, len, 1, ubl));
             }
             have = false;
         }
     }
-    if (have) emit_cluster(R, item, sub, cj1, cj2, 0, cub);
+    if (have) st.push(make_cluster(item, sub, cj1, cj2, 0, cub));
     return lb;
 }
+
+#define DMX_CLUSTER_STAGE                                                                 \
+    __shared__ Cluster s_cl[kStageCap];                                                   \
+    __shared__ uint32_t s_clcnt, s_clbase;                                                \
+    if (threadIdx.x == 0) s_clcnt = 0;                                                    \
+    const Stage<Cluster> st{s_cl, &s_clcnt, &s_clbase, R.cl, R.cl_count, R.cl_cap,        \
+                            R.flags, 1u};
 
 // Full scan (panels without a usable shared suffix): one lane per (item, orientation, adapter).
 __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kMaxAdapters];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
     __shared__ int8_t s_pacc[72 * kMaxAdapters];
+    DMX_CLUSTER_STAGE
     load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
     __syncthreads();
 
@@ -227,67 +231,95 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
     const int T = R.T;
     const int rpb = kScanBlock / T;
     const int tid = threadIdx.x;
-    if (tid >= rpb * T) return;
     const uint32_t item = blockIdx.x * (uint32_t)rpb + (uint32_t)(tid / T);
     const int sub = tid % T;
     const uint32_t n_items = R.items ? *R.n_items_dev : R.n_items;
-    if (item >= n_items) return;
-
-    TaskView tv;
-    task_view(R, item, sub, A, tv);
-    const int lb = scan_task(R, tv, item, sub, s_peq + tv.a, A, R.panel->ad[tv.a],
-                             s_acc + 72 * tv.a, s_pacc + 72 * tv.a, 0, true, 1, tv.len, true);
-    if (lb > 0) atomicMax(&R.lb[slot_of(R, item, sub)], lb);
+    if (tid < rpb * T && item < n_items) {
+        TaskView tv;
+        task_view(R, item, sub, A, tv);
+        const int lb = scan_task(R, st, tv, item, sub, s_peq + tv.a, A, R.panel->ad[tv.a],
+                                 s_acc + 72 * tv.a, s_pacc + 72 * tv.a, 0, true, 1, tv.len,
+                                 true);
+        if (lb > 0) atomicMax(&R.lb[slot_of(R, item, sub)], lb);
+    }
+    st.flush();
 }
 
 // ---------------------------------------------------------------------------------------------
-// filter: one lane per (item, orientation); 32-bit Myers of the panel's shared suffix block.
-// Hit columns (b(j) <= min(kf, pf[min(71, j + kf)])) are grouped into windows.
+// filter: persistent lanes over a block's range of (item, orientation) views; 32-bit Myers of
+// the panel's shared suffix block.  Hit columns (b(j) <= min(kf, pf[min(71, j + kf)])) are
+// grouped into windows.  A lane that finishes a view takes the block's next one, so lanes of a
+// wave stay busy however unequal the read lengths are.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void emit_window(const RoundArgs& R, uint32_t item, int o, uint32_t j1,
-                                            uint32_t j2, int lastcol) {
-    const uint32_t idx = atomicAdd(R.win_count, 1u);
-    if (idx < R.win_cap) {
-        Window w;
-        w.item = item;
-        w.o = (uint8_t)o;
-        w.lastcol = (uint8_t)lastcol;
-        w.pad = 0;
-        w.j1 = j1;
-        w.j2 = j2;
-        R.win[idx] = w;
-    } else {
-        atomicOr(R.flags, 4u);
-    }
+constexpr uint32_t kFilterViewsPerBlock = 1024;
+constexpr int kFilterChunksPerRound = 12;
+
+__device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskView& tv,
+                                              uint32_t j1, uint32_t j2, int lastcol) {
+    Window w;
+    w.item = item;
+    w.o = (uint8_t)o;
+    w.lastcol = (uint8_t)lastcol;
+    w.strand = (uint8_t)tv.strand;
+    w.pad = 0;
+    w.j1 = j1;
+    w.j2 = j2;
+    w.n = tv.n;
+    w.start = tv.start;
+    w.len = tv.len;
+    w.pad2 = 0;
+    w.off = tv.off;
+    return w;
 }
 
 __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
     __shared__ uint32_t s_fpeq[8];
     __shared__ int8_t s_pf[72];
+    __shared__ Window s_win[kStageCap];
+    __shared__ uint32_t s_wcnt, s_wbase, s_next;
     const DevPanel* P = R.panel;
+    const int no = P->n_orient;
+    const uint32_t n_items = R.items ? *R.n_items_dev : R.n_items;
+    const uint32_t n_views = n_items * (uint32_t)no;
+    const uint32_t vbeg = blockIdx.x * kFilterViewsPerBlock;
+    const uint32_t vend = min(n_views, vbeg + kFilterViewsPerBlock);
     if (threadIdx.x < 8) s_fpeq[threadIdx.x] = P->filter_peq[threadIdx.x];
     if (threadIdx.x < 72) s_pf[threadIdx.x] = P->pf[threadIdx.x];
+    if (threadIdx.x == 0) {
+        s_wcnt = 0;
+        s_next = vbeg;
+    }
     __syncthreads();
+    const Stage<Window> st{s_win, &s_wcnt, &s_wbase, R.win, R.win_count, R.win_cap, R.flags, 4u};
 
-    const int no = P->n_orient;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t item = t / (uint32_t)no;
-    const int o = (int)(t % (uint32_t)no);
-    const uint32_t n_items = R.items ? *R.n_items_dev : R.n_items;
-    if (item >= n_items) return;
-
-    TaskView tv;
-    task_view(R, item, o * P->n_adapters, P->n_adapters, tv);
     const bool front = P->where == kFront;
     const int L = P->filter_len;
     const uint32_t hbit = (uint32_t)(L - 1);
     const int kf = P->kf;
     const int kf_far = min(kf, (int)s_pf[71]);
     const uint32_t gap = (uint32_t)P->max_mk;
-    uint32_t pv = front ? 0u : ~0u, mv = 0u;
-    int b = front ? 0 : L;
+    const int A = P->n_adapters;
+
+    uint32_t v = vbeg < vend ? atomicAdd(&s_next, 1u) : vend;
+    bool active = v < vend;
+    uint32_t item = 0;
+    int o = 0;
+    TaskView tv;
+    uint32_t pv = 0, mv = 0, p0 = 0;
+    int b = 0;
     bool have = false;
     uint32_t w1 = 0, w2 = 0;
+    auto start_view = [&]() {
+        item = v / (uint32_t)no;
+        o = (int)(v % (uint32_t)no);
+        task_view(R, item, o * A, A, tv);
+        pv = front ? 0u : ~0u;
+        mv = 0u;
+        b = front ? 0 : L;
+        p0 = 0;
+        have = false;
+    };
+    if (active) start_view();
 
 #define DMX_FILTER_STEP(q)                                                                \
     {                                                                                     \
@@ -299,7 +331,7 @@ __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
                 if (have && j - w2 <= gap) {                                              \
                     w2 = j;                                                               \
                 } else {                                                                  \
-                    if (have) emit_window(R, item, o, w1, w2, 0);                         \
+                    if (have) st.push(make_window(item, o, tv, w1, w2, 0));               \
                     have = true;                                                          \
                     w1 = w2 = j;                                                          \
                 }                                                                         \
@@ -307,60 +339,82 @@ __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
         }                                                                                 \
     }
 
-    const uint32_t len = tv.len;
-    uint32_t p0 = 0;
-    for (; p0 + 16 <= len; p0 += 16) {
-        uint32_t codes, nb;
-        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
+    // Rounds of at most kFilterChunksPerRound chunks per lane; between rounds the block flushes
+    // its staged windows (a uniform point), so the LDS staging never overflows in practice.
+    while (__syncthreads_or(active)) {
+        for (int it = 0; it < kFilterChunksPerRound && active; ++it) {
+            uint32_t codes, nb;
+            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
+            if (p0 + 16 <= tv.len) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) DMX_FILTER_STEP(q)
-    }
-    if (p0 < len) {
-        uint32_t codes, nb;
-        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
-        const int cnt = (int)(len - p0);
-        for (int q = 0; q < cnt; ++q) DMX_FILTER_STEP(q)
+                for (int q = 0; q < 16; ++q) DMX_FILTER_STEP(q)
+                p0 += 16;
+            } else {
+                const int cnt = (int)(tv.len - p0);
+                for (int q = 0; q < cnt; ++q) DMX_FILTER_STEP(q)
+                // 3' panels: the last column (adapter prefix off the read end) is always checked
+                const uint32_t len = tv.len;
+                if (!front && len > 0) {
+                    if (have && len - w2 <= gap) {
+                        st.push(make_window(item, o, tv, w1, len, 1));
+                    } else {
+                        if (have) st.push(make_window(item, o, tv, w1, w2, 0));
+                        st.push(make_window(item, o, tv, len, len, 1));
+                    }
+                    have = false;
+                }
+                if (have) st.push(make_window(item, o, tv, w1, w2, 0));
+                v = atomicAdd(&s_next, 1u);
+                active = v < vend;
+                if (active) start_view();
+            }
+        }
+        st.flush();
     }
 #undef DMX_FILTER_STEP
-    // 3' panels: the last column (adapter prefix hanging off the read end) is always checked.
-    if (!front && len > 0) {
-        if (have && len - w2 <= gap) {
-            emit_window(R, item, o, w1, len, 1);
-        } else {
-            if (have) emit_window(R, item, o, w1, w2, 0);
-            emit_window(R, item, o, len, len, 1);
-        }
-        have = false;
-    }
-    if (have) emit_window(R, item, o, w1, w2, 0);
 }
 
-// Window scan: one lane per (window, adapter), grid-stride over the device-side window count.
+// Window scan: one lane per (window, adapter); block-uniform grid-stride over the device-side
+// window count so that the block can flush its staged clusters between strides.
 __global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kMaxAdapters];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
     __shared__ int8_t s_pacc[72 * kMaxAdapters];
+    DMX_CLUSTER_STAGE
     load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
     __syncthreads();
 
     const int A = R.panel->n_adapters;
     const uint64_t total = (uint64_t)min(*R.win_count, R.win_cap) * (uint64_t)A;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-         t += (uint64_t)gridDim.x * blockDim.x) {
-        const Window w = R.win[t / A];
-        const int a = (int)(t % A);
-        const int sub = w.o * A + a;
-        TaskView tv;
-        task_view(R, w.item, sub, A, tv);
-        const DevAdapter& ad = R.panel->ad[a];
-        int js = (int)w.j1 - (int)ad.m - (int)ad.k - 1;
-        const bool real = js <= 0;
-        if (real) js = 0;
-        const int lb = scan_task(R, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
-                                 s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2,
-                                 w.lastcol != 0);
-        if (lb > 0) atomicMax(&R.lb[slot_of(R, w.item, sub)], lb);
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < total;
+         base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = base + threadIdx.x;
+        if (t < total) {
+            const Window w = R.win[t / A];
+            const int a = (int)(t % A);
+            const int sub = w.o * A + a;
+            TaskView tv;
+            tv.read = 0;
+            tv.n = w.n;
+            tv.strand = w.strand;
+            tv.start = w.start;
+            tv.len = w.len;
+            tv.off = w.off;
+            tv.o = w.o;
+            tv.a = a;
+            const DevAdapter& ad = R.panel->ad[a];
+            int js = (int)w.j1 - (int)ad.m - (int)ad.k - 1;
+            const bool real = js <= 0;
+            if (real) js = 0;
+            const int lb = scan_task(R, st, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
+                                     s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2,
+                                     w.lastcol != 0);
+            if (lb > 0) atomicMax(&R.lb[slot_of(R, w.item, sub)], lb);
+        }
+        __syncthreads();                             // make the staged count block-uniform
+        if (s_clcnt > kStageCap / 2) st.flush();
     }
+    st.flush();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -450,6 +504,7 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
     const int A = R.panel->n_adapters;
     const uint32_t total = min(*R.cl_count, R.cl_cap);
     const int lane = threadIdx.x;
+    uint32_t n_resolved = 0, n_traces = 0;
     uint64_t* rp = s_rp + lane;
     uint64_t* rm = s_rm + lane;
     uint8_t* rcode = s_rc + lane;
@@ -469,6 +524,7 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
         }
         TaskView tv;
         task_view(R, c.item, c.sub, A, tv);
+        ++n_resolved;
         const DevAdapter& ad = R.panel->ad[tv.a];
         const int m = ad.m, k = ad.k, kk = ad.kk;
         const bool front = ad.where == kFront;
@@ -500,6 +556,7 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
                 score = j >= iend ? iend : j;
             } else {
                 W.trace(iend, j, origin, score);
+                ++n_traces;
             }
             const int lr = iend + (origin < 0 ? origin : 0);
             if (lr < 0 || cost > (int)acc[lr]) return;
@@ -547,6 +604,9 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
         }
         R.outc[ci] = out;
     }
+    // diagnostics: clusters that survived the lb prune, tracebacks walked (one atomic / lane)
+    if (n_resolved) atomicAdd(R.diag, n_resolved);
+    if (n_traces) atomicAdd(R.diag + 1, n_traces);
 }
 
 // select: the cluster whose outcome is the slot's winner publishes its origin.
@@ -737,13 +797,14 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
 
     const uint32_t rpb = kScanBlock / R.T;
     const uint32_t grid = (uint32_t)((R.n_items + rpb - 1) / rpb);
+    R.diag = c->d_counters + 8 + 2 * round;
     R.win = c->d_win;
     R.win_count = c->d_counters + 4 + round;
     R.win_cap = (uint32_t)c->win_cap;
     hipEventRecord(c->ev[round * 3 + 0], st);
     if (hp.filter) {
-        const uint32_t nthreads = R.n_items * (uint32_t)hp.n_orient;
-        const uint32_t fgrid = (nthreads + kScanBlock - 1) / kScanBlock;
+        const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
+        const uint32_t fgrid = (uint32_t)((nviews + kFilterViewsPerBlock - 1) / kFilterViewsPerBlock);
         if (fgrid > 0) hipLaunchKernelGGL(filter_kernel, dim3(fgrid), dim3(kScanBlock), 0, st, R);
         hipLaunchKernelGGL(wscan_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
     } else if (grid > 0) {

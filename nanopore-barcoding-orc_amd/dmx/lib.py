@@ -188,10 +188,11 @@ class Context:
 
     def stats(self):
         ms = (ctypes.c_float * 7)()
-        cl = np.zeros(4, dtype=np.uint64)
+        cl = np.zeros(8, dtype=np.uint64)
         fl = ctypes.c_int()
         self._check(self._L.dmx_stats(self._h, ms, 7, cl.ctypes.data, ctypes.byref(fl)),
                     "dmx_stats")
         names = ["scan0", "resolve0", "finalize0", "scan1", "resolve1", "finalize1", "total"]
         return {"ms": dict(zip(names, list(ms))), "clusters": cl[:2].tolist(),
-                "windows": cl[2:].tolist(), "flags": fl.value}
+                "windows": cl[2:4].tolist(), "resolved": cl[4:6].tolist(),
+                "traces": cl[6:8].tolist(), "flags": fl.value}

@@ -1,0 +1,90 @@
+"""Host-side logic without a GPU: the C-ABI library loads and exports every declared symbol,
+the packer's layout, panel parsing, synthetic generator determinism."""
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from dmx import lib, panel, synth
+
+ROOT = __import__("os").path.dirname(__import__("os").path.dirname(__file__))
+
+
+def test_library_exports_every_declared_symbol():
+    hdr = open(f"{ROOT}/include/dmx.h").read()
+    declared = set(re.findall(r"^\s*(?:int|void|const char\*|size_t)\s+(dmx_\w+)\(", hdr, re.M))
+    assert declared == set(lib.EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (dmx_\w+)", out))
+    assert declared <= exported
+    L = lib.load()
+    assert L.dmx_abi_version() == 1
+
+
+def _unpack(p: lib.Packed, i: int) -> str:
+    off, n = int(p.offsets[i]), int(p.lengths[i])
+    out = []
+    for x in range(off, off + n):
+        code = (int(p.seq2b[x // 16]) >> (2 * (x % 16))) & 3
+        nb = (int(p.nmask[x // 32]) >> (x % 32)) & 1
+        out.append("N" if nb else "ACGT"[code])
+    return "".join(out)
+
+
+def test_pack_layout_roundtrip():
+    rng = np.random.default_rng(0)
+    seqs = ["", "A", "acgtN", "".join(rng.choice(list("ACGTNRY"), 1000))] + \
+           ["".join(rng.choice(list("ACGT"), int(rng.integers(0, 300)))) for _ in range(50)]
+    blob = np.frombuffer("".join(seqs).encode(), dtype=np.uint8)
+    lens = np.array([len(s) for s in seqs], dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.uint64)
+    p = lib.pack(blob, offs, lens)
+    assert p.offsets[0] == lib.PACK_PAD and all(o % 32 == 0 for o in p.offsets)
+    for i, s in enumerate(seqs):
+        exp = "".join(c if c in "ACGT" else "N" for c in s.upper())
+        assert _unpack(p, i) == exp
+
+
+def test_fasta_panels_match_survey_facts():
+    n5, s5 = panel.load_panel(panel.SP5_FASTA)
+    n27, s27 = panel.load_panel(panel.SP27RC_FASTA)
+    assert len(s5) == 12 and {len(s) for s in s5} == {59}
+    assert len(s27) == 12 and {len(s) for s in s27} == {57}
+    assert n5[0] == "SP5_001" and n27[11] == "SP27_012"
+    assert all(s.startswith("CATGTAATGCACGTACTTTCAGGGT") for s in s5)
+    assert all(s.endswith("AGTCGTCGCAGCCTCACCTGATC") for s in s27)
+
+
+def test_fasta_blank_lines_and_iupac():
+    recs = panel.read_fasta(panel.RNA_FASTA)
+    assert [h.split("|")[0] for h, _ in recs] == ["SSU_F04", "28S_3RC", "F63.2", "R3264.2"]
+    assert recs[1][1] == "TTTTGGTAAGCAGAACTGGYG"
+
+
+def test_adapter_specs():
+    st = panel.AdapterSet()
+    st.add_spec("file:" + panel.SP5_FASTA, "front")
+    st.add_spec("ACGTu", "back")
+    st.add_spec("TNTC...GGAA", "front")
+    assert len(st.adapters) == 14
+    assert st.adapters[12].name == "1" and st.adapters[12].seq == "ACGTT"
+    assert isinstance(st.adapters[13], panel.LinkedAdapter) and st.adapters[13].name == "2"
+    with pytest.raises(ValueError):
+        panel.normalize("ACGZ")
+
+
+def test_synth_deterministic_and_shardable():
+    a = synth.generate("c2", n=300)
+    b = synth.generate("c2", n=100, first=200)
+    sa, sb = synth.to_strings(a), synth.to_strings(b)
+    assert sa[200:] == sb
+    assert np.array_equal(a["truth"][200:], b["truth"])
+
+
+def test_synthetic_24_panel_distance():
+    n1, s1, n2, s2 = synth.panels(24, 24)
+    assert len(set(s1)) == 24 and len(set(s2)) == 24
+    assert s1[:12] == panel.load_panel(panel.SP5_FASTA)[1]
+    assert all(s.startswith(s1[0][:25]) and s.endswith(s1[0][42:]) for s in s1)
