@@ -269,9 +269,9 @@ int dmx_set_panel(dmx_ctx* c, int round, const char* const* seqs, const int* len
         }
         const double rate = max_errors >= 1.0 ? max_errors / (double)m : max_errors;
         const int k = (int)(rate * m);
-        if (m + k + 2 > kRingSmall) hp.ring_small = false;
-        if (m + k + 2 > kRingLarge) {
-            c->err = "error rate too high for the resolve window (m + k + 2 > 128)";
+        if (m + k + 2 + 4 > kRingSmall) hp.ring_small = false;
+        if (m + k + 2 + 4 > kRingLarge) {
+            c->err = "error rate too high for the resolve window (m + k + 6 > 128)";
             return DMX_E_UNSUPPORTED;
         }
         int ncount[kMaxLen + 1];

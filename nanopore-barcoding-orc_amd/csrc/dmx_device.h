@@ -25,7 +25,7 @@ namespace dmx {
 
 constexpr int kMaxAdapters = 64;
 constexpr int kMaxLen = 64;       // adapter length limit: one 64-bit Myers word
-constexpr int kRingSmall = 68;    // resolve ring when every adapter has m + k + 2 <= 68
+constexpr int kRingSmall = 74;    // resolve ring when every adapter has m + k + 2 + 4 <= 74
 constexpr int kRingLarge = 128;   // otherwise (one 64-lane block per CU)
 constexpr int kScanBlock = 256;
 constexpr int kResolveBlock = 64;

@@ -122,6 +122,12 @@ __device__ __forceinline__ Cluster make_cluster(uint32_t item, int sub, uint32_t
     return c;
 }
 
+// Lower-bound key: the slot's best accepted score is >= lb, and a cell scoring exactly lb has a
+// cost <= cost (so an equal-score cell of higher cost can never win).  Max over tasks.
+__device__ __forceinline__ int lb_key(int lb, int cost) {
+    return lb > 0 ? (lb << 8) | (255 - cost) : 0;
+}
+
 // One task's Myers scan over view columns (js, jhi]; last-row candidates are reported for
 // columns in [jlo, jhi] only.  js == 0 with `real` uses cutadapt's column-0 initialisation;
 // otherwise the restricted start D'(i, js) = i, exact for every cell of cost <= k at column
@@ -136,15 +142,12 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
     const bool front = ad.where == kFront;
     const uint32_t hbit = (uint32_t)(m - 1);
     const uint32_t gap = (uint32_t)(m + ad.k + 1);
-    // FRONT cells beyond this column cannot start in column 0 (that would cost > k)
-    const uint32_t full_from = front ? (uint32_t)(m + ad.k + 1) : 0u;
-    const int acc_m = acc[m];
 
     uint64_t pv = (front && real) ? 0ull : ~0ull, mv = 0ull;
     int d = (front && real) ? 0 : m;
     bool have = false;
     uint32_t cj1 = 0, cj2 = 0;
-    int cub = -128, lb = 0;
+    int cub = -128, lbk = 0;   // lbk = (lower bound << 8) | (255 - its cost), 0 = none
 
 #define DMX_SCAN_STEP(q)                                                                  \
     {                                                                                     \
@@ -155,7 +158,10 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
             const int lr = min(m, (int)j + d);                                            \
             if (j >= jlo && d <= (int)pacc[lr]) {                                         \
                 const int ubc = lr - 2 * d;                                               \
-                if (j >= full_from && d <= acc_m) lb = max(lb, m - 3 * d);                \
+                {   /* certainly accepted: aligned length >= L0 and acc is monotone */       \
+                    const int L0 = min(m, (int)j - d);                                    \
+                    if (L0 >= 0 && d <= (int)acc[L0]) lbk = max(lbk, lb_key(L0 - 3 * d, d)); \
+                }                                                                         \
                 if (have && j - cj2 <= gap) {                                             \
                     cj2 = j;                                                              \
                     cub = max(cub, ubc);                                                  \
@@ -194,7 +200,7 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
             dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
             if (dd <= (int)acc[i]) {              // accepted for sure (aligned length is i)
                 ubl = max(ubl, i - 2 * dd);
-                lb = max(lb, i - 3 * dd);
+                lbk = max(lbk, lb_key(i - 3 * dd, dd));
             }
         }
         if (ubl > -128) {
@@ -208,7 +214,7 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
         }
     }
     if (have) st.push(make_cluster(item, sub, cj1, cj2, 0, cub));
-    return lb;
+    return lbk;
 }
 
 #define DMX_CLUSTER_STAGE                                                                 \
@@ -421,26 +427,38 @@ __global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
 // resolve: one lane per cluster; restricted Myers window + cutadapt tie-broken traceback.
 // The last RING columns of (Pv, Mv) and the read codes live in LDS, lane-interleaved.
 // ---------------------------------------------------------------------------------------------
+// The adapter's match vectors live in registers: Eq for a read code is a 3-level select.
+struct PeqRegs {
+    uint64_t p0, p1, p2, p3;
+    __device__ __forceinline__ uint64_t eq(uint32_t code) const {
+        const uint64_t a = (code & 1u) ? p1 : p0;
+        const uint64_t b = (code & 1u) ? p3 : p2;
+        const uint64_t e = (code & 2u) ? b : a;
+        return (code & 4u) ? 0ull : e;
+    }
+};
+
 template <int RING>
 struct Walker {
+    const uint32_t* seq;
+    const uint32_t* nmask;
     uint32_t* flags;
-    const uint64_t* peq;    // LDS, + adapter, stride A
-    int A;
+    TaskView tv;
+    PeqRegs peq;
     const uint64_t* rp;     // LDS ring (P): rp[slot * 64]
     const uint64_t* rm;
-    const uint8_t* rc;      // LDS ring of read codes: code of view position j-1 at slot(j)
     int js;
     bool real, front;
 
-    __device__ __forceinline__ int slot(int j) const { return (j - js) % RING; }
-
-    // Walk cutadapt's DP pointers from cell (i, j) back to the alignment start.
-    // Pointer rule (_align.pyx locate): equal characters -> diagonal; else mismatch if
-    // diag <= deletion and diag <= insertion; else insertion (up) if insertion <= deletion;
-    // else deletion (left).  Scores: +1 match, -1 mismatch, -2 indel.
-    __device__ void trace(int i, int j, int& origin, int& score) const {
+    // Walk cutadapt's DP pointers from cell (i, j) back to the alignment start; s0 = ring slot
+    // of column j.  Pointer rule (_align.pyx locate): equal characters -> diagonal; else
+    // mismatch if diag <= deletion and diag <= insertion; else insertion (up) if
+    // insertion <= deletion; else deletion (left).  Scores: +1 match, -1 mismatch, -2 indel.
+    // Runs of matches only touch registers; the ring is read at the <= k error cells.
+    __device__ void trace(int i, int j, int s0, int& origin, int& score) const {
         score = 0;
-        int s0 = slot(j);
+        int cbase = 1 << 30;          // view position of bit 0 of the cached 16-code chunk
+        uint32_t codes = 0, nb = 0;
         while (i > 0) {
             if (j == js) {
                 if (real) {
@@ -457,9 +475,15 @@ struct Walker {
                 }
                 return;
             }
+            const int p = j - 1;              // view position of column j's character
+            if (p < cbase) {
+                cbase = max(p - 15, 0);
+                fetch16(seq, nmask, tv.off, tv.n, tv.strand, tv.start, (uint32_t)cbase, codes, nb);
+            }
+            const int sh = p - cbase;
+            const uint32_t code = ((codes >> (2 * sh)) & 3u) | (((nb >> sh) & 1u) << 2);
             const int s1 = s0 == 0 ? RING - 1 : s0 - 1;
-            const uint32_t code = rc[s0 * 64];
-            if ((peq[code * A] >> (i - 1)) & 1ull) {
+            if ((peq.eq(code) >> (i - 1)) & 1ull) {
                 --i;
                 --j;
                 ++score;
@@ -488,37 +512,43 @@ struct Walker {
     }
 };
 
+// resolve: one lane per cluster.  The forward pass re-runs Myers over the cluster window and
+// keeps the last RING columns of (Pv, Mv) in LDS; candidate cells are only MARKED in a bitmask
+// and traced back at sync points every `sync` columns, so that all lanes of a wave walk their
+// tracebacks in lockstep (inline tracebacks at per-lane columns serialise the wave).
+// Dynamic LDS: ring P [RING*64] u64, ring M [RING*64] u64, acc [72*A], pacc [72*A].
 template <int RING>
 __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
-    __shared__ uint64_t s_peq[8 * kMaxAdapters];
-    __shared__ uint64_t s_rp[RING * kResolveBlock];
-    __shared__ uint64_t s_rm[RING * kResolveBlock];
-    __shared__ uint8_t s_rc[RING * kResolveBlock];
-    {
-        const int A = R.panel->n_adapters;
-        for (int x = threadIdx.x; x < 8 * A; x += blockDim.x)
-            s_peq[x] = R.panel->ad[x % A].peq[x / A];
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint64_t* s_rp = (uint64_t*)smem;
+    uint64_t* s_rm = s_rp + RING * kResolveBlock;
+    int8_t* s_acc = (int8_t*)(s_rm + RING * kResolveBlock);
+    const int A = R.panel->n_adapters;
+    int8_t* s_pacc = s_acc + 72 * A;
+    for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) {
+        s_acc[x] = R.panel->ad[x / 72].acc[x % 72];
+        s_pacc[x] = R.panel->ad[x / 72].pacc[x % 72];
     }
     __syncthreads();
 
-    const int A = R.panel->n_adapters;
     const uint32_t total = min(*R.cl_count, R.cl_cap);
     const int lane = threadIdx.x;
     uint32_t n_resolved = 0, n_traces = 0;
     uint64_t* rp = s_rp + lane;
     uint64_t* rm = s_rm + lane;
-    uint8_t* rcode = s_rc + lane;
 
     for (uint32_t ci = blockIdx.x * kResolveBlock + lane; ci < total;
          ci += gridDim.x * kResolveBlock) {
         const Cluster c = R.cl[ci];
         const uint32_t slot = slot_of(R, c.item, c.sub);
-        const int lbr = R.lb[slot];
+        const int lbk = R.lb[slot];
+        const int lbs = lbk ? (lbk >> 8) : -1000;    // slot's best score is >= lbs ...
+        const int lbc = 255 - (lbk & 255);            // ... reached with cost <= lbc
         Outcome out;
         out.key = ~0ull;
         out.origin = 0;
         out.pad = 0;
-        if ((int)c.ub < lbr) {            // cannot reach the slot's guaranteed best score
+        if ((int)c.ub < lbs) {            // cannot reach the slot's guaranteed best score
             R.outc[ci] = out;
             continue;
         }
@@ -528,9 +558,11 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
         const DevAdapter& ad = R.panel->ad[tv.a];
         const int m = ad.m, k = ad.k, kk = ad.kk;
         const bool front = ad.where == kFront;
+        const PeqRegs peq{ad.peq[0], ad.peq[1], ad.peq[2], ad.peq[3]};
         const uint64_t snapshot = R.winner[slot];
-        const int8_t* acc = ad.acc;       // global (L1/L2); rare-path reads only
-        const int8_t* pacc = ad.pacc;
+        const int8_t* acc = s_acc + 72 * tv.a;
+        const int8_t* pacc = s_pacc + 72 * tv.a;
+        const int sync = min(RING - (m + k + 2), 31);   // >= 4 by host-side ring choice
 
         int js = (int)c.j1 - m - k - 1;
         const bool real = js <= 0;
@@ -540,14 +572,19 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
         rp[0] = pv;                       // slot(js) = 0
         rm[0] = mv;
 
-        Walker<RING> W{R.flags, s_peq + tv.a, A, rp, rm, rcode, js, real, front};
+        const Walker<RING> W{R.seq, R.nmask, R.flags, tv, peq, rp, rm, js, real, front};
         bool found = false;
         int bs = 0, bc = 0, bo = 0;
         uint64_t bt = 0;
 
-        auto consider = [&](int iend, int j, int cost, uint64_t t) {
-            const int ub = min(iend, j + cost) - 2 * cost;   // score <= aligned length - 2 cost
-            if (ub < lbr) return;
+        // can a cell of cost `cost` whose aligned adapter length is <= lr still win the slot?
+        auto viable = [&](int lr, int cost) {
+            const int ub = lr - 2 * cost;   // score <= aligned length - 2 cost
+            return ub > lbs || (ub == lbs && cost <= lbc);
+        };
+        auto consider = [&](int iend, int j, int s, int cost, uint64_t t) {
+            const int ub = min(iend, j + cost) - 2 * cost;
+            if (!viable(min(iend, j + cost), cost)) return;
             if (found && (ub < bs || (ub == bs && cost >= bc))) return;
             if (make_key(ub, tv.o, cost, tv.a, t) > snapshot) return;
             int origin, score;
@@ -555,7 +592,7 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
                 origin = j - iend;            // (FRONT only when j < iend: reaches column 0)
                 score = j >= iend ? iend : j;
             } else {
-                W.trace(iend, j, origin, score);
+                W.trace(iend, j, s, origin, score);
                 ++n_traces;
             }
             const int lr = iend + (origin < 0 ? origin : 0);
@@ -570,31 +607,52 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
         };
 
         const uint32_t hbit = (uint32_t)(m - 1);
-        const uint64_t* peq = s_peq + tv.a;
-        int sl = 0;
+        int sl = 0;                       // ring slot of the current column
+        uint32_t pending = 0;             // candidate columns since the last sync (bit = age)
+        int since = 0;                    // columns since the last sync
+        uint32_t curj = (uint32_t)js;     // current column
+        // trace the marked cells, oldest first (locate's scan order), all lanes together
+        auto drain = [&]() {
+            while (pending) {
+                const int age = 31 - __clz(pending);          // oldest marked column
+                pending &= ~(1u << age);
+                const int sidx = sl - age < 0 ? sl - age + RING : sl - age;
+                const int j = (int)curj - age;
+                const int cost = col_cost(rp[sidx * 64], rm[sidx * 64], m);
+                consider(m, j, sidx, cost, (uint64_t)j);
+            }
+            since = 0;
+        };
+        uint32_t ncodes, nnb;             // next chunk, prefetched one chunk ahead
+        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, (uint32_t)js, ncodes, nnb);
         for (uint32_t p0 = (uint32_t)js; p0 < c.j2; p0 += 16) {
-            uint32_t codes, nb;
-            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
+            const uint32_t codes = ncodes, nb = nnb;
+            if (p0 + 16 < c.j2)
+                fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes, nnb);
             const uint32_t cnt = min(16u, c.j2 - p0);
             for (uint32_t q = 0; q < cnt; ++q) {
                 const uint32_t code = ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
-                myers_step(peq[code * A], pv, mv, d, hbit);
+                myers_step(peq.eq(code), pv, mv, d, hbit);
                 const uint32_t j = p0 + q + 1;
+                curj = j;
                 sl = sl == RING - 1 ? 0 : sl + 1;
                 rp[sl * 64] = pv;
                 rm[sl * 64] = mv;
-                rcode[sl * 64] = (uint8_t)code;
+                pending <<= 1;
                 if (j >= c.j1 && d <= kk) {
                     const int lr = min(m, (int)j + d);
-                    if (d <= (int)pacc[lr]) consider(m, (int)j, d, j);
+                    if (d <= (int)pacc[lr] && viable(lr, d)) pending |= 1u;
                 }
+                if (++since == sync) drain();
             }
         }
+        drain();
         if (c.lastcol && !front) {
             int dd = 0;
             for (int i = 1; i < m; ++i) {
                 dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
-                if (dd <= (int)acc[i]) consider(i, (int)tv.len, dd, (uint64_t)tv.len + 1 + i);
+                if (dd <= (int)acc[i])
+                    consider(i, (int)tv.len, sl, dd, (uint64_t)tv.len + 1 + i);
             }
         }
         if (found) {
@@ -811,12 +869,21 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         hipLaunchKernelGGL(scan_kernel, dim3(grid), dim3(kScanBlock), 0, st, R);
     }
     hipEventRecord(c->ev[round * 3 + 1], st);
+    const size_t tabs = (size_t)144 * hp.n;
+    static bool attr_set = false;
+    if (!attr_set) {   // dynamic LDS above 64 KiB must be allowed explicitly
+        hipFuncSetAttribute((const void*)resolve_kernel<kRingSmall>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)resolve_kernel<kRingLarge>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
     if (c->ring_small[round])
         hipLaunchKernelGGL(resolve_kernel<kRingSmall>, dim3(resolve_grid(c)), dim3(kResolveBlock),
-                           0, st, R);
+                           (size_t)kRingSmall * kResolveBlock * 16 + tabs, st, R);
     else
         hipLaunchKernelGGL(resolve_kernel<kRingLarge>, dim3(resolve_grid(c)), dim3(kResolveBlock),
-                           0, st, R);
+                           (size_t)kRingLarge * kResolveBlock * 16 + tabs, st, R);
     hipLaunchKernelGGL(select_kernel, dim3(1024), dim3(256), 0, st, R);
     hipEventRecord(c->ev[round * 3 + 2], st);
     return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
