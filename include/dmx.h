@@ -109,9 +109,10 @@ int dmx_counts(dmx_ctx* ctx, uint64_t* out_counts, size_t n_out);
 
 /* Diagnostics of the last dmx_exec: per-stage device time in ms measured with HIP events on the
  * context's stream (order: scan0, resolve0, finalize0, scan1, resolve1, finalize1, total), and
- * counts[8] = {candidate clusters r0, r1, filter windows r0, r1, clusters resolved after
- * pruning r0, r1, tracebacks r0, r1}, and flags
- * (bit0 cluster overflow, bit1 window violation, bit2 filter-window overflow; must be 0). */
+ * counts[8] = {candidate clusters r0, r1, filter windows r0, r1, candidate cells (band mode) or
+ * clusters resolved after pruning (ring mode) r0, r1, band DPs / tracebacks r0, r1}, and flags
+ * (bit0 cluster overflow, bit1 exactness-check violation, bit2 filter-window overflow, bit3
+ * candidate-cell overflow; must be 0). */
 int dmx_stats(dmx_ctx* ctx, float* stage_ms, int n_stage, uint64_t* clusters, int* flags);
 
 #ifdef __cplusplus

@@ -135,6 +135,16 @@ int ensure_pipeline(Ctx* c) {
         }
         c->cl_cap = want_cl;
     }
+    const size_t want_cand = 4 * std::max(slots0, n) + 65536;
+    if (c->cand_cap < want_cand) {
+        int rc;
+        for (int r = 0; r < 2; ++r)
+            for (int l = 0; l < 2; ++l) {
+                if ((rc = dev_alloc(c, &c->d_cand[r][l], want_cand))) return rc;
+                if ((rc = dev_alloc(c, &c->d_cand_out[r][l], want_cand))) return rc;
+            }
+        c->cand_cap = want_cand;
+    }
     const size_t want_win = 4 * 2 * std::max(slots0, n) + 65536;
     if (c->win_cap < want_win) {
         int rc;
@@ -148,6 +158,18 @@ int ensure_pipeline(Ctx* c) {
         if ((rc = dev_alloc(c, &c->d_counts, nc))) return rc;
         c->n_counts = nc;
     }
+    return DMX_OK;
+}
+
+int grow_cands(Ctx* c) {
+    const size_t want = c->cand_cap * 2;
+    int rc;
+    for (int r = 0; r < 2; ++r)
+        for (int l = 0; l < 2; ++l) {
+            if ((rc = dev_alloc(c, &c->d_cand[r][l], want))) return rc;
+            if ((rc = dev_alloc(c, &c->d_cand_out[r][l], want))) return rc;
+        }
+    c->cand_cap = want;
     return DMX_OK;
 }
 
@@ -188,6 +210,8 @@ int dmx_open(int device, dmx_ctx** out) {
     c->device = device;
     const char* nf = std::getenv("DMX_NO_FILTER");
     c->no_filter = nf && nf[0] == '1';
+    const char* rs = std::getenv("DMX_RESOLVE");
+    c->force_ring = rs && std::strcmp(rs, "ring") == 0;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -195,7 +219,7 @@ int dmx_open(int device, dmx_ctx** out) {
     }
     for (auto& e : c->ev) hipEventCreate(&e);
     for (int r = 0; r < 2; ++r) hipMalloc((void**)&c->d_panel[r], sizeof(DevPanel));
-    hipMalloc((void**)&c->d_counters, 16 * sizeof(uint32_t));
+    hipMalloc((void**)&c->d_counters, 32 * sizeof(uint32_t));
     *out = c;
     return DMX_OK;
 }
@@ -210,6 +234,11 @@ void dmx_close(dmx_ctx* c) {
                     c->d_counts,    c->d_panel[0],  c->d_panel[1]};
     for (void* b : bufs)
         if (b) hipFree(b);
+    for (int r = 0; r < 2; ++r)
+        for (int l = 0; l < 2; ++l) {
+            if (c->d_cand[r][l]) hipFree(c->d_cand[r][l]);
+            if (c->d_cand_out[r][l]) hipFree(c->d_cand_out[r][l]);
+        }
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
     hipStreamDestroy(c->stream);
@@ -349,6 +378,8 @@ int dmx_set_panel(dmx_ctx* c, int round, const char* const* seqs, const int* len
     }
     c->panel[round] = hp;
     c->ring_small[round] = hp.ring_small;
+    c->band_ok[round] = true;
+    for (int a = 0; a < n; ++a) c->band_ok[round] &= hp.ad[a].kk <= 7;
     for (int a = 0; a < n; ++a) dp.ad[a] = hp.ad[a];
     CK(hipSetDevice(c->device));
     CK(hipMemcpy(c->d_panel[round], &dp, sizeof(dp), hipMemcpyHostToDevice));
@@ -441,7 +472,7 @@ int dmx_exec(dmx_ctx* c) {
     if (rc) return rc;
     hipStream_t st = c->stream;
     CK(hipEventRecord(c->ev[8], st));
-    CK(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(uint32_t), st));
+    CK(hipMemsetAsync(c->d_counters, 0, 32 * sizeof(uint32_t), st));
     CK(hipMemsetAsync(c->d_counts, 0, c->n_counts * sizeof(unsigned long long), st));
     CK(hipMemsetAsync(c->d_winner[0], 0xFF, c->n_reads * sizeof(unsigned long long), st));
     if ((rc = launch_round(c, 0, st))) return rc;
@@ -508,22 +539,28 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* clusters, int*
     }
     hipEventElapsedTime(&t[6], c->ev[8], c->ev[6 + rounds - 1]);
     for (int i = 0; i < n_stage && i < 7; ++i) stage_ms[i] = t[i];
-    uint32_t cnt[12];
+    uint32_t cnt[32];
     CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
+    if (getenv("DMX_DEBUG_STATS"))
+        fprintf(stderr, "dmx stats: resolve max window %u %u, total window columns %u %u\n",
+                cnt[18], cnt[22], cnt[19], cnt[23]);
     if (clusters) {
         clusters[0] = cnt[0];
         clusters[1] = cnt[1];
         clusters[2] = cnt[4];
         clusters[3] = cnt[5];
-        clusters[4] = cnt[8];
-        clusters[5] = cnt[10];
-        clusters[6] = cnt[9];
-        clusters[7] = cnt[11];
+        const bool b0 = c->band_ok[0] && !c->force_ring, b1 = c->band_ok[1] && !c->force_ring;
+        clusters[4] = b0 ? (uint64_t)cnt[6] + cnt[7] : cnt[16];
+        clusters[5] = b1 ? (uint64_t)cnt[8] + cnt[9] : cnt[20];
+        clusters[6] = cnt[17];
+        clusters[7] = cnt[21];
     }
     if (flags) {
         int f = (int)cnt[3];
         if (cnt[0] > c->cl_cap || cnt[1] > c->cl_cap) f |= 1;
         if (cnt[4] > c->win_cap || cnt[5] > c->win_cap) f |= 4;
+        for (int x = 6; x < 10; ++x)
+            if (cnt[x] > c->cand_cap) f |= 8;
         *flags = f;
     }
     return DMX_OK;
@@ -543,10 +580,11 @@ int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint
             c->err = "internal: traceback left the exact window (please report)";
             return DMX_E_STATE;
         }
-        if (!(flags & 5)) return dmx_fetch(c, out);
+        if (!(flags & 13)) return dmx_fetch(c, out);
         // candidate overflow: retry with more room, never truncate
         if ((flags & 1) && (rc = grow_clusters(c))) return rc;
         if ((flags & 4) && (rc = grow_windows(c))) return rc;
+        if ((flags & 8) && (rc = grow_cands(c))) return rc;
     }
     c->err = "candidate cluster buffer overflow";
     return DMX_E_NOMEM;

@@ -79,13 +79,14 @@ struct Window {
 static_assert(sizeof(Window) == 40, "Window layout");
 
 constexpr int kStageCap = 256;    // LDS staging of emitted records per block
+constexpr int kCandStageCap = 128; // per candidate list
 
 // Block-level staging of appended records: lanes append to LDS (LDS atomics), the block then
 // reserves its range of the global list with ONE global atomic.  A single global counter
 // hammered by every lane serialises at the memory side (MI355X_MICROARCH.md, 'fanin').
-template <typename Rec>
+template <typename Rec, int CAP = kStageCap>
 struct Stage {
-    Rec* buf;              // LDS [kStageCap]
+    Rec* buf;              // LDS [CAP]
     uint32_t* cnt;         // LDS
     uint32_t* base;        // LDS scratch
     Rec* g;
@@ -96,7 +97,7 @@ struct Stage {
 
     __device__ __forceinline__ void push(const Rec& r) const {
         const uint32_t i = atomicAdd(cnt, 1u);
-        if (i < (uint32_t)kStageCap) {
+        if (i < (uint32_t)CAP) {
             buf[i] = r;
             return;
         }
@@ -107,7 +108,7 @@ struct Stage {
     // Every thread of the block must call flush().
     __device__ __forceinline__ void flush() const {
         __syncthreads();
-        const uint32_t n = min(*cnt, (uint32_t)kStageCap);
+        const uint32_t n = min(*cnt, (uint32_t)CAP);
         if (threadIdx.x == 0) *base = n ? atomicAdd(gcount, n) : 0u;
         __syncthreads();
         const uint32_t b = *base;
@@ -139,6 +140,20 @@ struct Cluster {      // candidate columns [j1, j2] of one task (item, orientati
     int8_t ub;        // upper bound of the score of any cell of the cluster
     uint32_t j1, j2;
 };
+
+// One candidate end cell (band mode): the window scan knows its exact cost; the band kernel
+// recovers cutadapt's origin and score for it.  Carries the oriented view (no dependent loads).
+struct Cand {
+    uint32_t item;
+    uint16_t sub;
+    uint8_t iend;        // end row (m for last-row cells, i < m for last-column cells)
+    uint8_t cost;
+    uint32_t j;          // end column
+    uint32_t n, start, len;
+    uint8_t strand, o, a, pad;
+    uint64_t off;
+};
+static_assert(sizeof(Cand) == 40, "Cand layout");
 
 struct Outcome {      // best cell found by the resolve lane of a cluster
     uint64_t key;     // ~0 = none

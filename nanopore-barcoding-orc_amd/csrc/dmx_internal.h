@@ -42,15 +42,20 @@ struct Ctx {
     int32_t* d_origin[2] = {nullptr, nullptr};
     int32_t* d_lb[2] = {nullptr, nullptr};
     bool ring_small[2] = {true, true};
+    bool band_ok[2] = {true, true};   // every adapter has kk <= 7: banded resolve
+    bool force_ring = false;          // DMX_RESOLVE=ring (A/B testing)
     size_t slot_cap = 0;
     Cluster* d_cl[2] = {nullptr, nullptr};
     Outcome* d_outc[2] = {nullptr, nullptr};
     size_t cl_cap = 0;
+    Cand* d_cand[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    Outcome* d_cand_out[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    size_t cand_cap = 0;
     Window* d_win = nullptr;
     size_t win_cap = 0;
     ItemView* d_items = nullptr;
     size_t item_cap = 0;
-    uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows
+    uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows, [6+2r..] candidates, [16+4r..] diag
     unsigned long long* d_counts = nullptr;
     size_t n_counts = 0;
     hipEvent_t ev[9] = {};

@@ -37,6 +37,11 @@ struct RoundArgs {
     uint32_t* win_count;
     uint32_t win_cap;
     uint32_t* diag;              // [0] resolved clusters, [1] tracebacks
+    int32_t band;                // 1: emit candidate cells (band kernels), 0: clusters (ring)
+    Cand* cand[2];               // candidate lists: [0] cost <= 3 (band 7), [1] cost 4..7 (15)
+    Outcome* cand_out[2];
+    uint32_t* cand_count;        // [2]
+    uint32_t cand_cap;
 };
 
 struct TaskView {
@@ -176,15 +181,17 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
     }
 
     uint32_t p0 = js;
+    uint32_t ncodes, nnb;             // next chunk, prefetched one chunk ahead
+    fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb);
     for (; p0 + 16 <= jhi; p0 += 16) {
-        uint32_t codes, nb;
-        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
+        const uint32_t codes = ncodes, nb = nnb;
+        if (p0 + 16 < jhi)
+            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes, nnb);
 #pragma unroll
         for (int q = 0; q < 16; ++q) DMX_SCAN_STEP(q)
     }
     if (p0 < jhi) {
-        uint32_t codes, nb;
-        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
+        const uint32_t codes = ncodes, nb = nnb;
         const int cnt = (int)(jhi - p0);
         for (int q = 0; q < cnt; ++q) DMX_SCAN_STEP(q)
     }
@@ -217,6 +224,178 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
     return lbk;
 }
 
+// Band mode: the same scan, but candidate END CELLS are emitted (after pruning with this
+// task's own score lower bound), each carrying its exact cost; no clusters, no resolve pass.
+struct CandSink {
+    Stage<Cand, kCandStageCap> st[2];
+};
+
+__device__ __forceinline__ Cand make_cand(const TaskView& tv, uint32_t item, int sub, int iend,
+                                          int cost, uint32_t j) {
+    Cand c;
+    c.item = item;
+    c.sub = (uint16_t)sub;
+    c.iend = (uint8_t)iend;
+    c.cost = (uint8_t)cost;
+    c.j = j;
+    c.n = tv.n;
+    c.start = tv.start;
+    c.len = tv.len;
+    c.strand = (uint8_t)tv.strand;
+    c.o = (uint8_t)tv.o;
+    c.a = (uint8_t)tv.a;
+    c.pad = 0;
+    c.off = tv.off;
+    return c;
+}
+
+// can a cell of cost `cost` whose aligned adapter length is <= lr beat the lower-bound key?
+__device__ __forceinline__ bool viable_lb(int lbk, int lr, int cost) {
+    if (!lbk) return true;
+    const int lbs = lbk >> 8, lbc = 255 - (lbk & 255);
+    const int ub = lr - 2 * cost;
+    return ub > lbs || (ub == lbs && cost <= lbc);
+}
+
+__device__ __forceinline__ void flush_cands(const CandSink& sink, const TaskView& tv, uint32_t item,
+                                         int sub, int m, int lbk, uint32_t seg, uint64_t cm,
+                                         uint64_t c0, uint64_t c1, uint64_t c2) {
+    while (cm) {
+        const int bit = __ffsll((unsigned long long)cm) - 1;
+        cm &= cm - 1;
+        const int cost = (int)((c0 >> bit) & 1ull) | ((int)((c1 >> bit) & 1ull) << 1) |
+                         ((int)((c2 >> bit) & 1ull) << 2);
+        const uint32_t j = seg + (uint32_t)bit;
+        if (!viable_lb(lbk, min(m, (int)j + cost), cost)) continue;
+        const Cand cd = make_cand(tv, item, sub, m, cost, j);
+        if (cost <= 3) sink.st[0].push(cd);
+        else sink.st[1].push(cd);
+    }
+}
+
+__device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const CandSink& sink,
+                                              const TaskView& tv, uint32_t item, int sub,
+                                              const uint64_t* peq, int A, const DevAdapter& ad,
+                                              const int8_t* acc, const int8_t* pacc,
+                                              uint32_t js, bool real, uint32_t jlo,
+                                              uint32_t jhi, bool lastcol) {
+    const int m = ad.m;
+    const int kk = ad.kk;   // <= 7 in band mode (three cost planes)
+    const bool front = ad.where == kFront;
+    const uint32_t hbit = (uint32_t)(m - 1);
+
+    uint64_t pv = (front && real) ? 0ull : ~0ull, mv = 0ull;
+    int d = (front && real) ? 0 : m;
+    int lbk = 0;
+    bool segset = false;
+    uint32_t seg = 0;
+    uint64_t cm = 0, c0 = 0, c1 = 0, c2 = 0;
+
+#define DMX_CAND_STEP(q)                                                                  \
+    {                                                                                     \
+        const uint32_t code = ((codes >> (2 * (q))) & 3u) | (((nb >> (q)) & 1u) << 2);    \
+        myers_step(peq[code * A], pv, mv, d, hbit);                                       \
+        if (d <= kk) {                                                                    \
+            const uint32_t j = p0 + (q) + 1;                                              \
+            const int lr = min(m, (int)j + d);                                            \
+            if (j >= jlo && d <= (int)pacc[lr]) {                                         \
+                {   /* certainly accepted: aligned length >= L0 and acc is monotone */       \
+                    const int L0 = min(m, (int)j - d);                                    \
+                    if (L0 >= 0 && d <= (int)acc[L0]) lbk = max(lbk, lb_key(L0 - 3 * d, d)); \
+                }                                                                         \
+                if (!segset) {                                                            \
+                    segset = true;                                                        \
+                    seg = j;                                                              \
+                }                                                                         \
+                const uint64_t bm = 1ull << (j - seg);                                    \
+                cm |= bm;                                                                 \
+                if (d & 1) c0 |= bm;                                                      \
+                if (d & 2) c1 |= bm;                                                      \
+                if (d & 4) c2 |= bm;                                                      \
+            }                                                                             \
+        }                                                                                 \
+    }
+
+    uint32_t p0 = js;
+    uint32_t ncodes, nnb;             // next chunk, prefetched one chunk ahead
+    fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb);
+    for (; p0 + 16 <= jhi; p0 += 16) {
+        const uint32_t codes = ncodes, nb = nnb;
+        if (p0 + 16 < jhi)
+            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes, nnb);
+        if (segset && p0 + 16 >= seg + 64) {   // this chunk could overflow the 64-bit segment
+            flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
+            segset = false;
+            cm = c0 = c1 = c2 = 0;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) DMX_CAND_STEP(q)
+    }
+    if (p0 < jhi) {
+        const uint32_t codes = ncodes, nb = nnb;
+        if (segset && p0 + 16 >= seg + 64) {
+            flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
+            segset = false;
+            cm = c0 = c1 = c2 = 0;
+        }
+        const int cnt = (int)(jhi - p0);
+        for (int q = 0; q < cnt; ++q) DMX_CAND_STEP(q)
+    }
+#undef DMX_CAND_STEP
+    // 3' adapters: last-column cells (adapter prefix aligned at the read end)
+    uint64_t rows = 0;
+    const uint32_t len = tv.len;
+    if (lastcol && !front && len > 0) {
+        int dd = 0;
+        for (int i = 1; i < m; ++i) {
+            dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
+            if (dd <= (int)acc[i]) {              // accepted for sure (aligned length is i)
+                rows |= 1ull << i;
+                lbk = max(lbk, lb_key(i - 3 * dd, dd));
+            }
+        }
+    }
+    if (cm) flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
+    while (rows) {                                // scan order: after every last-row cell
+        const int i = __ffsll((unsigned long long)rows) - 1;
+        rows &= rows - 1;
+        const int cost = col_cost(pv, mv, i);
+        if (!viable_lb(lbk, i, cost)) continue;
+        const Cand cd = make_cand(tv, item, sub, i, cost, len);
+        if (cost <= 3) sink.st[0].push(cd);
+        else sink.st[1].push(cd);
+    }
+    return lbk;
+}
+
+#define DMX_CAND_STAGE                                                                    \
+    __shared__ Cand s_cand[2][kCandStageCap];                                             \
+    __shared__ uint32_t s_ccnt[2], s_cbase[2];                                            \
+    if (threadIdx.x < 2) s_ccnt[threadIdx.x] = 0;                                         \
+    const CandSink sink{{Stage<Cand, kCandStageCap>{s_cand[0], &s_ccnt[0], &s_cbase[0],    \
+                                                    R.cand[0], R.cand_count, R.cand_cap,   \
+                                                    R.flags, 8u},                          \
+                         Stage<Cand, kCandStageCap>{s_cand[1], &s_ccnt[1], &s_cbase[1],    \
+                                                    R.cand[1], R.cand_count + 1,           \
+                                                    R.cand_cap, R.flags, 8u}}};
+
+// Both kernels are templated on BAND; only the stage the instantiation uses takes LDS.
+#define DMX_STAGES                                                                        \
+    __shared__ Cluster s_cl[BAND ? 1 : kStageCap];                                        \
+    __shared__ uint32_t s_clcnt, s_clbase;                                                \
+    if (threadIdx.x == 0) s_clcnt = 0;                                                    \
+    const Stage<Cluster> st{s_cl, &s_clcnt, &s_clbase, R.cl, R.cl_count, R.cl_cap,        \
+                            R.flags, 1u};                                                 \
+    __shared__ Cand s_cand[2][BAND ? kCandStageCap : 1];                                  \
+    __shared__ uint32_t s_ccnt[2], s_cbase[2];                                            \
+    if (threadIdx.x < 2) s_ccnt[threadIdx.x] = 0;                                         \
+    const CandSink sink{{Stage<Cand, kCandStageCap>{s_cand[0], &s_ccnt[0], &s_cbase[0],    \
+                                                    R.cand[0], R.cand_count, R.cand_cap,   \
+                                                    R.flags, 8u},                          \
+                         Stage<Cand, kCandStageCap>{s_cand[1], &s_ccnt[1], &s_cbase[1],    \
+                                                    R.cand[1], R.cand_count + 1,           \
+                                                    R.cand_cap, R.flags, 8u}}};
+
 #define DMX_CLUSTER_STAGE                                                                 \
     __shared__ Cluster s_cl[kStageCap];                                                   \
     __shared__ uint32_t s_clcnt, s_clbase;                                                \
@@ -225,11 +404,12 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
                             R.flags, 1u};
 
 // Full scan (panels without a usable shared suffix): one lane per (item, orientation, adapter).
+template <bool BAND>
 __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kMaxAdapters];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
     __shared__ int8_t s_pacc[72 * kMaxAdapters];
-    DMX_CLUSTER_STAGE
+    DMX_STAGES
     load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
     __syncthreads();
 
@@ -243,12 +423,21 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
     if (tid < rpb * T && item < n_items) {
         TaskView tv;
         task_view(R, item, sub, A, tv);
-        const int lb = scan_task(R, st, tv, item, sub, s_peq + tv.a, A, R.panel->ad[tv.a],
-                                 s_acc + 72 * tv.a, s_pacc + 72 * tv.a, 0, true, 1, tv.len,
-                                 true);
+        int lb;
+        if constexpr (BAND)
+            lb = scan_task_cand(R, sink, tv, item, sub, s_peq + tv.a, A, R.panel->ad[tv.a],
+                                s_acc + 72 * tv.a, s_pacc + 72 * tv.a, 0, true, 1, tv.len, true);
+        else
+            lb = scan_task(R, st, tv, item, sub, s_peq + tv.a, A, R.panel->ad[tv.a],
+                           s_acc + 72 * tv.a, s_pacc + 72 * tv.a, 0, true, 1, tv.len, true);
         if (lb > 0) atomicMax(&R.lb[slot_of(R, item, sub)], lb);
     }
-    st.flush();
+    if constexpr (BAND) {
+        sink.st[0].flush();
+        sink.st[1].flush();
+    } else {
+        st.flush();
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -257,7 +446,7 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
 // grouped into windows.  A lane that finishes a view takes the block's next one, so lanes of a
 // wave stay busy however unequal the read lengths are.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kFilterViewsPerBlock = 1024;
+constexpr uint32_t kFilterViewsPerBlock = 512;
 constexpr int kFilterChunksPerRound = 12;
 
 __device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskView& tv,
@@ -315,10 +504,12 @@ __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
     int b = 0;
     bool have = false;
     uint32_t w1 = 0, w2 = 0;
+    uint32_t ncodes = 0, nnb = 0;
     auto start_view = [&]() {
         item = v / (uint32_t)no;
         o = (int)(v % (uint32_t)no);
         task_view(R, item, o * A, A, tv);
+        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, 0, ncodes, nnb);
         pv = front ? 0u : ~0u;
         mv = 0u;
         b = front ? 0 : L;
@@ -349,8 +540,9 @@ __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
     // its staged windows (a uniform point), so the LDS staging never overflows in practice.
     while (__syncthreads_or(active)) {
         for (int it = 0; it < kFilterChunksPerRound && active; ++it) {
-            uint32_t codes, nb;
-            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, codes, nb);
+            const uint32_t codes = ncodes, nb = nnb;
+            if (p0 + 16 < tv.len)          // prefetch the next chunk of this view
+                fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes, nnb);
             if (p0 + 16 <= tv.len) {
 #pragma unroll
                 for (int q = 0; q < 16; ++q) DMX_FILTER_STEP(q)
@@ -381,12 +573,13 @@ __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
 }
 
 // Window scan: one lane per (window, adapter); block-uniform grid-stride over the device-side
-// window count so that the block can flush its staged clusters between strides.
+// window count so that the block can flush its staged records between strides.
+template <bool BAND>
 __global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kMaxAdapters];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
     __shared__ int8_t s_pacc[72 * kMaxAdapters];
-    DMX_CLUSTER_STAGE
+    DMX_STAGES
     load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
     __syncthreads();
 
@@ -412,15 +605,32 @@ __global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
             int js = (int)w.j1 - (int)ad.m - (int)ad.k - 1;
             const bool real = js <= 0;
             if (real) js = 0;
-            const int lb = scan_task(R, st, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
-                                     s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2,
-                                     w.lastcol != 0);
+            int lb;
+            if constexpr (BAND)
+                lb = scan_task_cand(R, sink, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
+                                    s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2,
+                                    w.lastcol != 0);
+            else
+                lb = scan_task(R, st, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
+                               s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2, w.lastcol != 0);
             if (lb > 0) atomicMax(&R.lb[slot_of(R, w.item, sub)], lb);
         }
-        __syncthreads();                             // make the staged count block-uniform
-        if (s_clcnt > kStageCap / 2) st.flush();
+        __syncthreads();                             // make the staged counts block-uniform
+        if constexpr (BAND) {
+            if (s_ccnt[0] > kCandStageCap / 2 || s_ccnt[1] > kCandStageCap / 2) {
+                sink.st[0].flush();
+                sink.st[1].flush();
+            }
+        } else {
+            if (s_clcnt > kStageCap / 2) st.flush();
+        }
     }
-    st.flush();
+    if constexpr (BAND) {
+        sink.st[0].flush();
+        sink.st[1].flush();
+    } else {
+        st.flush();
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -667,6 +877,174 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
     if (n_traces) atomicAdd(R.diag + 1, n_traces);
 }
 
+// ---------------------------------------------------------------------------------------------
+// resolve (banded): no ring.  Every optimal path to an end cell x of cost c stays within c
+// diagonals of x's diagonal (each indel moves one diagonal), and every cell that decides the
+// tie-broken path (a minimum option of a path cell) lies on such a path, so the full DP
+// (cost, origin, score) restricted to the 2H+1 diagonals around x (H >= c), evaluated from row 0
+// with cutadapt's initialisation, reproduces cutadapt's origin and score of x exactly
+// (DESIGN.md §3.5).  The band lives in registers: no LDS, full occupancy, no traceback.
+// ---------------------------------------------------------------------------------------------
+// 16 codes of view positions [p, p+16) for a possibly negative p (positions outside the view
+// are fetched from the padding and never used).
+__device__ __forceinline__ void fetch16s(const uint32_t* __restrict__ seq,
+                                         const uint32_t* __restrict__ nmask, const TaskView& tv,
+                                         int p, uint32_t& codes, uint32_t& nbits) {
+    if (tv.strand == 0) {
+        const uint64_t g = (uint64_t)((int64_t)tv.off + (int64_t)tv.start + p);
+        codes = window32(seq, 2 * g);
+        nbits = window32(nmask, g) & 0xFFFFu;
+    } else {
+        const uint64_t b = (uint64_t)((int64_t)tv.off + (int64_t)tv.n - 1 - (int64_t)tv.start -
+                                      p - 15);
+        codes = ~rev_pairs(window32(seq, 2 * b));
+        nbits = __brev(window32(nmask, b)) >> 16;
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void band_dp(const PeqRegs& peq, const uint32_t* seq,
+                                        const uint32_t* nmask, const TaskView& tv, bool front,
+                                        int ie, int je, int& cost, int& origin, int& score) {
+    constexpr int H = W / 2;
+    constexpr int INF = 1 << 20;
+    const int dx = je - ie;            // diagonal of the end cell; cell k <-> diagonal dx-H+k
+    const int n = (int)tv.len;
+    int C[W], O[W], S[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) {      // row 0: free start in the read
+        const int jj = dx - H + k;
+        C[k] = (jj >= 0 && jj <= n) ? 0 : INF;
+        O[k] = jj;
+        S[k] = 0;
+    }
+    uint32_t codes, nb;                // codes of row i: positions i + dx - H - 1 + k
+    fetch16s(seq, nmask, tv, dx - H, codes, nb);
+    for (int i = 1; i <= ie; ++i) {
+        uint32_t ncodes = 0, nnb = 0;  // prefetch next row's window
+        if (i < ie) fetch16s(seq, nmask, tv, i + dx - H, ncodes, nnb);
+        const uint32_t b = (uint32_t)(i - 1);
+        const uint32_t rmask = (uint32_t)((peq.p0 >> b) & 1ull) |
+                               ((uint32_t)((peq.p1 >> b) & 1ull) << 1) |
+                               ((uint32_t)((peq.p2 >> b) & 1ull) << 2) |
+                               ((uint32_t)((peq.p3 >> b) & 1ull) << 3);
+        int lc = INF, lo = 0, ls = 0;  // left neighbour (same row, already updated)
+        // in place, ascending k: C[k] is still the diagonal (row i-1), C[k+1] the cell above.
+        // Branch-free: the pointer rule becomes three selects.
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            const int jj = i + dx - H + k;
+            const int uc = (k + 1 < W) ? C[(k + 1) % W] : INF;
+            const int uo = (k + 1 < W) ? O[(k + 1) % W] : 0;
+            const int us = (k + 1 < W) ? S[(k + 1) % W] : 0;
+            const uint32_t code = (codes >> (2 * k)) & 3u;
+            const bool eq = !((nb >> k) & 1u) && ((rmask >> code) & 1u);
+            const bool take_diag = eq || (C[k] <= lc && C[k] <= uc);   // match or mismatch
+            const bool take_up = uc <= lc;                              // insertion vs deletion
+            const int ic = take_up ? uc : lc;
+            const int io = take_up ? uo : lo;
+            const int is = take_up ? us : ls;
+            int c = take_diag ? C[k] + (eq ? 0 : 1) : ic + 1;
+            int o = take_diag ? O[k] : io;
+            int sc = take_diag ? S[k] + (eq ? 1 : -1) : is - 2;
+            const bool col0 = jj == 0;                 // column 0: cutadapt's initialisation
+            c = col0 ? (front ? 0 : i) : c;
+            o = col0 ? (front ? -i : 0) : o;
+            sc = col0 ? (front ? 0 : -2 * i) : sc;
+            c = (jj < 0 || jj > n) ? INF : min(c, INF);
+            C[k] = c;
+            O[k] = o;
+            S[k] = sc;
+            lc = c;
+            lo = o;
+            ls = sc;
+        }
+        codes = ncodes;
+        nb = nnb;
+    }
+    cost = C[H];
+    origin = O[H];
+    score = S[H];
+}
+
+// Band kernel: one lane per candidate cell of one list (fixed band width W for the whole list,
+// so every lane of a wave runs the same code).  The slot's best is the minimum key over all its
+// candidates (key order = locate's / best_match's / ReverseComplementer's selection order).
+template <int W>
+__global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
+    const uint32_t total = min(R.cand_count[list], R.cand_cap);
+    const Cand* cl = R.cand[list];
+    Outcome* outs = R.cand_out[list];
+    uint32_t n_dp = 0;
+    for (uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x; ci < total;
+         ci += gridDim.x * blockDim.x) {
+        const Cand c = cl[ci];
+        const uint32_t slot = slot_of(R, c.item, c.sub);
+        const int cost = c.cost, iend = c.iend;
+        const int j = (int)c.j;
+        const DevAdapter& ad = R.panel->ad[c.a];
+        const int m = ad.m;
+        const uint64_t t = iend == m ? (uint64_t)j : (uint64_t)c.len + 1 + iend;
+        Outcome out;
+        out.key = ~0ull;
+        out.origin = 0;
+        out.pad = 0;
+        const int lrmax = min(iend, j + cost);
+        const int ub = lrmax - 2 * cost;
+        if (viable_lb(R.lb[slot], lrmax, cost) &&
+            make_key(ub, c.o, cost, c.a, t) <= R.winner[slot]) {
+            int origin, score;
+            if (cost == 0) {                  // exact: the pointer chain is the pure diagonal
+                origin = j - iend;
+                score = j >= iend ? iend : j;
+            } else {
+                TaskView tv;
+                tv.read = 0;
+                tv.n = c.n;
+                tv.strand = c.strand;
+                tv.start = c.start;
+                tv.len = c.len;
+                tv.off = c.off;
+                tv.o = c.o;
+                tv.a = c.a;
+                const PeqRegs peq{ad.peq[0], ad.peq[1], ad.peq[2], ad.peq[3]};
+                int c2;
+                band_dp<W>(peq, R.seq, R.nmask, tv, ad.where == kFront, iend, j, c2, origin,
+                           score);
+                ++n_dp;
+                if (c2 != cost) atomicOr(R.flags, 2u);    // band / scan disagreement: bug
+            }
+            const int lr = iend + (origin < 0 ? origin : 0);
+            if (lr >= 0 && cost <= (int)ad.acc[lr]) {
+                out.key = make_key(score, c.o, cost, c.a, t);
+                out.origin = origin;
+                atomicMin(&R.winner[slot], (unsigned long long)out.key);
+            }
+        }
+        outs[ci] = out;
+    }
+    __shared__ uint32_t s_n;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    if (n_dp) atomicAdd(&s_n, n_dp);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_n) atomicAdd(R.diag + 1, s_n);
+}
+
+__global__ void select_cand_kernel(RoundArgs R) {
+    for (int list = 0; list < 2; ++list) {
+        const uint32_t total = min(R.cand_count[list], R.cand_cap);
+        for (uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x; ci < total;
+             ci += gridDim.x * blockDim.x) {
+            const Outcome o = R.cand_out[list][ci];
+            if (o.key == ~0ull) continue;
+            const Cand c = R.cand[list][ci];
+            const uint32_t slot = slot_of(R, c.item, c.sub);
+            if (R.winner[slot] == o.key) R.origin[slot] = o.origin;
+        }
+    }
+}
+
 // select: the cluster whose outcome is the slot's winner publishes its origin.
 __global__ void select_kernel(RoundArgs R) {
     const uint32_t total = min(*R.cl_count, R.cl_cap);
@@ -855,20 +1233,37 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
 
     const uint32_t rpb = kScanBlock / R.T;
     const uint32_t grid = (uint32_t)((R.n_items + rpb - 1) / rpb);
-    R.diag = c->d_counters + 8 + 2 * round;
+    R.diag = c->d_counters + 16 + 4 * round;
     R.win = c->d_win;
     R.win_count = c->d_counters + 4 + round;
     R.win_cap = (uint32_t)c->win_cap;
+    const bool band = c->band_ok[round] && !c->force_ring;
+    R.band = band ? 1 : 0;
+    for (int l = 0; l < 2; ++l) {
+        R.cand[l] = c->d_cand[round][l];
+        R.cand_out[l] = c->d_cand_out[round][l];
+    }
+    R.cand_count = c->d_counters + 6 + 2 * round;
+    R.cand_cap = (uint32_t)c->cand_cap;
     hipEventRecord(c->ev[round * 3 + 0], st);
     if (hp.filter) {
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
         const uint32_t fgrid = (uint32_t)((nviews + kFilterViewsPerBlock - 1) / kFilterViewsPerBlock);
         if (fgrid > 0) hipLaunchKernelGGL(filter_kernel, dim3(fgrid), dim3(kScanBlock), 0, st, R);
-        hipLaunchKernelGGL(wscan_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
+        if (band) hipLaunchKernelGGL(wscan_kernel<true>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
+        else hipLaunchKernelGGL(wscan_kernel<false>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
     } else if (grid > 0) {
-        hipLaunchKernelGGL(scan_kernel, dim3(grid), dim3(kScanBlock), 0, st, R);
+        if (band) hipLaunchKernelGGL(scan_kernel<true>, dim3(grid), dim3(kScanBlock), 0, st, R);
+        else hipLaunchKernelGGL(scan_kernel<false>, dim3(grid), dim3(kScanBlock), 0, st, R);
     }
     hipEventRecord(c->ev[round * 3 + 1], st);
+    if (band) {
+        hipLaunchKernelGGL(band_cand_kernel<7>, dim3(256 * 8), dim3(256), 0, st, R, 0);
+        hipLaunchKernelGGL(band_cand_kernel<15>, dim3(256 * 4), dim3(256), 0, st, R, 1);
+        hipLaunchKernelGGL(select_cand_kernel, dim3(1024), dim3(256), 0, st, R);
+        hipEventRecord(c->ev[round * 3 + 2], st);
+        return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
+    }
     const size_t tabs = (size_t)144 * hp.n;
     static bool attr_set = false;
     if (!attr_set) {   // dynamic LDS above 64 KiB must be allowed explicitly

@@ -130,3 +130,14 @@ def test_error_rates_and_filter_toggle(ctx, e, monkeypatch):
         c2.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC, e)
         c2.set_mode(lib.MODE_TWO_ROUND)
         _assert_same(c2.run(lib.pack(d["blob"], d["offsets"], d["lengths"])), exp)
+
+
+@pytest.mark.parametrize("mode", ["band", "ring"])
+def test_resolve_kernels_agree(mode, monkeypatch):
+    """Both resolve kernels (banded DP / LDS-ring traceback) reproduce the oracle."""
+    if mode == "ring":
+        monkeypatch.setenv("DMX_RESOLVE", "ring")
+    d = synth.generate("c2", n=8000, seed=77)
+    exp = _oracle_two_round(d)
+    with lib.Context(0) as c:
+        _assert_same(_gpu_two_round(c, d), exp)
