@@ -149,6 +149,7 @@ int ensure_pipeline(Ctx* c) {
     if (c->win_cap < want_win) {
         int rc;
         if ((rc = dev_alloc(c, &c->d_win, want_win))) return rc;
+        if ((rc = dev_alloc(c, &c->d_win2, want_win))) return rc;
         c->win_cap = want_win;
     }
     const size_t a1 = c->mode == DMX_MODE_SINGLE ? 0 : (size_t)c->panel[1].n;
@@ -177,6 +178,7 @@ int grow_windows(Ctx* c) {
     const size_t want = c->win_cap * 2;
     int rc;
     if ((rc = dev_alloc(c, &c->d_win, want))) return rc;
+    if ((rc = dev_alloc(c, &c->d_win2, want))) return rc;
     c->win_cap = want;
     return DMX_OK;
 }
@@ -210,6 +212,8 @@ int dmx_open(int device, dmx_ctx** out) {
     c->device = device;
     const char* nf = std::getenv("DMX_NO_FILTER");
     c->no_filter = nf && nf[0] == '1';
+    const char* nv = std::getenv("DMX_NO_VERIFY");
+    c->no_verify = nv && nv[0] == '1';
     const char* rs = std::getenv("DMX_RESOLVE");
     c->force_ring = rs && std::strcmp(rs, "ring") == 0;
     if (hipSetDevice(device) != hipSuccess ||
@@ -230,7 +234,7 @@ void dmx_close(dmx_ctx* c) {
     hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_seq,       c->d_nmask,     c->d_offs,     c->d_lens,      c->d_res,
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
-                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_counters,
+                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_counters,
                     c->d_counts,    c->d_panel[0],  c->d_panel[1]};
     for (void* b : bufs)
         if (b) hipFree(b);
@@ -375,6 +379,29 @@ int dmx_set_panel(dmx_ctx* c, int round, const char* const* seqs, const int* len
         }
         dp.kf = kf;
         dp.max_mk = mk;
+        // shared prefix for the verification pass
+        int pre = lens[0];
+        int mmin = 1 << 30, mmax = 0;
+        for (int a = 0; a < n; ++a) {
+            int l = 0;
+            while (l < pre && l < lens[a] && seqs[a][l] == seqs[0][l]) ++l;
+            pre = l;
+            mmin = std::min(mmin, lens[a]);
+            mmax = std::max(mmax, lens[a]);
+        }
+        pre = std::min(pre, 32);
+        if (pre >= kMinFilterLen && pre + flen <= mmin && !c->no_verify) {
+            hp.verify = true;
+            dp.pre_len = pre;
+            dp.off_min = mmin - pre;
+            dp.off_max = mmax - pre;
+            dp.m_max = mmax;
+            for (int i = 0; i < pre; ++i) {
+                const uint8_t mask = iupac_mask(seqs[0][i]);
+                for (int code = 0; code < 4; ++code)
+                    if (mask & (1u << code)) dp.pre_peq[code] |= 1u << i;
+            }
+        }
     }
     c->panel[round] = hp;
     c->ring_small[round] = hp.ring_small;
@@ -547,8 +574,8 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* clusters, int*
     if (clusters) {
         clusters[0] = cnt[0];
         clusters[1] = cnt[1];
-        clusters[2] = cnt[4];
-        clusters[3] = cnt[5];
+        clusters[2] = c->panel[0].verify ? cnt[10] : cnt[4];
+        clusters[3] = c->panel[1].verify ? cnt[11] : cnt[5];
         const bool b0 = c->band_ok[0] && !c->force_ring, b1 = c->band_ok[1] && !c->force_ring;
         clusters[4] = b0 ? (uint64_t)cnt[6] + cnt[7] : cnt[16];
         clusters[5] = b1 ? (uint64_t)cnt[8] + cnt[9] : cnt[20];
@@ -559,6 +586,7 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* clusters, int*
         int f = (int)cnt[3];
         if (cnt[0] > c->cl_cap || cnt[1] > c->cl_cap) f |= 1;
         if (cnt[4] > c->win_cap || cnt[5] > c->win_cap) f |= 4;
+        if (cnt[10] > c->win_cap || cnt[11] > c->win_cap) f |= 4;
         for (int x = 6; x < 10; ++x)
             if (cnt[x] > c->cand_cap) f |= 8;
         *flags = f;

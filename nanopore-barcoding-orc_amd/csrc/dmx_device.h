@@ -62,6 +62,14 @@ struct DevPanel {
     int32_t max_mk;      // max over adapters of m + k + 1
     uint32_t filter_peq[8];
     int8_t pf[72];       // max over adapters of pacc[L]
+    // Shared-prefix verification (0 = disabled): the first `pre_len` (<= 32) characters are common
+    // to every adapter and pre_len + filter_len <= min m, so a full alignment of cost c ending at
+    // column j costs >= b(j) + min D_pre(j') over j' in [j - off_max - c, j - off_min + c]
+    // (off = m - pre_len), and a 3' last-column cell needs the prefix near the read end.
+    int32_t pre_len;
+    int32_t off_min, off_max;
+    int32_t m_max;
+    uint32_t pre_peq[8];
     DevAdapter ad[kMaxAdapters];
 };
 
@@ -71,8 +79,8 @@ struct Window {
     uint8_t o;
     uint8_t lastcol;     // 3' panel: window ends at the final column (last-column cells)
     uint8_t strand;      // oriented view of the item (copied so the window scan needs no
-    uint8_t pad;         // dependent loads): strand, start, len, read length n, first nt off
-    uint32_t j1, j2;     // candidate end columns [j1, j2]
+    uint8_t bmin;        // dependent loads): strand, start, len, read length n, first nt off;
+    uint32_t j1, j2;     // bmin = min suffix-block cost over the hits (255 = no hit)
     uint32_t n, start, len, pad2;
     uint64_t off;
 };

@@ -16,6 +16,7 @@ struct HostPanel {
     bool set = false;
     bool ring_small = true;
     bool filter = false;
+    bool verify = false;
     DevAdapter ad[kMaxAdapters];
 };
 
@@ -25,6 +26,7 @@ struct Ctx {
     std::string err;
     int mode = DMX_MODE_SINGLE;
     bool no_filter = false;   // DMX_NO_FILTER=1: always full scans (A/B testing)
+    bool no_verify = false;   // DMX_NO_VERIFY=1: skip the shared-prefix window verification
     HostPanel panel[2];
     DevPanel* d_panel[2] = {nullptr, nullptr};
 
@@ -52,10 +54,11 @@ struct Ctx {
     Outcome* d_cand_out[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
     size_t cand_cap = 0;
     Window* d_win = nullptr;
+    Window* d_win2 = nullptr;
     size_t win_cap = 0;
     ItemView* d_items = nullptr;
     size_t item_cap = 0;
-    uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows, [6+2r..] candidates, [16+4r..] diag
+    uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows, [6+2r..] candidates, [10+r] verified windows, [16+4r..] diag
     unsigned long long* d_counts = nullptr;
     size_t n_counts = 0;
     hipEvent_t ev[9] = {};

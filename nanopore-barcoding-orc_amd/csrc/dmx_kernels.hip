@@ -36,6 +36,8 @@ struct RoundArgs {
     Window* win;
     uint32_t* win_count;
     uint32_t win_cap;
+    Window* win2;                // verified windows (when the panel has a shared prefix)
+    uint32_t* win2_count;
     uint32_t* diag;              // [0] resolved clusters, [1] tracebacks
     int32_t band;                // 1: emit candidate cells (band kernels), 0: clusters (ring)
     Cand* cand[2];               // candidate lists: [0] cost <= 3 (band 7), [1] cost 4..7 (15)
@@ -450,13 +452,13 @@ constexpr uint32_t kFilterViewsPerBlock = 512;
 constexpr int kFilterChunksPerRound = 12;
 
 __device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskView& tv,
-                                              uint32_t j1, uint32_t j2, int lastcol) {
+                                              uint32_t j1, uint32_t j2, int lastcol, int bmin) {
     Window w;
     w.item = item;
     w.o = (uint8_t)o;
     w.lastcol = (uint8_t)lastcol;
     w.strand = (uint8_t)tv.strand;
-    w.pad = 0;
+    w.bmin = (uint8_t)min(bmin, 255);
     w.j1 = j1;
     w.j2 = j2;
     w.n = tv.n;
@@ -504,6 +506,7 @@ __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
     int b = 0;
     bool have = false;
     uint32_t w1 = 0, w2 = 0;
+    int wb = 255;
     uint32_t ncodes = 0, nnb = 0;
     auto start_view = [&]() {
         item = v / (uint32_t)no;
@@ -527,10 +530,12 @@ __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
             if (j + (uint32_t)kf >= 71u || b <= (int)s_pf[j + kf]) {                      \
                 if (have && j - w2 <= gap) {                                              \
                     w2 = j;                                                               \
+                    wb = min(wb, b);                                                      \
                 } else {                                                                  \
-                    if (have) st.push(make_window(item, o, tv, w1, w2, 0));               \
+                    if (have) st.push(make_window(item, o, tv, w1, w2, 0, wb));           \
                     have = true;                                                          \
                     w1 = w2 = j;                                                          \
+                    wb = b;                                                               \
                 }                                                                         \
             }                                                                             \
         }                                                                                 \
@@ -554,14 +559,14 @@ __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
                 const uint32_t len = tv.len;
                 if (!front && len > 0) {
                     if (have && len - w2 <= gap) {
-                        st.push(make_window(item, o, tv, w1, len, 1));
+                        st.push(make_window(item, o, tv, w1, len, 1, wb));
                     } else {
-                        if (have) st.push(make_window(item, o, tv, w1, w2, 0));
-                        st.push(make_window(item, o, tv, len, len, 1));
+                        if (have) st.push(make_window(item, o, tv, w1, w2, 0, wb));
+                        st.push(make_window(item, o, tv, len, len, 1, 255));
                     }
                     have = false;
                 }
-                if (have) st.push(make_window(item, o, tv, w1, w2, 0));
+                if (have) st.push(make_window(item, o, tv, w1, w2, 0, wb));
                 v = atomicAdd(&s_next, 1u);
                 active = v < vend;
                 if (active) start_view();
@@ -570,6 +575,98 @@ __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
         st.flush();
     }
 #undef DMX_FILTER_STEP
+}
+
+// ---------------------------------------------------------------------------------------------
+// verify: one lane per filter window; 32-bit Myers of the shared PREFIX block over the columns
+// where the prefix of an alignment ending in the window would end.  Keeps the window only if
+//   (rows) some full alignment ending in [j1, j2] could cost <= kf: bmin + min D_pre <= kf
+//          (FRONT windows near the read start may hold partial alignments: always kept), or
+//   (end)  3' last-column cells: an adapter prefix of length i at the read end costs
+//          D_pre(i, len) for i < pre_len, or contains the whole prefix block ending within
+//          m_max - 1 - pre_len + kf columns of the end.
+// Survivors are compacted into the second window list for the window scan.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
+    __shared__ Window s_w[kStageCap];
+    __shared__ uint32_t s_wc, s_wb;
+    __shared__ int8_t s_pf[72];
+    if (threadIdx.x == 0) s_wc = 0;
+    const DevPanel* P = R.panel;
+    if (threadIdx.x < 72) s_pf[threadIdx.x] = P->pf[threadIdx.x];
+    __syncthreads();
+    const Stage<Window> st{s_w, &s_wc, &s_wb, R.win2, R.win2_count, R.win_cap, R.flags, 4u};
+    const bool front = P->where == kFront;
+    const int L = P->pre_len, kf = P->kf;
+    const uint32_t total = min(*R.win_count, R.win_cap);
+    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
+        const uint32_t wi = base + threadIdx.x;
+        if (wi < total) {
+            const Window w = R.win[wi];
+            const int len = (int)w.len;
+            const bool rows_free = (front && (int)w.j1 <= P->max_mk) || w.bmin == 255;
+            // column ranges the prefix block must be evaluated on
+            int lo = 1 << 30, hi = -1;
+            if (!rows_free) {
+                lo = (int)w.j1 - P->off_max - kf;
+                hi = (int)w.j2 - P->off_min + kf;
+            }
+            const int end_lo = len - (P->m_max - 1 - L + kf);
+            if (w.lastcol) {
+                lo = min(lo, end_lo);
+                hi = len;
+            }
+            bool keep = rows_free && w.bmin != 255;    // near-start FRONT window: keep as is
+            if (!keep && hi >= 0) {
+                lo = max(lo, 0);
+                hi = min(hi, len);
+                TaskView tv;
+                tv.read = 0;
+                tv.n = w.n;
+                tv.strand = w.strand;
+                tv.start = w.start;
+                tv.len = w.len;
+                tv.off = w.off;
+                tv.o = w.o;
+                tv.a = 0;
+                int js = lo - L - kf - 1;              // restricted start: exact from lo on
+                if (js < 0) js = 0;
+                uint32_t pv = ~0u, mv = 0u;
+                int d = L;
+                int dmin_rows = 1 << 20, dmin_end = 1 << 20;
+                const uint32_t hbit = (uint32_t)(L - 1);
+                const int rlo = w.bmin == 255 ? (1 << 30) : (int)w.j1 - P->off_max - kf;
+                const int rhi = (int)w.j2 - P->off_min + kf;
+                for (int p0 = js; p0 < hi; p0 += 16) {
+                    uint32_t codes, nb;
+                    fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, (uint32_t)p0, codes,
+                            nb);
+                    const int cnt = min(16, hi - p0);
+                    for (int q = 0; q < cnt; ++q) {
+                        const uint32_t code = ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
+                        myers_step32(P->pre_peq[code], pv, mv, d, hbit);
+                        const int j = p0 + q + 1;
+                        if (j >= rlo && j <= rhi) dmin_rows = min(dmin_rows, d);
+                        if (j >= end_lo) dmin_end = min(dmin_end, d);
+                    }
+                }
+                if (!rows_free && (int)w.bmin + dmin_rows <= kf) keep = true;
+                if (w.lastcol) {
+                    if (dmin_end <= kf) keep = true;                  // whole prefix block at end
+                    int dd = 0;                                       // prefix cells at column len
+                    for (int i = 1; i < L && !keep; ++i) {
+                        dd += (int)((pv >> (i - 1)) & 1u) - (int)((mv >> (i - 1)) & 1u);
+                        if (dd <= (int)s_pf[i]) keep = true;
+                    }
+                    if (hi == 0) keep = true;                         // empty view: trivial
+                }
+            }
+            if (keep) st.push(w);
+        }
+        __syncthreads();
+        if (s_wc > kStageCap / 2) st.flush();
+    }
+    st.flush();
 }
 
 // Window scan: one lane per (window, adapter); block-uniform grid-stride over the device-side
@@ -584,12 +681,14 @@ __global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
     __syncthreads();
 
     const int A = R.panel->n_adapters;
-    const uint64_t total = (uint64_t)min(*R.win_count, R.win_cap) * (uint64_t)A;
+    const Window* wl = R.panel->pre_len ? R.win2 : R.win;
+    const uint32_t* wc = R.panel->pre_len ? R.win2_count : R.win_count;
+    const uint64_t total = (uint64_t)min(*wc, R.win_cap) * (uint64_t)A;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < total;
          base += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t t = base + threadIdx.x;
         if (t < total) {
-            const Window w = R.win[t / A];
+            const Window w = wl[t / A];
             const int a = (int)(t % A);
             const int sub = w.o * A + a;
             TaskView tv;
@@ -1236,6 +1335,8 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     R.diag = c->d_counters + 16 + 4 * round;
     R.win = c->d_win;
     R.win_count = c->d_counters + 4 + round;
+    R.win2 = c->d_win2;
+    R.win2_count = c->d_counters + 10 + round;
     R.win_cap = (uint32_t)c->win_cap;
     const bool band = c->band_ok[round] && !c->force_ring;
     R.band = band ? 1 : 0;
@@ -1250,6 +1351,8 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
         const uint32_t fgrid = (uint32_t)((nviews + kFilterViewsPerBlock - 1) / kFilterViewsPerBlock);
         if (fgrid > 0) hipLaunchKernelGGL(filter_kernel, dim3(fgrid), dim3(kScanBlock), 0, st, R);
+        if (hp.verify)
+            hipLaunchKernelGGL(verify_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
         if (band) hipLaunchKernelGGL(wscan_kernel<true>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(wscan_kernel<false>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
     } else if (grid > 0) {
