@@ -76,6 +76,11 @@ int dmx_abi_version(void);
  * an adapter iff it has a non-ACGT character (cutadapt default). */
 int dmx_set_panel(dmx_ctx* ctx, int round, const char* const* seqs, const int* lens,
                   int n_adapters, double max_errors, int min_overlap, int flags);
+/* As dmx_set_panel, with a per-adapter DMX_FRONT / DMX_BACK (one cutadapt call mixing -g and -a,
+ * scripts/04_cleaning_primers.sh:476-507); rc: 1 for --rc. */
+int dmx_set_panel_mixed(dmx_ctx* ctx, int round, const char* const* seqs, const int* lens,
+                        const int* wheres, int n_adapters, double max_errors, int min_overlap,
+                        int rc);
 int dmx_set_mode(dmx_ctx* ctx, int mode);
 
 /* Host-side packer (no GPU needed): ASCII reads -> 2-bit codes (A=0,C=1,G=2,T=3, 16 nt per

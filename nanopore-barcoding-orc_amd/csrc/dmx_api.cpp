@@ -265,8 +265,27 @@ int dmx_set_mode(dmx_ctx* c, int mode) {
     return DMX_OK;
 }
 
+static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const int* lens,
+                          const int* wheres, int n, double max_errors, int min_overlap,
+                          int flags);
+
 int dmx_set_panel(dmx_ctx* c, int round, const char* const* seqs, const int* lens, int n,
                   double max_errors, int min_overlap, int flags) {
+    return set_panel_impl(c, round, seqs, lens, nullptr, n, max_errors, min_overlap, flags);
+}
+
+int dmx_set_panel_mixed(dmx_ctx* c, int round, const char* const* seqs, const int* lens,
+                        const int* wheres, int n, double max_errors, int min_overlap, int rc) {
+    if (!wheres) return DMX_E_INVALID;
+    for (int a = 0; a < n; ++a)
+        if (wheres[a] != DMX_FRONT && wheres[a] != DMX_BACK) return DMX_E_INVALID;
+    return set_panel_impl(c, round, seqs, lens, wheres, n, max_errors, min_overlap,
+                          DMX_FRONT | (rc ? DMX_RC : 0));
+}
+
+static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const int* lens,
+                          const int* wheres, int n, double max_errors, int min_overlap,
+                          int flags) {
     if (!c || round < 0 || round > 1 || !seqs || !lens) return DMX_E_INVALID;
     if (n <= 0 || n > kMaxAdapters) {
         c->err = "panel must hold 1..64 adapters";
@@ -341,7 +360,8 @@ int dmx_set_panel(dmx_ctx* c, int round, const char* const* seqs, const int* len
         ad.m = (uint8_t)m;
         ad.k = (uint8_t)k;
         ad.kk = (int8_t)std::min(kk, k);
-        ad.where = (flags & DMX_FRONT) ? kFront : kBack;
+        ad.where = wheres ? (wheres[a] == DMX_FRONT ? kFront : kBack)
+                          : ((flags & DMX_FRONT) ? kFront : kBack);
     }
     hp.set = true;
     DevPanel dp;
@@ -349,6 +369,8 @@ int dmx_set_panel(dmx_ctx* c, int round, const char* const* seqs, const int* len
     dp.n_adapters = hp.n;
     dp.n_orient = hp.n_orient;
     dp.where = hp.ad[0].where;
+    for (int a = 1; a < n; ++a)
+        if (hp.ad[a].where != hp.ad[0].where) dp.where = 0;
     // Shared-suffix filter block: the longest suffix common to every adapter (<= 32 chars).
     int common = lens[0];
     for (int a = 1; a < n; ++a) {

@@ -26,7 +26,7 @@ RESULT_DTYPE = np.dtype([("bin1", "<i2"), ("bin2", "<i2"), ("rc1", "u1"), ("rc2"
 assert RESULT_DTYPE.itemsize == 40
 
 EXPORTS = ["dmx_abi_version", "dmx_open", "dmx_close", "dmx_last_error", "dmx_set_panel",
-           "dmx_set_mode", "dmx_pack_words", "dmx_pack", "dmx_run", "dmx_load", "dmx_exec",
+           "dmx_set_panel_mixed", "dmx_set_mode", "dmx_pack_words", "dmx_pack", "dmx_run", "dmx_load", "dmx_exec",
            "dmx_sync", "dmx_fetch", "dmx_counts", "dmx_stats"]
 
 
@@ -55,6 +55,9 @@ def load() -> ctypes.CDLL:
     L.dmx_last_error.restype = ctypes.c_char_p
     L.dmx_set_panel.argtypes = [P, c_int, ctypes.POINTER(ctypes.c_char_p),
                                 ctypes.POINTER(c_int), c_int, ctypes.c_double, c_int, c_int]
+    L.dmx_set_panel_mixed.argtypes = [P, c_int, ctypes.POINTER(ctypes.c_char_p),
+                                      ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int,
+                                      ctypes.c_double, c_int, c_int]
     L.dmx_set_mode.argtypes = [P, c_int]
     L.dmx_pack_words.argtypes = [ctypes.c_uint64, c_size]
     L.dmx_pack_words.restype = c_size
@@ -147,6 +150,17 @@ class Context:
         lens = (ctypes.c_int * len(seqs))(*[len(s) for s in seqs])
         self._check(self._L.dmx_set_panel(self._h, rnd, arr, lens, len(seqs), float(max_errors),
                                           int(min_overlap), int(flags)), "dmx_set_panel")
+        self.panel_sizes[rnd] = len(seqs)
+
+    def set_panel_mixed(self, rnd: int, seqs, wheres, rc: bool, max_errors: float = 0.1,
+                        min_overlap: int = 3):
+        """Per-adapter DMX_FRONT / DMX_BACK (a cutadapt call mixing -g and -a)."""
+        arr = (ctypes.c_char_p * len(seqs))(*[s.encode("ascii") for s in seqs])
+        lens = (ctypes.c_int * len(seqs))(*[len(s) for s in seqs])
+        wh = (ctypes.c_int * len(seqs))(*wheres)
+        self._check(self._L.dmx_set_panel_mixed(self._h, rnd, arr, lens, wh, len(seqs),
+                                                float(max_errors), int(min_overlap), int(rc)),
+                    "dmx_set_panel_mixed")
         self.panel_sizes[rnd] = len(seqs)
 
     def set_mode(self, mode: int):

@@ -1,0 +1,71 @@
+"""The drop-in CLI replaying scripts/02_cutadapt_loop.sh's command sequence on the GPU; every
+output file is compared record-for-record with outputs rendered from the oracle."""
+import glob
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from dmx import panel, synth
+from helpers import CLI, oracle_round, random_quals, read_fastq, write_fastq
+
+pytestmark = pytest.mark.gpu
+
+
+def test_02_cutadapt_loop_dropin(tmp_path):
+    d = synth.generate("c2", n=3000, seed=12)
+    seqs = synth.to_strings(d)
+    rng = np.random.default_rng(3)
+    names = [f"read{i} runid=abc ch={i % 512}" for i in range(len(seqs))]
+    quals = random_quals(rng, [len(s) for s in seqs])
+    ds = "sample1"
+    pych = tmp_path / "pychopped"
+    pych.mkdir()
+    infile = str(pych / f"pychopped_{ds}.fastq.gz")
+    write_fastq(infile, names, seqs, quals)
+    out = tmp_path / "demuxed"
+    (out / "SP5").mkdir(parents=True)
+    (out / "SP27").mkdir()
+    env = dict(os.environ)
+    # round 1 (02_cutadapt_loop.sh:64-72)
+    subprocess.run([CLI, "--action=trim", "-e", "0.1", "-j", "4", "--rc",
+                    "-g", f"file:{panel.SP5_FASTA}", "-o", f"{out}/SP5/{{name}}_{ds}.fastq.gz",
+                    infile, f"--json={out}/SP5/cutadapt_SP5_{ds}.json"], check=True, env=env,
+                   stdout=subprocess.DEVNULL)
+    suffix = f"_{ds}.fastq.gz"
+    ids = sorted(os.path.basename(f)[:-len(suffix)] for f in glob.glob(f"{out}/SP5/*{suffix}")
+                 if "unknown" not in f)
+    # round 2 (02_cutadapt_loop.sh:91-103)
+    for ident in ids:
+        subprocess.run([CLI, "--action=trim", "-e", "0.1", "-j", "4", "--rc",
+                        "-a", f"file:{panel.SP27RC_FASTA}",
+                        "-o", f"{out}/SP27/{{name}}_{ident}_{ds}.fastq.gz",
+                        f"{out}/SP5/{ident}_{ds}.fastq.gz", f"--json={out}/SP27/{ident}_{ds}.json"],
+                       check=True, env=env, stdout=subprocess.DEVNULL)
+
+    n5, s5 = panel.load_panel(panel.SP5_FASTA)
+    n27, s27 = panel.load_panel(panel.SP27RC_FASTA)
+    assert ids == n5    # every SP5 output exists (created even if empty)
+    records = [("@" + n, s, q) for n, s, q in zip(names, seqs, quals)]
+    exp1 = oracle_round(records, s5, oracle.FRONT, True)
+    got_unknown = read_fastq(f"{out}/SP5/unknown{suffix}")
+    assert got_unknown == [(("@" + n), s, q) for n, s, q in exp1.get(-1, [])]
+    total2 = 0
+    for a, ident in enumerate(n5):
+        exp_bin = exp1.get(a, [])
+        got_bin = read_fastq(f"{out}/SP5/{ident}{suffix}")
+        assert got_bin == [("@" + n, s, q) for n, s, q in exp_bin], ident
+        exp2 = oracle_round([("@" + n, s, q) for n, s, q in exp_bin], s27, oracle.BACK, True)
+        for b, name27 in enumerate(n27):
+            got = read_fastq(f"{out}/SP27/{name27}_{ident}{suffix}")
+            assert got == [("@" + n, s, q) for n, s, q in exp2.get(b, [])], (ident, name27)
+            total2 += len(got)
+    assert total2 > 0.6 * len(seqs)
+    import json
+    rep = json.load(open(f"{out}/SP5/cutadapt_SP5_{ds}.json"))
+    assert rep["read_counts"]["input"] == len(seqs)
+    assert rep["read_counts"]["read1_with_adapter"] == sum(len(v) for k, v in exp1.items()
+                                                          if k >= 0)
+    assert [a["name"] for a in rep["adapters_read1"]] == n5
