@@ -121,6 +121,7 @@ int ensure_pipeline(Ctx* c) {
             if ((rc = dev_alloc(c, &c->d_lb[r], s))) return rc;
         }
         if ((rc = dev_alloc(c, &c->d_items, items))) return rc;
+        if ((rc = dev_alloc(c, &c->d_linked, n))) return rc;
         c->slot_cap = s;
         c->item_cap = items;
         c->cap_reads = n;
@@ -234,7 +235,7 @@ void dmx_close(dmx_ctx* c) {
     hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_seq,       c->d_nmask,     c->d_offs,     c->d_lens,      c->d_res,
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
-                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_counters,
+                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_counters,
                     c->d_counts,    c->d_panel[0],  c->d_panel[1]};
     for (void* b : bufs)
         if (b) hipFree(b);
@@ -256,10 +257,6 @@ int dmx_set_mode(dmx_ctx* c, int mode) {
     if (mode != DMX_MODE_SINGLE && mode != DMX_MODE_TWO_ROUND && mode != DMX_MODE_LINKED) {
         c->err = "unknown mode";
         return DMX_E_INVALID;
-    }
-    if (mode == DMX_MODE_LINKED) {
-        c->err = "linked mode is not implemented on the GPU path yet";
-        return DMX_E_UNSUPPORTED;
     }
     c->mode = mode;
     return DMX_OK;
@@ -523,11 +520,13 @@ int dmx_exec(dmx_ctx* c) {
     CK(hipEventRecord(c->ev[8], st));
     CK(hipMemsetAsync(c->d_counters, 0, 32 * sizeof(uint32_t), st));
     CK(hipMemsetAsync(c->d_counts, 0, c->n_counts * sizeof(unsigned long long), st));
-    CK(hipMemsetAsync(c->d_winner[0], 0xFF, c->n_reads * sizeof(unsigned long long), st));
+    const size_t slots0 = c->mode == DMX_MODE_LINKED ? c->n_reads * (size_t)c->panel[0].n
+                                                     : c->n_reads;
+    CK(hipMemsetAsync(c->d_winner[0], 0xFF, slots0 * sizeof(unsigned long long), st));
     if ((rc = launch_round(c, 0, st))) return rc;
     if ((rc = launch_finalize(c, 0, st))) return rc;
-    if (c->mode == DMX_MODE_TWO_ROUND) {
-        CK(hipMemsetAsync(c->d_winner[1], 0xFF, c->n_reads * sizeof(unsigned long long), st));
+    if (c->mode != DMX_MODE_SINGLE) {
+        CK(hipMemsetAsync(c->d_winner[1], 0xFF, c->item_cap * sizeof(unsigned long long), st));
         if ((rc = launch_round(c, 1, st))) return rc;
         if ((rc = launch_finalize(c, 1, st))) return rc;
     }

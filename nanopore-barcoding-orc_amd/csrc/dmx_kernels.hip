@@ -1200,7 +1200,90 @@ struct FinalArgs {
     int32_t mode;
     int32_t A0, A1;             // adapters per panel
     unsigned long long* counts; // (A0+1)*(A1+1) + 2
+    // linked mode
+    const unsigned long long* winner0;   // per (read, pair) front winners
+    const int32_t* origin0;
+    unsigned long long* linked_best;     // per read: best pair key
 };
+
+// ---------------------------------------------------------------------------------------------
+// linked adapters (-g F...R; adapters.py LinkedAdapter.match_to, both parts required):
+//   round 0: one winner per (read, pair) = the front primer's own best cell on the read;
+//   round 1: each pair with a front match scans its back primer on read[front.rstop:];
+//   combine: best pair by summed score, then summed errors, then pair order.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void finalize0_linked_kernel(FinalArgs F) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= F.n_reads) return;
+    dmx_result out;
+    out.bin1 = out.bin2 = -1;
+    out.rc1 = out.rc2 = 0;
+    out.flags = 0;
+    out._pad = 0;
+    out.m1 = dmx_match{0, 0, 0, 0, 0, 0};
+    out.m2 = out.m1;
+    F.res[r] = out;
+    F.linked_best[r] = ~0ull;
+    const uint32_t n = F.lens[r];
+    for (int a = 0; a < F.A0; ++a) {
+        const uint64_t key = F.winner[(size_t)r * F.A0 + a];
+        if (key == ~0ull) continue;
+        dmx_match m;
+        int aa, o;
+        decode_match(key, F.origin[(size_t)r * F.A0 + a], n, F.p0, m, aa, o);
+        ItemView v;
+        v.read = r;
+        v.strand = 0;
+        v.pad = 0;
+        v.only_adapter = (int16_t)a;
+        v.start = (uint32_t)m.rstop;
+        v.len = n - (uint32_t)m.rstop;
+        const uint32_t idx = atomicAdd(F.n_items, 1u);
+        F.items[idx] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void finalize1_linked_kernel(FinalArgs F) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *F.n_items) return;
+    const ItemView v = F.items[i];
+    const uint64_t kb = F.winner[i];
+    if (kb == ~0ull) return;
+    const int a = v.only_adapter;
+    const uint64_t kf = F.winner0[(size_t)v.read * F.A0 + a];
+    const int sum = key_score(kf) + key_score(kb);
+    const int err = key_cost(kf) + key_cost(kb);
+    const uint64_t ck = ((uint64_t)(511 - sum) << 54) | ((uint64_t)err << 46) |
+                        ((uint64_t)a << 38) | (uint64_t)i;
+    atomicMin(&F.linked_best[v.read], (unsigned long long)ck);
+}
+
+__global__ __launch_bounds__(256) void finalize2_linked_kernel(FinalArgs F) {
+    __shared__ unsigned int s_hist[kMaxAdapters + 1];
+    for (int x = threadIdx.x; x <= F.A0; x += blockDim.x) s_hist[x] = 0;
+    __syncthreads();
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < F.n_reads) {
+        const uint64_t ck = F.linked_best[r];
+        int b = -1;
+        if (ck != ~0ull) {
+            const uint32_t i = (uint32_t)(ck & ((1ull << 38) - 1));
+            const int a = (int)((ck >> 38) & 255);
+            const ItemView v = F.items[i];
+            dmx_result& out = F.res[r];
+            int aa, o;
+            decode_match(F.winner0[(size_t)r * F.A0 + a], F.origin0[(size_t)r * F.A0 + a],
+                         F.lens[r], F.p0, out.m1, aa, o);
+            decode_match(F.winner[i], F.origin[i], v.len, F.p1, out.m2, aa, o);
+            out.bin1 = out.bin2 = (int16_t)a;
+            b = a;
+        }
+        atomicAdd(&s_hist[b + 1], 1u);
+    }
+    __syncthreads();
+    for (int x = threadIdx.x; x <= F.A0; x += blockDim.x)
+        if (s_hist[x]) atomicAdd(&F.counts[x * (F.A0 + 1) + x], (unsigned long long)s_hist[x]);
+}
 
 // Round 0 epilogue (one thread per read): write m1/bin1, build the round-1 view (the
 // round-0-trimmed sequence: FRONT -> view[rstop:], BACK -> view[:rstart]) and queue it.
@@ -1347,7 +1430,7 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     R.cand_count = c->d_counters + 6 + 2 * round;
     R.cand_cap = (uint32_t)c->cand_cap;
     hipEventRecord(c->ev[round * 3 + 0], st);
-    if (hp.filter) {
+    if (hp.filter && !linked) {   // linked primers: short, no shared suffix block; plain scan
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
         const uint32_t fgrid = (uint32_t)((nviews + kFilterViewsPerBlock - 1) / kFilterViewsPerBlock);
         if (fgrid > 0) hipLaunchKernelGGL(filter_kernel, dim3(fgrid), dim3(kScanBlock), 0, st, R);
@@ -1402,6 +1485,21 @@ int launch_finalize(Ctx* c, int round, hipStream_t st) {
     F.A0 = c->panel[0].n;
     F.A1 = c->mode == DMX_MODE_SINGLE ? 0 : c->panel[1].n;
     F.counts = c->d_counts;
+    F.winner0 = c->d_winner[0];
+    F.origin0 = c->d_origin[0];
+    F.linked_best = c->d_linked;
+    if (c->mode == DMX_MODE_LINKED) {
+        const uint32_t gr = (uint32_t)((c->n_reads + 255) / 256);
+        if (round == 0) {
+            if (gr) hipLaunchKernelGGL(finalize0_linked_kernel, dim3(gr), dim3(256), 0, st, F);
+        } else {
+            const uint32_t gi = (uint32_t)((c->item_cap + 255) / 256);
+            if (gi) hipLaunchKernelGGL(finalize1_linked_kernel, dim3(gi), dim3(256), 0, st, F);
+            if (gr) hipLaunchKernelGGL(finalize2_linked_kernel, dim3(gr), dim3(256), 0, st, F);
+        }
+        hipEventRecord(c->ev[6 + round], st);
+        return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
+    }
     if (round == 0) {
         const uint32_t grid = (uint32_t)((c->n_reads + 255) / 256);
         if (grid) hipLaunchKernelGGL(finalize0_kernel, dim3(grid), dim3(256), 0, st, F);

@@ -13,6 +13,7 @@ blank lines (RNA_primers.fa:5); both are tolerated.
 from __future__ import annotations
 
 import os
+import re
 from dataclasses import dataclass, field
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
@@ -116,3 +117,35 @@ def load_panel(path: str) -> tuple[list[str], list[str]]:
     """(names, sequences) of a FASTA panel."""
     recs = read_fasta(path)
     return [h.split()[0] for h, _ in recs], [normalize(s) for _, s in recs]
+
+
+_PAIR_ID = re.compile(r"_([A-Z])(?=\s|$|_)")
+
+
+def primer_pairs(path: str) -> list[tuple[str, str, str]]:
+    """Linked primer pairs [(pair_id, forward, reverse)] from a round-1 primer FASTA.
+
+    Restates the header convention of scripts/04_cleaning_primers.sh:184-270: a header holding
+    "Forward" / "Reverse" assigns its sequence to every pair id `_X` it carries (X one capital
+    letter followed by whitespace, `_` or the end); pair order = first appearance; a later
+    record for the same (id, orientation) replaces the earlier one; incomplete pairs are skipped
+    (:380-385).  The sequences are used as written (the script does not reverse-complement)."""
+    fwd: dict[str, str] = {}
+    rev: dict[str, str] = {}
+    order: list[str] = []
+    for head, seq in read_fasta(path):
+        seq = "".join(seq.split())
+        if not seq:
+            continue
+        ids = _PAIR_ID.findall(">" + head)
+        if "Forward" in head:
+            dst = fwd
+        elif "Reverse" in head:
+            dst = rev
+        else:
+            continue
+        for pid in ids:
+            dst[pid] = seq
+            if pid not in order:
+                order.append(pid)
+    return [(p, fwd[p], rev[p]) for p in order if p in fwd and p in rev]

@@ -135,3 +135,25 @@ def two_round(sp5, sp27, seq, use_rc=True, e=0.1):
         return (a, rc1, m1, -1, False, None, None)
     b, rc2, m2, t2 = demux_round(sp27, [BACK] * len(sp27), t1, use_rc, e)
     return (a, rc1, m1, b, rc2, m2, t2 if b >= 0 else None)
+
+
+def linked(fronts, backs, seq, e=0.1):
+    """-g F...R without anchoring: LinkedAdapter.match_to with both parts required (cutadapt 4.9
+    adapters.py, LinkedAdapter; front on the read, back on read[front.rstop:]); the best pair is
+    picked by AdapterCutter.best_match on LinkedMatch.score / .errors = summed parts.
+    Returns (index, front_match, back_match, trimmed) or (-1, None, None, seq)."""
+    best, bf, bb, bs, be = -1, None, None, 0, 0
+    for a, (f, r) in enumerate(zip(fronts, backs)):
+        mf = locate(f, seq, e / len(f) if e >= 1 else e, FRONT)
+        if mf is None:
+            continue
+        rest = seq[mf[3]:]
+        mb = locate(r, rest, e / len(r) if e >= 1 else e, BACK)
+        if mb is None:
+            continue
+        s, er = mf[4] + mb[4], mf[5] + mb[5]
+        if best < 0 or s > bs or (s == bs and er < be):
+            best, bf, bb, bs, be = a, mf, mb, s, er
+    if best < 0:
+        return -1, None, None, seq
+    return best, bf, bb, seq[bf[3]:][:bb[2]]

@@ -9,7 +9,8 @@ import pytest
 
 import oracle
 from dmx import panel, synth
-from helpers import CLI, oracle_round, random_quals, read_fastq, write_fastq
+from helpers import (CLI, amplicon_reads, oracle_linked, oracle_round, random_quals, read_fastq,
+                     write_fastq)
 
 pytestmark = pytest.mark.gpu
 
@@ -69,3 +70,31 @@ def test_02_cutadapt_loop_dropin(tmp_path):
     assert rep["read_counts"]["read1_with_adapter"] == sum(len(v) for k, v in exp1.items()
                                                           if k >= 0)
     assert [a["name"] for a in rep["adapters_read1"]] == n5
+
+
+def _read_fasta(path):
+    recs = panel.read_fasta(path)
+    return [(h, s, None) for h, s in recs]
+
+
+def test_04_linked_primers_dropin(tmp_path):
+    """scripts/04_cleaning_primers.sh:371-393: one call with every linked pair, FASTA in/out,
+    --untrimmed-output; trimmed and untrimmed files equal the oracle's, record for record."""
+    pairs = panel.primer_pairs(os.path.join(os.path.dirname(panel.SP5_FASTA), "COI_primers.fa"))
+    rng = np.random.default_rng(8)
+    seqs = amplicon_reads(rng, [(f, r) for _, f, r in pairs], 2500)
+    infile = tmp_path / "consensus.fasta"
+    names = [f"cluster{i};size={int(rng.integers(2, 90))}" for i in range(len(seqs))]
+    infile.write_text("".join(f">{n}\n{s}\n" for n, s in zip(names, seqs)))
+    out = tmp_path / "round1_amplicon.fasta"
+    unt = tmp_path / "untrimmed_round1.fasta"
+    cmd = [CLI, "-j", "4"]
+    for _, f, r in pairs:
+        cmd += ["-g", f"{f}...{r}"]
+    cmd += [f"--untrimmed-output={unt}", "-o", str(out), str(infile)]
+    subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL)
+    trimmed, untrimmed = oracle_linked([(n, s, None) for n, s in zip(names, seqs)],
+                                       [(f, r) for _, f, r in pairs])
+    assert len(trimmed) > 0.6 * len(seqs) and len(untrimmed) > 0
+    assert _read_fasta(str(out)) == trimmed
+    assert _read_fasta(str(unt)) == untrimmed

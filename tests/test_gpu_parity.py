@@ -5,8 +5,11 @@ Bit-exact on every field of every read: bins, RC flags, trim coordinates, scores
 import numpy as np
 import pytest
 
+import os
+
 import oracle
-from dmx import lib, synth
+from dmx import lib, panel, synth
+from helpers import amplicon_reads
 
 pytestmark = pytest.mark.gpu
 
@@ -147,3 +150,34 @@ def test_resolve_kernels_agree(mode, monkeypatch):
     exp = _oracle_two_round(d)
     with lib.Context(0) as c:
         _assert_same(_gpu_two_round(c, d), exp)
+
+
+def _linked_pairs(kind, rng):
+    data = os.path.join(os.path.dirname(panel.SP5_FASTA))
+    if kind in ("COI", "RNA"):
+        return [(f, r) for _, f, r in panel.primer_pairs(os.path.join(data, f"{kind}_primers.fa"))]
+    return [tuple(_random_panel(rng, 2, 12, 40, 0.1)) for _ in range(7)]
+
+
+@pytest.mark.parametrize("kind", ["COI", "RNA", "random7"])
+def test_linked_matches_oracle(ctx, kind):
+    """Linked -g F...R (scripts/04_cleaning_primers.sh:377): per-pair front scan, back scan on
+    read[front.rstop:], best pair by summed score then errors then pair order."""
+    rng = np.random.default_rng({"COI": 1, "RNA": 2, "random7": 3}[kind])
+    pairs = _linked_pairs(kind, rng)
+    seqs = amplicon_reads(rng, pairs, 4000) + ["", "ACGT", pairs[0][0], pairs[0][0] + pairs[0][1]]
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    exp = oracle.run_batch(oracle.Panel([p[0] for p in pairs], oracle.FRONT),
+                           oracle.Panel([p[1] for p in pairs], oracle.BACK),
+                           blob, offs, lens, mode=2, use_rc=False, threads=8)
+    assert (exp["bin1"] >= 0).mean() > 0.5
+    ctx.set_panel(0, [p[0] for p in pairs], lib.DMX_FRONT)
+    ctx.set_panel(1, [p[1] for p in pairs], lib.DMX_BACK)
+    ctx.set_mode(lib.MODE_LINKED)
+    got = ctx.run(lib.pack(blob, offs, lens))
+    _assert_same(got, exp)
+    c = ctx.counts()
+    A = len(pairs)
+    for a in range(A):
+        assert c[(a + 1) * (A + 1) + a + 1] == (exp["bin1"] == a).sum()
+    assert c[0] == (exp["bin1"] < 0).sum()

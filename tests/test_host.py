@@ -88,3 +88,16 @@ def test_synthetic_24_panel_distance():
     assert len(set(s1)) == 24 and len(set(s2)) == 24
     assert s1[:12] == panel.load_panel(panel.SP5_FASTA)[1]
     assert all(s.startswith(s1[0][:25]) and s.endswith(s1[0][42:]) for s in s1)
+
+
+def test_primer_pairs_follow_04_header_convention(tmp_path):
+    """scripts/04_cleaning_primers.sh:184-270: pair ids `_X` from Forward/Reverse headers; one
+    reverse primer may serve several pairs; incomplete pairs are dropped."""
+    import os
+    coi = panel.primer_pairs(os.path.join(os.path.dirname(panel.SP5_FASTA), "COI_primers.fa"))
+    assert [p[0] for p in coi] == ["A", "B"]
+    assert coi[0][2] == coi[1][2] == "TGRTTYTTYGGNCAYCCNGNRGTNTA"
+    f = tmp_path / "p.fa"
+    f.write_text(">x|Forward_A\nACGT\nACGT\n\n>y|Forward_C\nGGGG\n>z|Reverse_A_C_D\nTTTT\n"
+                 ">w|Forward_A\nCCCCAAAA\n")
+    assert panel.primer_pairs(str(f)) == [("A", "CCCCAAAA", "TTTT"), ("C", "GGGG", "TTTT")]

@@ -132,3 +132,30 @@ def test_two_round_batch_equals_composition():
             assert fused["m1_rstop"][i] == m1[3] and fused["m1_score"][i] == m1[4]
         if a >= 0 and b >= 0:
             assert fused["m2_rstart"][i] == m2[2] and fused["m2_errors"][i] == m2[5]
+
+
+def test_linked_c_oracle_equals_full_matrix():
+    """orc_linked (C) == pyref.linked (full-matrix restatement of LinkedAdapter.match_to)."""
+    import os
+    import numpy as np
+    from dmx import panel
+    from helpers import amplicon_reads
+    pairs = [(f, r) for _, f, r in panel.primer_pairs(
+        os.path.join(os.path.dirname(panel.SP5_FASTA), "COI_primers.fa"))]
+    rng = np.random.default_rng(4)
+    seqs = amplicon_reads(rng, pairs, 60, body=(20, 150), flank=(0, 12)) + ["", "ACG"]
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    res = oracle.run_batch(oracle.Panel([p[0] for p in pairs], F),
+                           oracle.Panel([p[1] for p in pairs], B), blob, offs, lens, mode=2,
+                           use_rc=False)
+    hits = 0
+    for i, s in enumerate(seqs):
+        a, mf, mb, _ = pyref.linked([p[0] for p in pairs], [p[1] for p in pairs], s)
+        assert res["bin1"][i] == a and res["bin2"][i] == a
+        if a >= 0:
+            hits += 1
+            assert (res["m1_rstart"][i], res["m1_rstop"][i], res["m1_score"][i],
+                    res["m1_errors"][i]) == (mf[2], mf[3], mf[4], mf[5])
+            assert (res["m2_rstart"][i], res["m2_rstop"][i], res["m2_score"][i],
+                    res["m2_errors"][i]) == (mb[2], mb[3], mb[4], mb[5])
+    assert hits > 30
