@@ -31,12 +31,28 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CUs x 4 SIMD32 x 2.4 GHz, 32-bit lane-ops
 
 
-def scan_algorithmic_bytes(lengths: np.ndarray, n_clusters: int) -> float:
-    """Algorithmic HBM bytes of one scan launch over these views: the 2-bit
-    packed read once (L/4 B), its 1-bit no-match mask (L/8 B), offset + length (12 B), plus the
-    16-B candidate-cluster records it writes."""
+def filter_algorithmic_bytes(lengths: np.ndarray, n_windows: int) -> float:
+    """Algorithmic HBM bytes of one filter launch over these views: each read's
+    2-bit packed codes once (L/4 B) and its 1-bit no-match mask (L/8 B), its offset + length
+    (12 B), plus the 40-B window records the launch writes.  Both orientations of a read are
+    filtered from the same bytes."""
     L = lengths.astype(np.float64)
-    return float(np.sum(np.ceil(L / 4) + np.ceil(L / 8) + 12.0) + 16.0 * n_clusters)
+    return float(np.sum(np.ceil(L / 4) + np.ceil(L / 8) + 12.0) + 40.0 * n_windows)
+
+
+def pmc_traffic(workload: str, reads: int):
+    """HBM bytes per filter launch from the committed rocprofv3 PMC summary (FETCH_SIZE and
+    WRITE_SIZE passes, corrected per MI355X_MICROARCH.md), if one exists for this workload."""
+    path = os.path.join(ROOT, "profiles", "filter_pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    key = f"{workload}:{reads}"
+    if key not in d:
+        return None, None
+    return d[key]["bytes_per_launch"], d[key]["source"]
 
 
 def cpu_baseline(workload: str, threads: int, target_s: float = 12.0):
@@ -125,9 +141,10 @@ def main():
         allreduce_counts()
 
     stage = {k: 0.0 for k in ("scan0", "resolve0", "finalize0", "scan1", "resolve1",
-                              "finalize1", "total")}
+                              "finalize1", "total", "filter0", "verify0", "filter1", "verify1")}
     clusters = np.zeros(2)
     windows = np.zeros(2)
+    windows_raw = np.zeros(2)
     resolved = np.zeros(2)
     traces = np.zeros(2)
     barrier_sync()
@@ -142,6 +159,7 @@ def main():
             stage[k] += st["ms"][k]
         clusters += np.array(st["clusters"], dtype=np.float64)
         windows += np.array(st["windows"], dtype=np.float64)
+        windows_raw += np.array(st["windows_raw"], dtype=np.float64)
         resolved += np.array(st["resolved"], dtype=np.float64)
         traces += np.array(st["traces"], dtype=np.float64)
         flags |= st["flags"]
@@ -159,18 +177,20 @@ def main():
     K = args.steps
     total_reads = args.reads * world * K
     value = total_reads / elapsed / 1e6
-    # roofline of the dominant kernel (scan; two launches per step: round 1 and round 2)
-    scan_ms = (stage["scan0"] + stage["scan1"]) / (2 * K)
+    # roofline of the dominant kernel: the shared-suffix filter (reads every base of every
+    # view; two launches per step, round 1 over the reads, round 2 over the round-1 tails)
+    filt_ms = (stage["filter0"] + stage["filter1"]) / (2 * K)
     res = ctx.fetch()
-    n2 = int((res["bin1"] >= 0).sum())
-    len2 = (lengths[res["bin1"] >= 0] - res["m1_rstop"][res["bin1"] >= 0]).astype(np.int64)
-    bytes0 = scan_algorithmic_bytes(lengths, int(clusters[0] / K))
-    bytes1 = scan_algorithmic_bytes(len2, int(clusters[1] / K))
-    achieved = (bytes0 + bytes1) / 2 / (scan_ms / 1e3) / 1e9
+    m2 = res["bin1"] >= 0
+    n2 = int(m2.sum())
+    len2 = (lengths[m2] - res["m1_rstop"][m2]).astype(np.int64)
+    bytes0 = filter_algorithmic_bytes(lengths, int(windows_raw[0] / K))
+    bytes1 = filter_algorithmic_bytes(len2, int(windows_raw[1] / K))
+    alg_bytes = (bytes0 + bytes1) / 2
+    achieved = alg_bytes / (filt_ms / 1e3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.workload, args.reads)
     A0, A1 = ctx.panel_sizes
-    steps_r0 = float(lengths.sum()) * A0 * 2
-    steps_r1 = float(len2.sum()) * A1 * 2
-    word_steps_per_s = (steps_r0 + steps_r1) / ((stage["scan0"] + stage["scan1"]) / K / 1e3)
+    cols = float(lengths.sum()) * 2 + float(len2.sum()) * 2     # filter columns, both strands
 
     out = {
         "metric": METRIC, "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
@@ -183,11 +203,14 @@ def main():
                    "panel": f"{A0}x{A1}", "reads_per_gpu": args.reads,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                     "kernel": "dmx::scan_kernel", "avg_launch_ms": round(scan_ms, 3),
-                     "note": "integer bit-vector scan is VALU-bound by construction "
-                             "(DESIGN.md §5); see 'valu'"},
-        "valu": {"word_steps_per_s": word_steps_per_s,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": round(alg_bytes),
+                     "kernel": "dmx::filter_kernel", "avg_launch_ms": round(filt_ms, 3),
+                     "note": "the bit-vector filter is VALU-bound by construction "
+                             "(DESIGN.md §5): see 'valu' for its issue-rate fraction"},
+        "valu": {"filter_columns_per_s": cols / ((stage["filter0"] + stage["filter1"]) / K / 1e3),
+                 "filter_lane_ops_per_column": 20,
                  "peak_lane_ops_per_s": VALU_PEAK_TOPS * 1e12},
         "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
         "clusters_per_step": (clusters / K).tolist(),

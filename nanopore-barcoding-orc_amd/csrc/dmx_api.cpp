@@ -31,6 +31,7 @@ namespace {
 
 constexpr int kPackAlign = 32;   // every read starts on a 32-nt (one nmask word) boundary
 constexpr int kMinFilterLen = 10; // shortest shared suffix worth a filter pass
+constexpr size_t kGuardWords = 64; // zeroed words before/after the packed device buffers
 
 uint8_t iupac_mask(char ch) {
     switch (ch) {
@@ -233,7 +234,7 @@ void dmx_close(dmx_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->d_seq,       c->d_nmask,     c->d_offs,     c->d_lens,      c->d_res,
+    void* bufs[] = {c->d_seq_alloc, c->d_nmask_alloc,     c->d_offs,     c->d_lens,      c->d_res,
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
                     c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_counters,
                     c->d_counts,    c->d_panel[0],  c->d_panel[1]};
@@ -380,7 +381,20 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
     const int flen = std::min(common, 32);
     bool uniform = true;
     for (int a = 1; a < n; ++a) uniform &= hp.ad[a].where == hp.ad[0].where;
-    hp.filter = uniform && flen >= kMinFilterLen && !(c->no_filter);
+    int kf_all = -1;
+    for (int a = 0; a < n; ++a) kf_all = std::max(kf_all, (int)hp.ad[a].kk);
+    // The filter's first 64 columns per segment carry per-column thresholds: the warm-up
+    // W = flen + kf and the near-start acceptance pf[j + kf] < kf must both end within them.
+    int8_t pf_all[72];
+    for (int L = 0; L < 72; ++L) {
+        pf_all[L] = -1;
+        for (int a = 0; a < n; ++a) pf_all[L] = std::max(pf_all[L], hp.ad[a].pacc[L]);
+    }
+    const int kf_far = std::min(kf_all, (int)pf_all[71]);
+    bool near_ok = true;
+    for (int j = 65; j + kf_all < 71; ++j) near_ok &= pf_all[j + kf_all] >= kf_far;
+    hp.filter = uniform && flen >= kMinFilterLen && flen + kf_all <= 64 && near_ok &&
+                !(c->no_filter);
     if (hp.filter) {
         dp.filter_len = flen;
         const char* blk = seqs[0] + lens[0] - flen;
@@ -484,10 +498,18 @@ int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uin
     }
     CK(hipSetDevice(c->device));
     int rc;
-    if (c->cap_words < n_words) {
-        if ((rc = dev_alloc(c, &c->d_seq, n_words))) return rc;
-        if ((rc = dev_alloc(c, &c->d_nmask, n_words))) return rc;
+    if (c->cap_words < n_words || !c->d_seq_alloc) {
+        const size_t total = n_words + 2 * kGuardWords;
+        if ((rc = dev_alloc(c, &c->d_seq_alloc, total))) return rc;
+        if ((rc = dev_alloc(c, &c->d_nmask_alloc, total))) return rc;
+        CK(hipMemsetAsync(c->d_seq_alloc, 0, total * 4, c->stream));
+        CK(hipMemsetAsync(c->d_nmask_alloc, 0, total * 4, c->stream));
+        c->d_seq = c->d_seq_alloc + kGuardWords;
+        c->d_nmask = c->d_nmask_alloc + kGuardWords;
         c->cap_words = n_words;
+    } else if (c->n_words > n_words) {   // stale tail of a longer batch: keep the guard zero
+        CK(hipMemsetAsync(c->d_seq + n_words, 0, (c->n_words - n_words) * 4, c->stream));
+        CK(hipMemsetAsync(c->d_nmask + n_words, 0, (c->n_words - n_words) * 4, c->stream));
     }
     if (!c->d_offs || c->cap_reads < n_reads) {
         if ((rc = dev_alloc(c, &c->d_offs, n_reads))) return rc;
@@ -570,7 +592,8 @@ int dmx_counts(dmx_ctx* c, uint64_t* out, size_t n_out) {
     return (int)c->n_counts;
 }
 
-int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* clusters, int* flags) {
+int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_counts,
+              int* flags) {
     if (!c) return DMX_E_INVALID;
     if (!c->executed) {
         c->err = "dmx_stats before dmx_exec";
@@ -579,29 +602,37 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* clusters, int*
     CK(hipSetDevice(c->device));
     CK(hipStreamSynchronize(c->stream));
     const int rounds = c->mode == DMX_MODE_SINGLE ? 1 : 2;
-    float t[7] = {0, 0, 0, 0, 0, 0, 0};
+    float t[11] = {};
     for (int r = 0; r < rounds; ++r) {
         hipEventElapsedTime(&t[3 * r + 0], c->ev[3 * r + 0], c->ev[3 * r + 1]);
         hipEventElapsedTime(&t[3 * r + 1], c->ev[3 * r + 1], c->ev[3 * r + 2]);
         hipEventElapsedTime(&t[3 * r + 2], c->ev[3 * r + 2], c->ev[6 + r]);
+        const bool f = c->panel[r].filter && !(c->mode == DMX_MODE_LINKED);
+        if (f) {
+            hipEventElapsedTime(&t[7 + 2 * r], c->ev[3 * r + 0], c->ev[9 + 2 * r]);
+            hipEventElapsedTime(&t[8 + 2 * r], c->ev[9 + 2 * r], c->ev[10 + 2 * r]);
+        }
     }
     hipEventElapsedTime(&t[6], c->ev[8], c->ev[6 + rounds - 1]);
-    for (int i = 0; i < n_stage && i < 7; ++i) stage_ms[i] = t[i];
+    for (int i = 0; i < n_stage && i < 11; ++i) stage_ms[i] = t[i];
     uint32_t cnt[32];
     CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
     if (getenv("DMX_DEBUG_STATS"))
         fprintf(stderr, "dmx stats: resolve max window %u %u, total window columns %u %u\n",
                 cnt[18], cnt[22], cnt[19], cnt[23]);
-    if (clusters) {
-        clusters[0] = cnt[0];
-        clusters[1] = cnt[1];
-        clusters[2] = c->panel[0].verify ? cnt[10] : cnt[4];
-        clusters[3] = c->panel[1].verify ? cnt[11] : cnt[5];
+    if (counts) {
         const bool b0 = c->band_ok[0] && !c->force_ring, b1 = c->band_ok[1] && !c->force_ring;
-        clusters[4] = b0 ? (uint64_t)cnt[6] + cnt[7] : cnt[16];
-        clusters[5] = b1 ? (uint64_t)cnt[8] + cnt[9] : cnt[20];
-        clusters[6] = cnt[17];
-        clusters[7] = cnt[21];
+        const uint64_t v[10] = {cnt[0],
+                                cnt[1],
+                                c->panel[0].verify ? cnt[10] : cnt[4],
+                                c->panel[1].verify ? cnt[11] : cnt[5],
+                                b0 ? (uint64_t)cnt[6] + cnt[7] : cnt[16],
+                                b1 ? (uint64_t)cnt[8] + cnt[9] : cnt[20],
+                                cnt[17],
+                                cnt[21],
+                                cnt[4],
+                                cnt[5]};
+        for (int i = 0; i < n_counts && i < 10; ++i) counts[i] = v[i];
     }
     if (flags) {
         int f = (int)cnt[3];
@@ -624,7 +655,7 @@ int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint
         uint64_t cl[8];
         int flags = 0;
         float ms[7];
-        if ((rc = dmx_stats(c, ms, 7, cl, &flags))) return rc;
+        if ((rc = dmx_stats(c, ms, 7, cl, 8, &flags))) return rc;
         if (flags & 2) {
             c->err = "internal: traceback left the exact window (please report)";
             return DMX_E_STATE;

@@ -241,7 +241,9 @@ __device__ __forceinline__ void myers_step32(uint32_t eq, uint32_t& pv, uint32_t
     const uint32_t xh = (((eq & pv) + pv) ^ pv) | eq;
     uint32_t ph = mv | ~(xh | pv);
     uint32_t mh = pv & xh;
-    d += (int)((ph >> hbit) & 1u) - (int)((mh >> hbit) & 1u);
+    // +1 / -1 from the last row's horizontal deltas: one v_add3 of an unsigned and a signed
+    // one-bit field
+    d += (int)__builtin_amdgcn_ubfe(ph, hbit, 1) + __builtin_amdgcn_sbfe((int)mh, hbit, 1);
     ph <<= 1;
     mh <<= 1;
     pv = mh | ~(xv | ph);

@@ -33,8 +33,10 @@ struct Ctx {
     // resident batch
     size_t n_reads = 0, n_words = 0;
     size_t cap_reads = 0, cap_words = 0;
-    uint32_t* d_seq = nullptr;
+    uint32_t* d_seq = nullptr;          // = d_seq_alloc + kGuardWords
     uint32_t* d_nmask = nullptr;
+    uint32_t* d_seq_alloc = nullptr;    // packed buffers with zeroed guard words on both sides
+    uint32_t* d_nmask_alloc = nullptr;  // (the filter loads whole aligned 64-nt blocks)
     uint64_t* d_offs = nullptr;
     uint32_t* d_lens = nullptr;
 
@@ -62,7 +64,8 @@ struct Ctx {
     unsigned long long* d_counts = nullptr;
     unsigned long long* d_linked = nullptr;   // linked mode: best pair key per read
     size_t n_counts = 0;
-    hipEvent_t ev[9] = {};
+    hipEvent_t ev[13] = {};   // [3r..3r+2] round r stages, [6+r] finalize, [8] start,
+                              // [9+2r] after filter, [10+2r] after verify
     bool executed = false;
 };
 

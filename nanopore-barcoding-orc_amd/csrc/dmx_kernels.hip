@@ -443,13 +443,19 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// filter: persistent lanes over a block's range of (item, orientation) views; 32-bit Myers of
-// the panel's shared suffix block.  Hit columns (b(j) <= min(kf, pf[min(71, j + kf)])) are
-// grouped into windows.  A lane that finishes a view takes the block's next one, so lanes of a
-// wave stay busy however unequal the read lengths are.
+// filter: 32-bit Myers of the panel's shared suffix block (L rows) over every view, cut into
+// SEGMENTS of S = 256 - W view positions.  One lane per segment: lanes of a wave take
+// consecutive segments of the same view, so their loads cover one contiguous stretch of the
+// packed read (each lane loads its 256 positions once, as five aligned 64-nt blocks).
+// A segment after the first starts W = L + kf columns early with the restricted-start column
+// D(i) = i: an alignment of the block with cost <= kf spans at most L + kf columns, so every
+// hit column of the segment (b(j) <= kf) is computed exactly.  Hit columns
+// (b(j) <= min(kf, pf[min(71, j + kf)])) are grouped into windows; a window never crosses a
+// segment boundary.  Segments are ordered strand 0 first, then strand 1, so the strand branch is
+// wave-uniform except in one wave per block.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kFilterViewsPerBlock = 512;
-constexpr int kFilterChunksPerRound = 12;
+constexpr uint32_t kSegViewsPerBlock = 1024;
+constexpr int kSegSpan = 256;                 // view positions loaded per segment (S + W)
 
 __device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskView& tv,
                                               uint32_t j1, uint32_t j2, int lastcol, int bmin) {
@@ -469,112 +475,314 @@ __device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskVi
     return w;
 }
 
+__device__ __forceinline__ uint32_t align32(uint32_t hi, uint32_t lo, uint32_t r) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> r);
+}
+
+struct SegState {
+    uint32_t pv, mv;
+    int b;
+    bool have;
+    uint32_t w1, w2;
+    int wb;
+};
+
+// One 16-position chunk (view positions p0 .. p0+15) of a filter segment.  All 16 steps always
+// run (lanes of a wave stay in lockstep); columns past the segment end (q >= cnt) cannot hit.
+// The steps are branch-free: hit columns go into a 16-bit mask (and the chunk's minimum b, a
+// lower bound of every hit's b, into cb); windows are formed afterwards.  CAREFUL (the first 64
+// positions of every segment): per-column thresholds, -1 in the warm-up (columns <= hit_from)
+// and the prefix-max acceptance pf[j + kf] near the view start; beyond them every column's
+// threshold is kf_far (the host checks pf[j + kf] >= kf_far for j > 64).
+template <bool CAREFUL>
+__device__ __forceinline__ void filter_chunk(uint32_t codes, uint32_t nb, uint32_t p0, int cnt,
+                                             SegState& S, const uint32_t* s_fpeq,
+                                             const int8_t* s_thr, uint32_t hbit, int kf,
+                                             int kf_far, uint32_t gap, uint32_t hit_from,
+                                             const Stage<Window>& st, uint32_t item, int o,
+                                             const TaskView& tv) {
+    uint32_t eq[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+        eq[q] = s_fpeq[((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)];
+    uint4 tw = {0u, 0u, 0u, 0u};
+    if constexpr (CAREFUL)   // 16 per-position thresholds (s_thr: 16-byte aligned rows)
+        tw = *reinterpret_cast<const uint4*>(s_thr + (hit_from == 0 ? p0 : 240u));
+    uint32_t hits = 0;
+    int cb = 127;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        {
+            myers_step32(eq[q], S.pv, S.mv, S.b, hbit);
+            int t = kf_far;
+            if constexpr (CAREFUL) {
+                const uint32_t w = q < 4 ? tw.x : q < 8 ? tw.y : q < 12 ? tw.z : tw.w;
+                t = __builtin_amdgcn_sbfe((int)w, 8 * (q & 3), 8) |
+                    ((int)(p0 + (uint32_t)q - hit_from) >> 31);      // -1 in the warm-up
+            }
+            hits |= S.b <= t ? (1u << q) : 0u;
+            cb = min(cb, S.b);
+        }
+    }
+    hits &= cnt >= 16 ? 0xFFFFu : (cnt > 0 ? (1u << cnt) - 1u : 0u);
+    while (hits) {
+        const int q = __ffs(hits) - 1;
+        hits &= hits - 1;
+        const uint32_t j = p0 + (uint32_t)q + 1;
+        if (S.have && j - S.w2 <= gap) {
+            S.w2 = j;
+            S.wb = min(S.wb, cb);
+        } else {
+            if (S.have) st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb));
+            S.have = true;
+            S.w1 = S.w2 = j;
+            S.wb = cb;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t bsel(uint32_t mask, uint32_t a, uint32_t b) {
+    return (a & mask) | (b & ~mask);      // mask ? a : b, bitwise (stays in registers)
+}
+
+// The 5 aligned 64-nt blocks of a segment (ascending global nt; 4 code words + 2 mask words
+// per block) and the lane's bit offset into them.
+struct SegBlocks {
+    uint32_t cw[20], nw[10];
+    uint32_t m1, m2, mv1;      // word-offset select masks
+    uint32_t r, r2;            // bit offsets within a word (codes, mask)
+};
+
+// The next 64 view positions as 4 chunks (2-bit codes; 16 no-match bits each), then advance
+// the block window by one block (strand 0 up, strand 1 down).
+template <int STRAND>
+__device__ __forceinline__ void seg_extract(SegBlocks& B, uint32_t vc[4], uint32_t vn[4]) {
+    constexpr int b0 = STRAND == 0 ? 0 : 3;
+    uint32_t a[7], t[5], asc[4], tn[3];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) a[k] = bsel(B.m1, B.cw[4 * b0 + k + 1], B.cw[4 * b0 + k]);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t[k] = bsel(B.m2, a[k + 2], a[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) asc[k] = align32(t[k + 1], t[k], B.r);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tn[k] = bsel(B.mv1, B.nw[2 * b0 + k + 1], B.nw[2 * b0 + k]);
+    const uint32_t an[2] = {align32(tn[1], tn[0], B.r2), align32(tn[2], tn[1], B.r2)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if constexpr (STRAND == 0) {
+            vc[c] = asc[c];
+            vn[c] = (an[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+        } else {
+            const int d = 3 - c;
+            vc[c] = ~rev_pairs(asc[d]);                        // complement = 3 - code
+            vn[c] = __brev((an[d >> 1] >> (16 * (d & 1))) & 0xFFFFu) >> 16;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if constexpr (STRAND == 0) B.cw[k] = B.cw[k + 4];
+        else B.cw[19 - k] = B.cw[15 - k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if constexpr (STRAND == 0) B.nw[k] = B.nw[k + 2];
+        else B.nw[9 - k] = B.nw[7 - k];
+    }
+}
+
+// Process view positions [P0, P1) (P1 - P0 <= kSegSpan) of one view.  Loaded: 256 positions
+// from the ascending global nt index g (strand 0: off + start + P0; strand 1: the lowest global
+// nt of the 256 positions, whose view order is descending).
+__device__ __forceinline__ void filter_segment(const RoundArgs& R, const TaskView& tv,
+                                               uint32_t P0, uint32_t P1, SegState& S,
+                                               const uint32_t* s_fpeq, const int8_t* s_thr,
+                                               uint32_t hbit, int kf, int kf_far, uint32_t gap,
+                                               uint32_t hit_from, const Stage<Window>& st,
+                                               uint32_t item, int o) {
+    const bool rev = tv.strand != 0;
+    const int64_t g = rev ? (int64_t)tv.off + (int64_t)tv.n - 1 - tv.start - P0 - (kSegSpan - 1)
+                          : (int64_t)tv.off + tv.start + P0;
+    const int64_t blk = g >> 6;                   // floor: the buffers carry guard words
+    const uint32_t sh = (uint32_t)(g & 63);
+    const uint4* sp = reinterpret_cast<const uint4*>(R.seq) + blk;
+    const uint2* np = reinterpret_cast<const uint2*>(R.nmask) + blk;
+    SegBlocks B;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint4 c4 = sp[k];
+        B.cw[4 * k + 0] = c4.x;
+        B.cw[4 * k + 1] = c4.y;
+        B.cw[4 * k + 2] = c4.z;
+        B.cw[4 * k + 3] = c4.w;
+        const uint2 n2 = np[k];
+        B.nw[2 * k + 0] = n2.x;
+        B.nw[2 * k + 1] = n2.y;
+    }
+    B.m1 = ((sh >> 4) & 1u) ? ~0u : 0u;           // code-word offset sh / 16
+    B.m2 = ((sh >> 5) & 1u) ? ~0u : 0u;
+    B.mv1 = B.m2;                                 // mask-word offset sh / 32
+    B.r = (2u * sh) & 31u;
+    B.r2 = sh & 31u;
+
+    for (uint32_t p0 = P0; p0 < P1; p0 += 64) {
+        uint32_t vc[4], vn[4];
+        if (rev) seg_extract<1>(B, vc, vn);
+        else seg_extract<0>(B, vc, vn);
+        const bool careful = p0 == P0;                 // uniform: every lane's first 64
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t pc = p0 + 16u * (uint32_t)c;
+            const int cnt = (int)P1 - (int)pc;
+            if (careful)
+                filter_chunk<true>(vc[0], vn[0], pc, cnt, S, s_fpeq, s_thr, hbit, kf, kf_far, gap,
+                                   hit_from, st, item, o, tv);
+            else
+                filter_chunk<false>(vc[0], vn[0], pc, cnt, S, s_fpeq, s_thr, hbit, kf, kf_far,
+                                    gap, hit_from, st, item, o, tv);
+            vc[0] = vc[1];
+            vc[1] = vc[2];
+            vc[2] = vc[3];
+            vn[0] = vn[1];
+            vn[1] = vn[2];
+            vn[2] = vn[3];
+        }
+    }
+}
+
 __global__ __launch_bounds__(kScanBlock) void filter_kernel(RoundArgs R) {
     __shared__ uint32_t s_fpeq[8];
     __shared__ int8_t s_pf[72];
+    __shared__ __attribute__((aligned(16))) int8_t s_thr[kScanBlock];
     __shared__ Window s_win[kStageCap];
-    __shared__ uint32_t s_wcnt, s_wbase, s_next;
+    __shared__ uint32_t s_wcnt, s_wbase;
+    __shared__ uint32_t s_pre[2][kSegViewsPerBlock];   // per strand: segments before view v
+    __shared__ uint32_t s_tot[2][kScanBlock];
     const DevPanel* P = R.panel;
     const int no = P->n_orient;
     const uint32_t n_items = R.items ? *R.n_items_dev : R.n_items;
     const uint32_t n_views = n_items * (uint32_t)no;
-    const uint32_t vbeg = blockIdx.x * kFilterViewsPerBlock;
-    const uint32_t vend = min(n_views, vbeg + kFilterViewsPerBlock);
+    const uint32_t vbeg = blockIdx.x * kSegViewsPerBlock;
+    if (vbeg >= n_views) return;                       // block-uniform
+    const uint32_t nv = min(n_views - vbeg, kSegViewsPerBlock);
+    const int A = P->n_adapters;
+    const int L = P->filter_len;
+    const int kf = P->kf;
+    const uint32_t W = (uint32_t)(L + kf);
+    const uint32_t SEG = (uint32_t)kSegSpan - W;       // host guarantees W <= 96
     if (threadIdx.x < 8) s_fpeq[threadIdx.x] = P->filter_peq[threadIdx.x];
     if (threadIdx.x < 72) s_pf[threadIdx.x] = P->pf[threadIdx.x];
-    if (threadIdx.x == 0) {
-        s_wcnt = 0;
-        s_next = vbeg;
+    if (threadIdx.x == 0) s_wcnt = 0;
+    {   // hit threshold of the column after view position p: min(kf_far, pf[min(p+1+kf, 71)])
+        const int kf0 = P->kf;
+        const int far0 = min(kf0, (int)P->pf[71]);
+        s_thr[threadIdx.x] =
+            (int8_t)min(far0, (int)P->pf[min((int)threadIdx.x + 1 + kf0, 71)]);
+    }
+
+    // segment counts per view, grouped by strand; block-wide exclusive scan
+    constexpr int VPT = kSegViewsPerBlock / kScanBlock;   // 4 views per thread
+    uint32_t cnt[VPT];
+    int grp[VPT];
+    uint32_t sum0 = 0, sum1 = 0;
+#pragma unroll
+    for (int e = 0; e < VPT; ++e) {
+        const uint32_t vl = threadIdx.x * VPT + e;
+        cnt[e] = 0;
+        grp[e] = 0;
+        if (vl < nv) {
+            const uint32_t v = vbeg + vl;
+            TaskView tv;
+            task_view(R, v / (uint32_t)no, (int)(v % (uint32_t)no) * A, A, tv);
+            cnt[e] = (tv.len + SEG - 1) / SEG;
+            grp[e] = (int)tv.strand;
+        }
+        if (grp[e]) sum1 += cnt[e];
+        else sum0 += cnt[e];
+    }
+    s_tot[0][threadIdx.x] = sum0;
+    s_tot[1][threadIdx.x] = sum1;
+    __syncthreads();
+    for (uint32_t d = 1; d < kScanBlock; d <<= 1) {   // inclusive Hillis-Steele scan
+        uint32_t x0 = 0, x1 = 0;
+        if (threadIdx.x >= d) {
+            x0 = s_tot[0][threadIdx.x - d];
+            x1 = s_tot[1][threadIdx.x - d];
+        }
+        __syncthreads();
+        s_tot[0][threadIdx.x] += x0;
+        s_tot[1][threadIdx.x] += x1;
+        __syncthreads();
+    }
+    {
+        uint32_t r0 = s_tot[0][threadIdx.x] - sum0, r1 = s_tot[1][threadIdx.x] - sum1;
+#pragma unroll
+        for (int e = 0; e < VPT; ++e) {
+            const uint32_t vl = threadIdx.x * VPT + e;
+            if (vl < kSegViewsPerBlock) {
+                s_pre[0][vl] = r0;
+                s_pre[1][vl] = r1;
+            }
+            if (grp[e]) r1 += cnt[e];
+            else r0 += cnt[e];
+        }
     }
     __syncthreads();
+    const uint32_t T0 = s_tot[0][kScanBlock - 1], T1 = s_tot[1][kScanBlock - 1];
     const Stage<Window> st{s_win, &s_wcnt, &s_wbase, R.win, R.win_count, R.win_cap, R.flags, 4u};
 
     const bool front = P->where == kFront;
-    const int L = P->filter_len;
     const uint32_t hbit = (uint32_t)(L - 1);
-    const int kf = P->kf;
     const int kf_far = min(kf, (int)s_pf[71]);
     const uint32_t gap = (uint32_t)P->max_mk;
-    const int A = P->n_adapters;
 
-    uint32_t v = vbeg < vend ? atomicAdd(&s_next, 1u) : vend;
-    bool active = v < vend;
-    uint32_t item = 0;
-    int o = 0;
-    TaskView tv;
-    uint32_t pv = 0, mv = 0, p0 = 0;
-    int b = 0;
-    bool have = false;
-    uint32_t w1 = 0, w2 = 0;
-    int wb = 255;
-    uint32_t ncodes = 0, nnb = 0;
-    auto start_view = [&]() {
-        item = v / (uint32_t)no;
-        o = (int)(v % (uint32_t)no);
-        task_view(R, item, o * A, A, tv);
-        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, 0, ncodes, nnb);
-        pv = front ? 0u : ~0u;
-        mv = 0u;
-        b = front ? 0 : L;
-        p0 = 0;
-        have = false;
-    };
-    if (active) start_view();
-
-#define DMX_FILTER_STEP(q)                                                                \
-    {                                                                                     \
-        const uint32_t code = ((codes >> (2 * (q))) & 3u) | (((nb >> (q)) & 1u) << 2);    \
-        myers_step32(s_fpeq[code], pv, mv, b, hbit);                                      \
-        if (b <= kf_far) {                                                                \
-            const uint32_t j = p0 + (q) + 1;                                              \
-            if (j + (uint32_t)kf >= 71u || b <= (int)s_pf[j + kf]) {                      \
-                if (have && j - w2 <= gap) {                                              \
-                    w2 = j;                                                               \
-                    wb = min(wb, b);                                                      \
-                } else {                                                                  \
-                    if (have) st.push(make_window(item, o, tv, w1, w2, 0, wb));           \
-                    have = true;                                                          \
-                    w1 = w2 = j;                                                          \
-                    wb = b;                                                               \
-                }                                                                         \
-            }                                                                             \
-        }                                                                                 \
-    }
-
-    // Rounds of at most kFilterChunksPerRound chunks per lane; between rounds the block flushes
-    // its staged windows (a uniform point), so the LDS staging never overflows in practice.
-    while (__syncthreads_or(active)) {
-        for (int it = 0; it < kFilterChunksPerRound && active; ++it) {
-            const uint32_t codes = ncodes, nb = nnb;
-            if (p0 + 16 < tv.len)          // prefetch the next chunk of this view
-                fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes, nnb);
-            if (p0 + 16 <= tv.len) {
-#pragma unroll
-                for (int q = 0; q < 16; ++q) DMX_FILTER_STEP(q)
-                p0 += 16;
-            } else {
-                const int cnt = (int)(tv.len - p0);
-                for (int q = 0; q < cnt; ++q) DMX_FILTER_STEP(q)
-                // 3' panels: the last column (adapter prefix off the read end) is always checked
-                const uint32_t len = tv.len;
-                if (!front && len > 0) {
-                    if (have && len - w2 <= gap) {
-                        st.push(make_window(item, o, tv, w1, len, 1, wb));
-                    } else {
-                        if (have) st.push(make_window(item, o, tv, w1, w2, 0, wb));
-                        st.push(make_window(item, o, tv, len, len, 1, 255));
-                    }
-                    have = false;
-                }
-                if (have) st.push(make_window(item, o, tv, w1, w2, 0, wb));
-                v = atomicAdd(&s_next, 1u);
-                active = v < vend;
-                if (active) start_view();
+    for (uint32_t tb = 0; tb < T0 + T1; tb += kScanBlock) {
+        const uint32_t t = tb + threadIdx.x;
+        if (t < T0 + T1) {
+            const int g = t < T0 ? 0 : 1;
+            const uint32_t tt = g ? t - T0 : t;
+            // the last view whose segment prefix is <= tt (views of the other strand add 0)
+            uint32_t lo = 0, hi = nv;                  // answer in [lo, hi)
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_pre[g][mid] <= tt) lo = mid;
+                else hi = mid;
             }
+            const uint32_t v = vbeg + lo;
+            const uint32_t k = tt - s_pre[g][lo];
+            const uint32_t item = v / (uint32_t)no;
+            const int o = (int)(v % (uint32_t)no);
+            TaskView tv;
+            task_view(R, item, o * A, A, tv);
+            const uint32_t seg0 = k * SEG;
+            const uint32_t P0 = k ? seg0 - W : 0u;
+            const uint32_t P1 = min(tv.len, seg0 + SEG);
+            SegState S;
+            const bool fresh = k == 0;                 // view start: the panel's own column 0
+            S.pv = (fresh && front) ? 0u : ~0u;
+            S.mv = 0u;
+            S.b = (fresh && front) ? 0 : L;
+            S.have = false;
+            S.w1 = S.w2 = 0;
+            S.wb = 255;
+            filter_segment(R, tv, P0, P1, S, s_fpeq, s_thr, hbit, kf, kf_far, gap, seg0, st, item,
+                           o);
+            const uint32_t len = tv.len;
+            if (!front && P1 == len && len > 0) {
+                // 3' panels: the last column (adapter prefix off the read end) is always checked
+                if (S.have && len - S.w2 <= gap) {
+                    st.push(make_window(item, o, tv, S.w1, len, 1, S.wb));
+                } else {
+                    if (S.have) st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb));
+                    st.push(make_window(item, o, tv, len, len, 1, 255));
+                }
+                S.have = false;
+            }
+            if (S.have) st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb));
         }
-        st.flush();
+        __syncthreads();                               // staged count is block-uniform here
+        if (s_wcnt > kStageCap / 2) st.flush();
     }
-#undef DMX_FILTER_STEP
+    st.flush();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1432,13 +1640,17 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     hipEventRecord(c->ev[round * 3 + 0], st);
     if (hp.filter && !linked) {   // linked primers: short, no shared suffix block; plain scan
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
-        const uint32_t fgrid = (uint32_t)((nviews + kFilterViewsPerBlock - 1) / kFilterViewsPerBlock);
+        const uint32_t fgrid = (uint32_t)((nviews + kSegViewsPerBlock - 1) / kSegViewsPerBlock);
         if (fgrid > 0) hipLaunchKernelGGL(filter_kernel, dim3(fgrid), dim3(kScanBlock), 0, st, R);
+        hipEventRecord(c->ev[9 + 2 * round], st);
         if (hp.verify)
             hipLaunchKernelGGL(verify_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
+        hipEventRecord(c->ev[10 + 2 * round], st);
         if (band) hipLaunchKernelGGL(wscan_kernel<true>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(wscan_kernel<false>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
     } else if (grid > 0) {
+        hipEventRecord(c->ev[9 + 2 * round], st);
+        hipEventRecord(c->ev[10 + 2 * round], st);
         if (band) hipLaunchKernelGGL(scan_kernel<true>, dim3(grid), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(scan_kernel<false>, dim3(grid), dim3(kScanBlock), 0, st, R);
     }

@@ -68,9 +68,9 @@ def load() -> ctypes.CDLL:
     L.dmx_sync.argtypes = [P]
     L.dmx_fetch.argtypes = [P, P]
     L.dmx_counts.argtypes = [P, c_u64p, c_size]
-    L.dmx_stats.argtypes = [P, ctypes.POINTER(ctypes.c_float), c_int, c_u64p,
+    L.dmx_stats.argtypes = [P, ctypes.POINTER(ctypes.c_float), c_int, c_u64p, c_int,
                             ctypes.POINTER(c_int)]
-    if L.dmx_abi_version() != 1:
+    if L.dmx_abi_version() != 2:
         raise DmxError("libdmx ABI mismatch")
     _lib = L
     return L
@@ -201,12 +201,14 @@ class Context:
         return out
 
     def stats(self):
-        ms = (ctypes.c_float * 7)()
-        cl = np.zeros(8, dtype=np.uint64)
+        ms = (ctypes.c_float * 11)()
+        cl = np.zeros(10, dtype=np.uint64)
         fl = ctypes.c_int()
-        self._check(self._L.dmx_stats(self._h, ms, 7, cl.ctypes.data, ctypes.byref(fl)),
+        self._check(self._L.dmx_stats(self._h, ms, 11, cl.ctypes.data, 10, ctypes.byref(fl)),
                     "dmx_stats")
-        names = ["scan0", "resolve0", "finalize0", "scan1", "resolve1", "finalize1", "total"]
+        names = ["scan0", "resolve0", "finalize0", "scan1", "resolve1", "finalize1", "total",
+                 "filter0", "verify0", "filter1", "verify1"]
         return {"ms": dict(zip(names, list(ms))), "clusters": cl[:2].tolist(),
                 "windows": cl[2:4].tolist(), "resolved": cl[4:6].tolist(),
-                "traces": cl[6:8].tolist(), "flags": fl.value}
+                "traces": cl[6:8].tolist(), "windows_raw": cl[8:10].tolist(),
+                "flags": fl.value}
