@@ -152,7 +152,9 @@ int ensure_pipeline(Ctx* c) {
         int rc;
         if ((rc = dev_alloc(c, &c->d_win, want_win))) return rc;
         if ((rc = dev_alloc(c, &c->d_win2, want_win))) return rc;
+        if ((rc = dev_alloc(c, &c->d_pairs, 4 * want_win))) return rc;
         c->win_cap = want_win;
+        c->pair_cap = 4 * want_win;
     }
     const size_t a1 = c->mode == DMX_MODE_SINGLE ? 0 : (size_t)c->panel[1].n;
     const size_t nc = ((size_t)c->panel[0].n + 1) * (a1 + 1) + 2;
@@ -181,7 +183,9 @@ int grow_windows(Ctx* c) {
     int rc;
     if ((rc = dev_alloc(c, &c->d_win, want))) return rc;
     if ((rc = dev_alloc(c, &c->d_win2, want))) return rc;
+    if ((rc = dev_alloc(c, &c->d_pairs, 4 * want))) return rc;
     c->win_cap = want;
+    c->pair_cap = 4 * want;
     return DMX_OK;
 }
 
@@ -218,6 +222,8 @@ int dmx_open(int device, dmx_ctx** out) {
     c->no_verify = nv && nv[0] == '1';
     const char* rs = std::getenv("DMX_RESOLVE");
     c->force_ring = rs && std::strcmp(rs, "ring") == 0;
+    const char* ns = std::getenv("DMX_SIEVE");   // experimental window sieve (default off)
+    c->no_sieve = !(ns && ns[0] == '1');
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -236,7 +242,7 @@ void dmx_close(dmx_ctx* c) {
     hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_seq_alloc, c->d_nmask_alloc,     c->d_offs,     c->d_lens,      c->d_res,
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
-                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_counters,
+                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_pairs, c->d_counters,
                     c->d_counts,    c->d_panel[0],  c->d_panel[1]};
     for (void* b : bufs)
         if (b) hipFree(b);
@@ -412,6 +418,7 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
         }
         dp.kf = kf;
         dp.max_mk = mk;
+        hp.sieve = mk + 16 + 15 <= 112;   // window sieve: >= 16 candidate columns per piece
         // shared prefix for the verification pass
         int pre = lens[0];
         int mmin = 1 << 30, mmax = 0;
@@ -618,8 +625,11 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
     uint32_t cnt[32];
     CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
     if (getenv("DMX_DEBUG_STATS"))
-        fprintf(stderr, "dmx stats: resolve max window %u %u, total window columns %u %u\n",
-                cnt[18], cnt[22], cnt[19], cnt[23]);
+        fprintf(stderr,
+                "dmx stats: windows raw %u %u verified %u %u sieve pieces %u %u pairs %u %u cand %u %u "
+                "%u %u\n",
+                cnt[4], cnt[5], cnt[10], cnt[11], cnt[18], cnt[22], cnt[12], cnt[13], cnt[6],
+                cnt[7], cnt[8], cnt[9]);
     if (counts) {
         const bool b0 = c->band_ok[0] && !c->force_ring, b1 = c->band_ok[1] && !c->force_ring;
         const uint64_t v[10] = {cnt[0],
@@ -639,6 +649,7 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
         if (cnt[0] > c->cl_cap || cnt[1] > c->cl_cap) f |= 1;
         if (cnt[4] > c->win_cap || cnt[5] > c->win_cap) f |= 4;
         if (cnt[10] > c->win_cap || cnt[11] > c->win_cap) f |= 4;
+        if (cnt[12] > c->pair_cap || cnt[13] > c->pair_cap) f |= 4;
         for (int x = 6; x < 10; ++x)
             if (cnt[x] > c->cand_cap) f |= 8;
         *flags = f;

@@ -86,6 +86,16 @@ struct Window {
 };
 static_assert(sizeof(Window) == 40, "Window layout");
 
+// A (window, adapter) pair that survived the window sieve, with the candidate column range
+// [jlo, jhi] (a piece of the window's [j1, j2]); the window scan runs only these.
+struct Pair {
+    uint32_t win;
+    uint32_t jlo, jhi;
+    uint16_t a;
+    uint16_t pad;
+};
+static_assert(sizeof(Pair) == 16, "Pair layout");
+
 constexpr int kStageCap = 256;    // LDS staging of emitted records per block
 constexpr int kCandStageCap = 128; // per candidate list
 
@@ -221,17 +231,47 @@ __device__ __forceinline__ void fetch16(const uint32_t* __restrict__ seq,
 // One Myers/Hyyro column step for semi-global matching with a free start in the read
 // (D(0, j) = 0 for all j, so the row-0 horizontal delta shifted in is 0).
 // Bit i-1 of Pv/Mv: vertical delta D(i, j) - D(i-1, j) is +1 / -1.
+// Written on 32-bit halves so gfx950 folds the boolean algebra into v_bitop3 (the 64-bit form
+// compiles to separate and/or/xor pairs); one 64-bit add carries between the halves.
+// HB: 0 = the last row's bit (hbit) is in the low word, 1 = in the high word, -1 = select.
+template <int HB>
+__device__ __forceinline__ void myers_step_hw(uint32_t eql, uint32_t eqh, uint32_t& pvl,
+                                              uint32_t& pvh, uint32_t& mvl, uint32_t& mvh, int& d,
+                                              uint32_t hbit) {
+    const uint32_t xvl = eql | mvl, xvh = eqh | mvh;
+    const uint64_t t = ((uint64_t)(eqh & pvh) << 32) | (eql & pvl);
+    const uint64_t s = t + (((uint64_t)pvh << 32) | pvl);
+    const uint32_t xhl = ((uint32_t)s ^ pvl) | eql, xhh = ((uint32_t)(s >> 32) ^ pvh) | eqh;
+    const uint32_t phl = mvl | ~(xhl | pvl), phh = mvh | ~(xhh | pvh);
+    const uint32_t mhl = pvl & xhl, mhh = pvh & xhh;
+    uint32_t ps, ms;
+    if constexpr (HB == 0) {
+        ps = phl;
+        ms = mhl;
+    } else if constexpr (HB == 1) {
+        ps = phh;
+        ms = mhh;
+    } else {
+        ps = hbit >= 32 ? phh : phl;
+        ms = hbit >= 32 ? mhh : mhl;
+    }
+    d += (int)__builtin_amdgcn_ubfe(ps, hbit & 31u, 1) +
+         __builtin_amdgcn_sbfe((int)ms, hbit & 31u, 1);
+    const uint32_t phh1 = __builtin_amdgcn_alignbit(phh, phl, 31), phl1 = phl << 1;
+    const uint32_t mhh1 = __builtin_amdgcn_alignbit(mhh, mhl, 31), mhl1 = mhl << 1;
+    pvl = mhl1 | ~(xvl | phl1);
+    pvh = mhh1 | ~(xvh | phh1);
+    mvl = phl1 & xvl;
+    mvh = phh1 & xvh;
+}
+
 __device__ __forceinline__ void myers_step(uint64_t eq, uint64_t& pv, uint64_t& mv, int& d,
                                            uint32_t hbit) {
-    const uint64_t xv = eq | mv;
-    const uint64_t xh = (((eq & pv) + pv) ^ pv) | eq;
-    uint64_t ph = mv | ~(xh | pv);
-    uint64_t mh = pv & xh;
-    d += (int)((ph >> hbit) & 1u) - (int)((mh >> hbit) & 1u);
-    ph <<= 1;
-    mh <<= 1;
-    pv = mh | ~(xv | ph);
-    mv = ph & xv;
+    uint32_t pvl = (uint32_t)pv, pvh = (uint32_t)(pv >> 32);
+    uint32_t mvl = (uint32_t)mv, mvh = (uint32_t)(mv >> 32);
+    myers_step_hw<-1>((uint32_t)eq, (uint32_t)(eq >> 32), pvl, pvh, mvl, mvh, d, hbit);
+    pv = ((uint64_t)pvh << 32) | pvl;
+    mv = ((uint64_t)mvh << 32) | mvl;
 }
 
 // 32-bit variant for the shared-suffix filter block.

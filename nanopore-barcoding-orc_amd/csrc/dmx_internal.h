@@ -11,6 +11,7 @@
 namespace dmx {
 
 struct HostPanel {
+    bool sieve = false;       // window sieve usable (band mode, max_mk small enough)
     int n = 0;
     int n_orient = 1;
     bool set = false;
@@ -62,7 +63,10 @@ struct Ctx {
     size_t item_cap = 0;
     uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows, [6+2r..] candidates, [10+r] verified windows, [16+4r..] diag
     unsigned long long* d_counts = nullptr;
-    unsigned long long* d_linked = nullptr;   // linked mode: best pair key per read
+    unsigned long long* d_linked = nullptr;
+    Pair* d_pairs = nullptr;             // window sieve survivors
+    size_t pair_cap = 0;
+    bool no_sieve = true;                // window sieve off unless DMX_SIEVE=1   // linked mode: best pair key per read
     size_t n_counts = 0;
     hipEvent_t ev[13] = {};   // [3r..3r+2] round r stages, [6+r] finalize, [8] start,
                               // [9+2r] after filter, [10+2r] after verify

@@ -44,6 +44,10 @@ struct RoundArgs {
     Outcome* cand_out[2];
     uint32_t* cand_count;        // [2]
     uint32_t cand_cap;
+    int32_t sieve;               // 1: the window scan runs the sieve's surviving pairs
+    Pair* pairs;
+    uint32_t* pair_count;
+    uint32_t pair_cap;
 };
 
 struct TaskView {
@@ -879,6 +883,181 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
 
 // Window scan: one lane per (window, adapter); block-uniform grid-stride over the device-side
 // window count so that the block can flush its staged records between strides.
+// ---------------------------------------------------------------------------------------------
+// window sieve: one lane per window, adapters in a block-uniform loop (their parameters are
+// scalar, their match vectors an LDS broadcast).  Each adapter's 64-bit Myers runs over the
+// window's columns with branch-free steps; a (window piece, adapter) pair survives when some
+// candidate column j in [jlo, jhi] has cost d <= thr(j) = the largest d <= kk with
+// d <= pacc[min(m, j + d)] (a superset of the window scan's candidate test), or, for a 3'
+// window at the view end, when some last-column row is accepted.  Only survivors reach the
+// window scan, which then decides every cell exactly.  A window longer than kSieveSpan columns
+// is cut into pieces [jlo, jhi] of at most sieve_cr candidate columns.
+// ---------------------------------------------------------------------------------------------
+constexpr int kSieveChunks = 7;
+constexpr int kSieveSpan = 16 * kSieveChunks;     // view positions held per lane
+
+__global__ __launch_bounds__(kScanBlock) void sieve_kernel(RoundArgs R) {
+    __shared__ uint64_t s_peq[8 * kMaxAdapters];
+    __shared__ __attribute__((aligned(16))) int8_t s_thr[kMaxAdapters * 128];
+    __shared__ Pair s_pair[kStageCap];
+    __shared__ uint32_t s_pc, s_pb;
+    __shared__ uint2 s_code[kSieveChunks][kScanBlock];
+    __shared__ int s_m[kMaxAdapters];
+    __shared__ int8_t s_acc[72 * kMaxAdapters];
+    __shared__ uint32_t s_pfx[kScanBlock];
+    const DevPanel* P = R.panel;
+    const int A = P->n_adapters;
+    for (int x = threadIdx.x; x < 8 * A; x += blockDim.x) s_peq[x] = P->ad[x % A].peq[x / A];
+    for (int x = threadIdx.x; x < A; x += blockDim.x) s_m[x] = P->ad[x].m;
+    for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
+    for (int x = threadIdx.x; x < 128 * A; x += blockDim.x) {
+        const DevAdapter& ad = P->ad[x >> 7];
+        const int j = (x & 127) + 1;                   // column after view position x & 127
+        int t = -1;
+        for (int d = 0; d <= ad.kk; ++d)
+            if (d <= (int)ad.pacc[min((int)ad.m, j + d)]) t = d;
+        s_thr[x] = (int8_t)t;
+    }
+    if (threadIdx.x == 0) s_pc = 0;
+    __syncthreads();
+    const Stage<Pair> st{s_pair, &s_pc, &s_pb, R.pairs, R.pair_count, R.pair_cap, R.flags, 4u};
+    const Window* wl = P->pre_len ? R.win2 : R.win;
+    const uint32_t* wc = P->pre_len ? R.win2_count : R.win_count;
+    const uint32_t total = min(*wc, R.win_cap);
+    const bool front = P->where == kFront;
+    const int max_mk = P->max_mk;
+    const int cr = kSieveSpan - 15 - max_mk;           // candidate columns per piece (host: >= 16)
+
+    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
+        // pieces of this block's windows, flattened so every lane takes one piece per round
+        {
+            const uint32_t wi = base + threadIdx.x;
+            uint32_t np = 0;
+            if (wi < total) {
+                const Window w = wl[wi];
+                np = (w.j2 - w.j1) / (uint32_t)cr + 1;
+            }
+            s_pfx[threadIdx.x] = np;
+        }
+        __syncthreads();
+        for (uint32_t dlt = 1; dlt < kScanBlock; dlt <<= 1) {   // inclusive scan
+            const uint32_t x = threadIdx.x >= dlt ? s_pfx[threadIdx.x - dlt] : 0u;
+            __syncthreads();
+            s_pfx[threadIdx.x] += x;
+            __syncthreads();
+        }
+        const uint32_t npieces = s_pfx[kScanBlock - 1];
+        for (uint32_t pb = 0; pb < npieces; pb += kScanBlock) {
+        const uint32_t pi = pb + threadIdx.x;
+        const bool act = pi < npieces;
+        Window w;
+        uint32_t wi = 0, jlo = 1, jhi = 0;
+        if (act) {
+            uint32_t lo = 0, hi = kScanBlock - 1;      // first lane with inclusive prefix > pi
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_pfx[mid] > pi) hi = mid;
+                else lo = mid + 1;
+            }
+            const uint32_t before = lo ? s_pfx[lo - 1] : 0u;
+            wi = base + lo;
+            w = wl[wi];
+            jlo = w.j1 + (pi - before) * (uint32_t)cr;
+            jhi = min(w.j2, jlo + (uint32_t)cr - 1);
+        } else {
+            w.j1 = 1;
+            w.j2 = 0;
+            w.lastcol = 0;
+            w.len = 0;
+        }
+        {
+            const int s0 = max(0, (int)jlo - max_mk);
+            const bool lastc = !front && w.lastcol && jhi == w.j2;
+            // chunk grid: 16-aligned from `start`; a 3' window at the view end is aligned to end
+            // exactly at jhi (its last-column state is then the state after the chunk loop)
+            uint32_t start = s0 <= 0 ? 0u : ((uint32_t)s0 & ~15u);
+            int nch = (int)((jhi - start + 15) / 16);
+            bool fallback = false;
+            if (lastc) {
+                const int n2 = (int)((jhi - (uint32_t)s0 + 15) / 16);
+                const int st2 = (int)jhi - 16 * n2;
+                if (st2 >= 64) {                       // thresholds are kk that far from 0
+                    start = (uint32_t)st2;
+                    nch = n2;
+                } else {
+                    fallback = true;                   // short view: the window scan decides
+                }
+            }
+            if (!act) nch = 0;
+            const bool real = start == 0;
+            // the piece's codes stay in a lane-private LDS column for all adapters
+            for (int c = 0; c < nch; ++c) {
+                uint32_t cc, nn;
+                fetch16(R.seq, R.nmask, w.off, w.n, w.strand, w.start, start + 16u * c, cc, nn);
+                s_code[c][threadIdx.x] = make_uint2(cc, nn);
+            }
+            for (int a = 0; a < A; ++a) {
+                const int m = __builtin_amdgcn_readfirstlane(s_m[a]);   // LDS: no byte loads
+                const uint32_t hbit = (uint32_t)(m - 1);
+                const bool zero = real && front;
+                uint64_t pv = zero ? 0ull : ~0ull, mv = 0ull;
+                int d = zero ? 0 : m;
+                bool surv = fallback;
+                const int8_t* thr_row = s_thr + 128 * a;
+                for (int c = 0; c < nch; ++c) {
+                    {
+                        const uint32_t p0 = start + 16u * (uint32_t)c;
+                        const uint2 cn = s_code[c][threadIdx.x];
+                        const uint32_t codes = cn.x, nb = cn.y;
+                        // thresholds: the table below column 64 (16-aligned there), kk beyond
+                        const uint4 tw =
+                            *reinterpret_cast<const uint4*>(thr_row + (p0 < 64u ? p0 : 112u));
+                        uint32_t hits = 0;
+#pragma unroll
+                        for (int q = 0; q < 16; ++q) {
+                            const uint32_t code =
+                                ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
+                            myers_step(s_peq[code * A + a], pv, mv, d, hbit);
+                            const uint32_t wd = q < 4 ? tw.x : q < 8 ? tw.y : q < 12 ? tw.z : tw.w;
+                            const int t = __builtin_amdgcn_sbfe((int)wd, 8 * (q & 3), 8);
+                            hits |= d <= t ? (1u << q) : 0u;
+                        }
+                        // candidate columns j = p0 + q + 1 in [jlo, jhi]
+                        const int lo = (int)jlo - (int)p0 - 1, hi = (int)jhi - (int)p0 - 1;
+                        const uint32_t mlo = lo <= 0 ? 0xFFFFu : (lo >= 16 ? 0u : (0xFFFFu << lo));
+                        const uint32_t mhi =
+                            hi >= 15 ? 0xFFFFu : (hi < 0 ? 0u : (0xFFFFu >> (15 - hi)));
+                        surv |= (hits & mlo & mhi & 0xFFFFu) != 0u;
+                    }
+                }
+                if (lastc && !surv) {
+                    // last-column rows i < m at column len: cost D(i, len) <= acc[i]
+                    int dd = 0;
+                    for (int i = 1; i < m; ++i) {
+                        dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
+                        surv |= dd <= (int)s_acc[72 * a + i];
+                    }
+                }
+                if (act && surv) {
+                    Pair pr;
+                    pr.win = wi;
+                    pr.jlo = jlo;
+                    pr.jhi = jhi;
+                    pr.a = (uint16_t)a;
+                    pr.pad = 0;
+                    st.push(pr);
+                }
+            }
+        }
+        const int np = __syncthreads_count(act);       // also orders the staged count
+        if (threadIdx.x == 0) atomicAdd(&R.diag[2], (uint32_t)np);   // pieces (diagnostic)
+        if (s_pc > kStageCap / 2) st.flush();
+        }
+        __syncthreads();                               // s_pfx is rewritten next
+    }
+    st.flush();
+}
+
 template <bool BAND>
 __global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kMaxAdapters];
@@ -891,13 +1070,25 @@ __global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
     const int A = R.panel->n_adapters;
     const Window* wl = R.panel->pre_len ? R.win2 : R.win;
     const uint32_t* wc = R.panel->pre_len ? R.win2_count : R.win_count;
-    const uint64_t total = (uint64_t)min(*wc, R.win_cap) * (uint64_t)A;
+    const uint64_t total = R.sieve ? (uint64_t)min(*R.pair_count, R.pair_cap)
+                                   : (uint64_t)min(*wc, R.win_cap) * (uint64_t)A;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < total;
          base += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t t = base + threadIdx.x;
         if (t < total) {
-            const Window w = wl[t / A];
-            const int a = (int)(t % A);
+            Window w;
+            int a;
+            if (R.sieve) {   // one surviving (window piece, adapter) pair
+                const Pair pr = R.pairs[t];
+                w = wl[pr.win];
+                a = pr.a;
+                w.lastcol = (w.lastcol && pr.jhi == w.j2) ? 1 : 0;
+                w.j1 = pr.jlo;
+                w.j2 = pr.jhi;
+            } else {
+                w = wl[t / A];
+                a = (int)(t % A);
+            }
             const int sub = w.o * A + a;
             TaskView tv;
             tv.read = 0;
@@ -1637,6 +1828,10 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     }
     R.cand_count = c->d_counters + 6 + 2 * round;
     R.cand_cap = (uint32_t)c->cand_cap;
+    R.sieve = (band && hp.filter && hp.sieve && !linked && !c->no_sieve) ? 1 : 0;
+    R.pairs = c->d_pairs;
+    R.pair_count = c->d_counters + 12 + round;
+    R.pair_cap = (uint32_t)c->pair_cap;
     hipEventRecord(c->ev[round * 3 + 0], st);
     if (hp.filter && !linked) {   // linked primers: short, no shared suffix block; plain scan
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
@@ -1646,6 +1841,8 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         if (hp.verify)
             hipLaunchKernelGGL(verify_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
         hipEventRecord(c->ev[10 + 2 * round], st);
+        if (R.sieve)
+            hipLaunchKernelGGL(sieve_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
         if (band) hipLaunchKernelGGL(wscan_kernel<true>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(wscan_kernel<false>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
     } else if (grid > 0) {
