@@ -1465,67 +1465,193 @@ __device__ __forceinline__ void band_dp(const PeqRegs& peq, const uint32_t* seq,
     score = S[H];
 }
 
-// Band kernel: one lane per candidate cell of one list (fixed band width W for the whole list,
-// so every lane of a wave runs the same code).  The slot's best is the minimum key over all its
-// candidates (key order = locate's / best_match's / ReverseComplementer's selection order).
+// Banded DP, two state words per cell: C = cost and P = origin * 256 + V, V = vertical moves on
+// the chosen path.  The score follows from them at the end cell: with A adapter chars aligned,
+// score = matches - mismatches - 2 * indels = A - 2 * cost - V (A = ie, or ie - i0 for a FRONT
+// path entering at column 0 of row i0).  Cutadapt's pointer rule (_align.pyx) as selects:
+//   diagonal if the characters match or cost(diag) <= min(up, left); else up (insertion) if
+//   cost(up) <= cost(left); else left.  EDGE: the band reaches column 0 or beyond the view end.
+template <int W, bool EDGE>
+__device__ __forceinline__ void band_dp2(const uint8_t* rm, const uint32_t* seq,
+                                         const uint32_t* nmask, const TaskView& tv, bool front,
+                                         int ie, int je, int& cost, int& origin, int& score) {
+    constexpr int H = W / 2;
+    constexpr int INF = 1 << 20;
+    const int dx = je - ie;            // diagonal of the end cell; cell k <-> diagonal dx-H+k
+    const int n = (int)tv.len;
+    int C[W], P[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) {      // row 0: free start in the read
+        const int jj = dx - H + k;
+        C[k] = (EDGE && (jj < 0 || jj > n)) ? INF : 0;
+        P[k] = jj * 256;
+    }
+    // read codes of row i, cell k: view position i - 1 + dx - H + k; a 48-position window of
+    // three 16-code words (w0 current, w1 next, w2 prefetched) advancing 16 rows at a time
+    int base = dx - H;
+    uint32_t w0, n0, w1, n1, w2, n2;
+    fetch16s(seq, nmask, tv, base, w0, n0);
+    fetch16s(seq, nmask, tv, base + 16, w1, n1);
+    fetch16s(seq, nmask, tv, base + 32, w2, n2);
+    int o = 0;
+    uint32_t rnext = rm[0];
+    for (int i = 1; i <= ie; ++i) {
+        if (o == 16) {                 // uniform: every lane advances one row per iteration
+            w0 = w1;
+            n0 = n1;
+            w1 = w2;
+            n1 = n2;
+            base += 16;
+            fetch16s(seq, nmask, tv, base + 32, w2, n2);
+            o = 0;
+        }
+        const uint32_t codes = o ? __builtin_amdgcn_alignbit(w1, w0, 2 * o) : w0;
+        const uint32_t nb = ((n1 << 16) | n0) >> o;
+        const uint32_t rmask = rnext;
+        rnext = rm[min(i, 63)];
+        int lc = INF, lp = 0;          // left neighbour (same row, already updated)
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            const int uc = (k + 1 < W) ? C[(k + 1) % W] : INF;
+            const int up = (k + 1 < W) ? P[(k + 1) % W] : 0;
+            const uint32_t code = (codes >> (2 * k)) & 3u;
+            const bool eq = ((rmask >> code) & 1u) > ((nb >> k) & 1u);   // N matches nothing
+            const int mn = min(lc, uc);
+            const int ip = uc <= lc ? up + 1 : lp;
+            const bool td = eq || C[k] <= mn;
+            int c = td ? C[k] + (eq ? 0 : 1) : mn + 1;
+            int pp = td ? P[k] : ip;
+            if constexpr (EDGE) {
+                const int jj = i + dx - H + k;
+                if (jj == 0) {                         // column 0: cutadapt's initialisation
+                    c = front ? 0 : i;
+                    pp = front ? -i * 256 : i;
+                }
+                if (jj < 0 || jj > n) c = INF;
+            }
+            C[k] = c;
+            P[k] = pp;
+            lc = c;
+            lp = pp;
+        }
+        ++o;
+    }
+    cost = C[H];
+    origin = P[H] >> 8;
+    const int v = P[H] & 255;
+    score = ie - max(-origin, 0) - 2 * cost - v;
+}
+
+// Band kernel over one candidate list (fixed band width W, so every lane of a wave runs the same
+// code).  Per block round of 256 candidates: cheap checks first (score upper bound against the
+// slot's lower bound and current winner; cost-0 cells need no DP), then the surviving cells are
+// compacted in LDS — band-interior ones from the front, ones touching column 0 or the view end
+// from the back — so full waves run each DP variant.  The slot's best is the minimum key over all
+// its candidates (key order = locate's / best_match's / ReverseComplementer's selection order).
 template <int W>
 __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
+    __shared__ uint8_t s_rm[kMaxAdapters * 64];   // s_rm[a * 64 + i]: bit c = char i matches c
+    __shared__ uint32_t s_q[256];
+    __shared__ uint32_t s_qi, s_qe, s_n;
+    const DevPanel* P = R.panel;
+    const int A = P->n_adapters;
+    for (int x = threadIdx.x; x < 64 * A; x += blockDim.x) {
+        const DevAdapter& ad = P->ad[x >> 6];
+        const int i = x & 63;
+        uint32_t r = 0;
+        for (int c = 0; c < 4; ++c) r |= (uint32_t)((ad.peq[c] >> i) & 1ull) << c;
+        s_rm[x] = (uint8_t)r;
+    }
+    if (threadIdx.x == 0) {
+        s_qi = 0;
+        s_qe = 0;
+        s_n = 0;
+    }
+    __syncthreads();
     const uint32_t total = min(R.cand_count[list], R.cand_cap);
     const Cand* cl = R.cand[list];
     Outcome* outs = R.cand_out[list];
-    uint32_t n_dp = 0;
-    for (uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x; ci < total;
-         ci += gridDim.x * blockDim.x) {
-        const Cand c = cl[ci];
-        const uint32_t slot = slot_of(R, c.item, c.sub);
-        const int cost = c.cost, iend = c.iend;
-        const int j = (int)c.j;
-        const DevAdapter& ad = R.panel->ad[c.a];
-        const int m = ad.m;
-        const uint64_t t = iend == m ? (uint64_t)j : (uint64_t)c.len + 1 + iend;
-        Outcome out;
-        out.key = ~0ull;
-        out.origin = 0;
-        out.pad = 0;
-        const int lrmax = min(iend, j + cost);
-        const int ub = lrmax - 2 * cost;
-        if (viable_lb(R.lb[slot], lrmax, cost) &&
-            make_key(ub, c.o, cost, c.a, t) <= R.winner[slot]) {
-            int origin, score;
-            if (cost == 0) {                  // exact: the pointer chain is the pure diagonal
-                origin = j - iend;
-                score = j >= iend ? iend : j;
-            } else {
-                TaskView tv;
-                tv.read = 0;
-                tv.n = c.n;
-                tv.strand = c.strand;
-                tv.start = c.start;
-                tv.len = c.len;
-                tv.off = c.off;
-                tv.o = c.o;
-                tv.a = c.a;
-                const PeqRegs peq{ad.peq[0], ad.peq[1], ad.peq[2], ad.peq[3]};
-                int c2;
-                band_dp<W>(peq, R.seq, R.nmask, tv, ad.where == kFront, iend, j, c2, origin,
-                           score);
-                ++n_dp;
-                if (c2 != cost) atomicOr(R.flags, 2u);    // band / scan disagreement: bug
+    constexpr int H = W / 2;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
+        const uint32_t ci = base + threadIdx.x;
+        if (ci < total) {
+            const Cand c = cl[ci];
+            const uint32_t slot = slot_of(R, c.item, c.sub);
+            const int cost = c.cost, iend = c.iend;
+            const int j = (int)c.j;
+            const uint64_t t = iend == P->ad[c.a].m ? (uint64_t)j : (uint64_t)c.len + 1 + iend;
+            Outcome out;
+            out.key = ~0ull;
+            out.origin = 0;
+            out.pad = 0;
+            const int lrmax = min(iend, j + cost);
+            const int ub = lrmax - 2 * cost;
+            if (viable_lb(R.lb[slot], lrmax, cost) &&
+                make_key(ub, c.o, cost, c.a, t) <= R.winner[slot]) {
+                if (cost == 0) {              // exact: the pointer chain is the pure diagonal
+                    const int origin = j - iend;
+                    const int score = j >= iend ? iend : j;
+                    const int lr = iend + (origin < 0 ? origin : 0);
+                    if (lr >= 0 && 0 <= (int)P->ad[c.a].acc[lr]) {
+                        out.key = make_key(score, c.o, 0, c.a, t);
+                        out.origin = origin;
+                        atomicMin(&R.winner[slot], (unsigned long long)out.key);
+                    }
+                } else {
+                    const int dx = j - iend;
+                    const bool edge = dx - H < 0 || j + H > (int)c.len;
+                    const uint32_t q = edge ? 255u - atomicAdd(&s_qe, 1u) : atomicAdd(&s_qi, 1u);
+                    s_q[q] = ci;
+                }
             }
+            outs[ci] = out;
+        }
+        __syncthreads();
+        const uint32_t ni = s_qi, ne = s_qe;
+        const bool mine = threadIdx.x < ni || threadIdx.x >= 256u - ne;
+        if (mine) {
+            const uint32_t ci = s_q[threadIdx.x];
+            const Cand c = cl[ci];
+            const uint32_t slot = slot_of(R, c.item, c.sub);
+            const int cost = c.cost, iend = c.iend;
+            const int j = (int)c.j;
+            const DevAdapter& ad = P->ad[c.a];
+            const uint64_t t = iend == ad.m ? (uint64_t)j : (uint64_t)c.len + 1 + iend;
+            TaskView tv;
+            tv.read = 0;
+            tv.n = c.n;
+            tv.strand = c.strand;
+            tv.start = c.start;
+            tv.len = c.len;
+            tv.off = c.off;
+            tv.o = c.o;
+            tv.a = c.a;
+            int c2, origin, score;
+            if (threadIdx.x < ni)
+                band_dp2<W, false>(s_rm + 64 * c.a, R.seq, R.nmask, tv, ad.where == kFront, iend,
+                                   j, c2, origin, score);
+            else
+                band_dp2<W, true>(s_rm + 64 * c.a, R.seq, R.nmask, tv, ad.where == kFront, iend,
+                                  j, c2, origin, score);
+            if (c2 != cost) atomicOr(R.flags, 2u);    // band / scan disagreement: bug
             const int lr = iend + (origin < 0 ? origin : 0);
             if (lr >= 0 && cost <= (int)ad.acc[lr]) {
+                Outcome out;
                 out.key = make_key(score, c.o, cost, c.a, t);
                 out.origin = origin;
+                out.pad = 0;
                 atomicMin(&R.winner[slot], (unsigned long long)out.key);
+                outs[ci] = out;
             }
         }
-        outs[ci] = out;
+        const int nd = __syncthreads_count(mine);
+        if (threadIdx.x == 0) {
+            s_n += (uint32_t)nd;
+            s_qi = 0;
+            s_qe = 0;
+        }
+        __syncthreads();
     }
-    __shared__ uint32_t s_n;
-    if (threadIdx.x == 0) s_n = 0;
-    __syncthreads();
-    if (n_dp) atomicAdd(&s_n, n_dp);
-    __syncthreads();
     if (threadIdx.x == 0 && s_n) atomicAdd(R.diag + 1, s_n);
 }
 
