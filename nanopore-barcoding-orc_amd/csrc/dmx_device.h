@@ -239,9 +239,10 @@ __device__ __forceinline__ void myers_step_hw(uint32_t eql, uint32_t eqh, uint32
                                               uint32_t& pvh, uint32_t& mvl, uint32_t& mvh, int& d,
                                               uint32_t hbit) {
     const uint32_t xvl = eql | mvl, xvh = eqh | mvh;
-    const uint64_t t = ((uint64_t)(eqh & pvh) << 32) | (eql & pvl);
-    const uint64_t s = t + (((uint64_t)pvh << 32) | pvl);
-    const uint32_t xhl = ((uint32_t)s ^ pvl) | eql, xhh = ((uint32_t)(s >> 32) ^ pvh) | eqh;
+    uint32_t cy, cy2;
+    const uint32_t sl = __builtin_addc(eql & pvl, pvl, 0u, &cy);     // v_add_co / v_addc_co
+    const uint32_t sh = __builtin_addc(eqh & pvh, pvh, cy, &cy2);
+    const uint32_t xhl = (sl ^ pvl) | eql, xhh = (sh ^ pvh) | eqh;
     const uint32_t phl = mvl | ~(xhl | pvl), phh = mvh | ~(xhh | pvh);
     const uint32_t mhl = pvl & xhl, mhh = pvh & xhh;
     uint32_t ps, ms;
@@ -265,11 +266,12 @@ __device__ __forceinline__ void myers_step_hw(uint32_t eql, uint32_t eqh, uint32
     mvh = phh1 & xvh;
 }
 
+template <int HB = -1>
 __device__ __forceinline__ void myers_step(uint64_t eq, uint64_t& pv, uint64_t& mv, int& d,
                                            uint32_t hbit) {
     uint32_t pvl = (uint32_t)pv, pvh = (uint32_t)(pv >> 32);
     uint32_t mvl = (uint32_t)mv, mvh = (uint32_t)(mv >> 32);
-    myers_step_hw<-1>((uint32_t)eq, (uint32_t)(eq >> 32), pvl, pvh, mvl, mvh, d, hbit);
+    myers_step_hw<HB>((uint32_t)eq, (uint32_t)(eq >> 32), pvl, pvh, mvl, mvh, d, hbit);
     pv = ((uint64_t)pvh << 32) | pvl;
     mv = ((uint64_t)mvh << 32) | mvl;
 }

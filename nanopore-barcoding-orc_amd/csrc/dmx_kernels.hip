@@ -100,8 +100,8 @@ __device__ __forceinline__ void load_panel_lds(const DevPanel* P, uint64_t* s_pe
                                                int8_t* s_pacc) {
     const int A = P->n_adapters;
     for (int x = threadIdx.x; x < 8 * A; x += blockDim.x) {
-        const int c = x / A, a = x % A;
-        s_peq[x] = P->ad[a].peq[c];   // code-major: lanes of one read hit consecutive words
+        const int c = x / A, a = x % A;   // code-major, power-of-two row stride (no multiply)
+        s_peq[c * kMaxAdapters + a] = P->ad[a].peq[c];   // lanes of one read: consecutive words
     }
     for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) {
         s_acc[x] = P->ad[x / 72].acc[x % 72];
@@ -163,7 +163,7 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
 #define DMX_SCAN_STEP(q)                                                                  \
     {                                                                                     \
         const uint32_t code = ((codes >> (2 * (q))) & 3u) | (((nb >> (q)) & 1u) << 2);    \
-        myers_step(peq[code * A], pv, mv, d, hbit);                                       \
+        myers_step(peq[code * kMaxAdapters], pv, mv, d, hbit);                                       \
         if (d <= kk) {                                                                    \
             const uint32_t j = p0 + (q) + 1;                                              \
             const int lr = min(m, (int)j + d);                                            \
@@ -263,6 +263,22 @@ __device__ __forceinline__ bool viable_lb(int lbk, int lr, int cost) {
     return ub > lbs || (ub == lbs && cost <= lbc);
 }
 
+// 16 view positions from view position p (may be negative or past the view: guard words).
+__device__ __forceinline__ void fetch16s(const uint32_t* __restrict__ seq,
+                                         const uint32_t* __restrict__ nmask, const TaskView& tv,
+                                         int p, uint32_t& codes, uint32_t& nbits) {
+    if (tv.strand == 0) {
+        const uint64_t g = (uint64_t)((int64_t)tv.off + (int64_t)tv.start + p);
+        codes = window32(seq, 2 * g);
+        nbits = window32(nmask, g) & 0xFFFFu;
+    } else {
+        const uint64_t b = (uint64_t)((int64_t)tv.off + (int64_t)tv.n - 1 - (int64_t)tv.start -
+                                      p - 15);
+        codes = ~rev_pairs(window32(seq, 2 * b));
+        nbits = __brev(window32(nmask, b)) >> 16;
+    }
+}
+
 __device__ __forceinline__ void flush_cands(const CandSink& sink, const TaskView& tv, uint32_t item,
                                          int sub, int m, int lbk, uint32_t seg, uint64_t cm,
                                          uint64_t c0, uint64_t c1, uint64_t c2) {
@@ -279,12 +295,13 @@ __device__ __forceinline__ void flush_cands(const CandSink& sink, const TaskView
     }
 }
 
-__device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const CandSink& sink,
-                                              const TaskView& tv, uint32_t item, int sub,
-                                              const uint64_t* peq, int A, const DevAdapter& ad,
-                                              const int8_t* acc, const int8_t* pacc,
-                                              uint32_t js, bool real, uint32_t jlo,
-                                              uint32_t jhi, bool lastcol) {
+template <int HB>
+__device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const CandSink& sink,
+                                                 const TaskView& tv, uint32_t item, int sub,
+                                                 const uint64_t* peq, int A, const DevAdapter& ad,
+                                                 const int8_t* acc, const int8_t* pacc,
+                                                 uint32_t js, bool real, uint32_t jlo,
+                                                 uint32_t jhi, bool lastcol) {
     const int m = ad.m;
     const int kk = ad.kk;   // <= 7 in band mode (three cost planes)
     const bool front = ad.where == kFront;
@@ -300,7 +317,7 @@ __device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const CandSink
 #define DMX_CAND_STEP(q)                                                                  \
     {                                                                                     \
         const uint32_t code = ((codes >> (2 * (q))) & 3u) | (((nb >> (q)) & 1u) << 2);    \
-        myers_step(peq[code * A], pv, mv, d, hbit);                                       \
+        myers_step<HB>(peq[code * kMaxAdapters], pv, mv, d, hbit);                                       \
         if (d <= kk) {                                                                    \
             const uint32_t j = p0 + (q) + 1;                                              \
             const int lr = min(m, (int)j + d);                                            \
@@ -372,6 +389,21 @@ __device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const CandSink
         else sink.st[1].push(cd);
     }
     return lbk;
+}
+
+// The last adapter row's bit sits in the low or the high word of the 64-bit vectors; both
+// variants are compiled so the step needs no per-column select.
+__device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const CandSink& sink,
+                                              const TaskView& tv, uint32_t item, int sub,
+                                              const uint64_t* peq, int A, const DevAdapter& ad,
+                                              const int8_t* acc, const int8_t* pacc,
+                                              uint32_t js, bool real, uint32_t jlo,
+                                              uint32_t jhi, bool lastcol) {
+    if (ad.m > 32)
+        return scan_task_cand_hb<1>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real, jlo,
+                                    jhi, lastcol);
+    return scan_task_cand_hb<0>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real, jlo, jhi,
+                                lastcol);
 }
 
 #define DMX_CAND_STAGE                                                                    \
@@ -907,7 +939,8 @@ __global__ __launch_bounds__(kScanBlock) void sieve_kernel(RoundArgs R) {
     __shared__ uint32_t s_pfx[kScanBlock];
     const DevPanel* P = R.panel;
     const int A = P->n_adapters;
-    for (int x = threadIdx.x; x < 8 * A; x += blockDim.x) s_peq[x] = P->ad[x % A].peq[x / A];
+    for (int x = threadIdx.x; x < 8 * A; x += blockDim.x)
+        s_peq[(x / A) * kMaxAdapters + x % A] = P->ad[x % A].peq[x / A];
     for (int x = threadIdx.x; x < A; x += blockDim.x) s_m[x] = P->ad[x].m;
     for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
     for (int x = threadIdx.x; x < 128 * A; x += blockDim.x) {
@@ -1017,7 +1050,7 @@ __global__ __launch_bounds__(kScanBlock) void sieve_kernel(RoundArgs R) {
                         for (int q = 0; q < 16; ++q) {
                             const uint32_t code =
                                 ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
-                            myers_step(s_peq[code * A + a], pv, mv, d, hbit);
+                            myers_step(s_peq[code * kMaxAdapters + a], pv, mv, d, hbit);
                             const uint32_t wd = q < 4 ? tw.x : q < 8 ? tw.y : q < 12 ? tw.z : tw.w;
                             const int t = __builtin_amdgcn_sbfe((int)wd, 8 * (q & 3), 8);
                             hits |= d <= t ? (1u << q) : 0u;
@@ -1383,88 +1416,6 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
 // with cutadapt's initialisation, reproduces cutadapt's origin and score of x exactly
 // (DESIGN.md §3.5).  The band lives in registers: no LDS, full occupancy, no traceback.
 // ---------------------------------------------------------------------------------------------
-// 16 codes of view positions [p, p+16) for a possibly negative p (positions outside the view
-// are fetched from the padding and never used).
-__device__ __forceinline__ void fetch16s(const uint32_t* __restrict__ seq,
-                                         const uint32_t* __restrict__ nmask, const TaskView& tv,
-                                         int p, uint32_t& codes, uint32_t& nbits) {
-    if (tv.strand == 0) {
-        const uint64_t g = (uint64_t)((int64_t)tv.off + (int64_t)tv.start + p);
-        codes = window32(seq, 2 * g);
-        nbits = window32(nmask, g) & 0xFFFFu;
-    } else {
-        const uint64_t b = (uint64_t)((int64_t)tv.off + (int64_t)tv.n - 1 - (int64_t)tv.start -
-                                      p - 15);
-        codes = ~rev_pairs(window32(seq, 2 * b));
-        nbits = __brev(window32(nmask, b)) >> 16;
-    }
-}
-
-template <int W>
-__device__ __forceinline__ void band_dp(const PeqRegs& peq, const uint32_t* seq,
-                                        const uint32_t* nmask, const TaskView& tv, bool front,
-                                        int ie, int je, int& cost, int& origin, int& score) {
-    constexpr int H = W / 2;
-    constexpr int INF = 1 << 20;
-    const int dx = je - ie;            // diagonal of the end cell; cell k <-> diagonal dx-H+k
-    const int n = (int)tv.len;
-    int C[W], O[W], S[W];
-#pragma unroll
-    for (int k = 0; k < W; ++k) {      // row 0: free start in the read
-        const int jj = dx - H + k;
-        C[k] = (jj >= 0 && jj <= n) ? 0 : INF;
-        O[k] = jj;
-        S[k] = 0;
-    }
-    uint32_t codes, nb;                // codes of row i: positions i + dx - H - 1 + k
-    fetch16s(seq, nmask, tv, dx - H, codes, nb);
-    for (int i = 1; i <= ie; ++i) {
-        uint32_t ncodes = 0, nnb = 0;  // prefetch next row's window
-        if (i < ie) fetch16s(seq, nmask, tv, i + dx - H, ncodes, nnb);
-        const uint32_t b = (uint32_t)(i - 1);
-        const uint32_t rmask = (uint32_t)((peq.p0 >> b) & 1ull) |
-                               ((uint32_t)((peq.p1 >> b) & 1ull) << 1) |
-                               ((uint32_t)((peq.p2 >> b) & 1ull) << 2) |
-                               ((uint32_t)((peq.p3 >> b) & 1ull) << 3);
-        int lc = INF, lo = 0, ls = 0;  // left neighbour (same row, already updated)
-        // in place, ascending k: C[k] is still the diagonal (row i-1), C[k+1] the cell above.
-        // Branch-free: the pointer rule becomes three selects.
-#pragma unroll
-        for (int k = 0; k < W; ++k) {
-            const int jj = i + dx - H + k;
-            const int uc = (k + 1 < W) ? C[(k + 1) % W] : INF;
-            const int uo = (k + 1 < W) ? O[(k + 1) % W] : 0;
-            const int us = (k + 1 < W) ? S[(k + 1) % W] : 0;
-            const uint32_t code = (codes >> (2 * k)) & 3u;
-            const bool eq = !((nb >> k) & 1u) && ((rmask >> code) & 1u);
-            const bool take_diag = eq || (C[k] <= lc && C[k] <= uc);   // match or mismatch
-            const bool take_up = uc <= lc;                              // insertion vs deletion
-            const int ic = take_up ? uc : lc;
-            const int io = take_up ? uo : lo;
-            const int is = take_up ? us : ls;
-            int c = take_diag ? C[k] + (eq ? 0 : 1) : ic + 1;
-            int o = take_diag ? O[k] : io;
-            int sc = take_diag ? S[k] + (eq ? 1 : -1) : is - 2;
-            const bool col0 = jj == 0;                 // column 0: cutadapt's initialisation
-            c = col0 ? (front ? 0 : i) : c;
-            o = col0 ? (front ? -i : 0) : o;
-            sc = col0 ? (front ? 0 : -2 * i) : sc;
-            c = (jj < 0 || jj > n) ? INF : min(c, INF);
-            C[k] = c;
-            O[k] = o;
-            S[k] = sc;
-            lc = c;
-            lo = o;
-            ls = sc;
-        }
-        codes = ncodes;
-        nb = nnb;
-    }
-    cost = C[H];
-    origin = O[H];
-    score = S[H];
-}
-
 // Banded DP, two state words per cell: C = cost and P = origin * 256 + V, V = vertical moves on
 // the chosen path.  The score follows from them at the end cell: with A adapter chars aligned,
 // score = matches - mismatches - 2 * indels = A - 2 * cost - V (A = ie, or ie - i0 for a FRONT
