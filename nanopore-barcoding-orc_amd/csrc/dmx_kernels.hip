@@ -236,6 +236,54 @@ struct CandSink {
     Stage<Cand, kCandStageCap> st[2];
 };
 
+// Per-wave staging: each wave appends to its own LDS slice and flushes it on its own (one
+// global atomic per flush, no block barrier), so waves of a block never wait for each other.
+template <class Rec, int CAP>
+struct WaveStage {
+    Rec* buf;              // LDS [CAP], this wave's slice
+    uint32_t* cnt;         // LDS, this wave's counter
+    Rec* g;
+    uint32_t* gcount;
+    uint32_t gcap;
+    uint32_t* flags;
+    uint32_t ovf;
+
+    __device__ __forceinline__ void push(const Rec& r) const {
+        const uint32_t i = atomicAdd(cnt, 1u);
+        if (i < (uint32_t)CAP) {
+            buf[i] = r;
+            return;
+        }
+        const uint32_t gi = atomicAdd(gcount, 1u);   // slice full: direct (rare)
+        if (gi < gcap) g[gi] = r;
+        else atomicOr(flags, ovf);
+    }
+    __device__ __forceinline__ uint32_t count() const { return *cnt; }
+    // Every lane of the wave calls this at a wave-uniform point.  LDS operations of one wave
+    // complete in issue order, so the slice written by the pushes above is visible here.
+    __device__ __forceinline__ void flush() const {
+        const uint32_t n = min(*cnt, (uint32_t)CAP);
+        if (n == 0) return;
+        const uint32_t lane = threadIdx.x & 63u;
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(gcount, n);
+        b = __builtin_amdgcn_readfirstlane(b);
+        for (uint32_t i = lane; i < n; i += 64) {
+            if (b + i < gcap) g[b + i] = buf[i];
+            else atomicOr(flags, ovf);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) *cnt = 0;
+        __builtin_amdgcn_wave_barrier();
+    }
+};
+
+constexpr int kWaveCandCap = 64;
+
+struct WaveCandSink {
+    WaveStage<Cand, kWaveCandCap> st[2];
+};
+
 __device__ __forceinline__ Cand make_cand(const TaskView& tv, uint32_t item, int sub, int iend,
                                           int cost, uint32_t j) {
     Cand c;
@@ -279,7 +327,8 @@ __device__ __forceinline__ void fetch16s(const uint32_t* __restrict__ seq,
     }
 }
 
-__device__ __forceinline__ void flush_cands(const CandSink& sink, const TaskView& tv, uint32_t item,
+template <class Sink>
+__device__ __forceinline__ void flush_cands(const Sink& sink, const TaskView& tv, uint32_t item,
                                          int sub, int m, int lbk, uint32_t seg, uint64_t cm,
                                          uint64_t c0, uint64_t c1, uint64_t c2) {
     while (cm) {
@@ -295,8 +344,8 @@ __device__ __forceinline__ void flush_cands(const CandSink& sink, const TaskView
     }
 }
 
-template <int HB>
-__device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const CandSink& sink,
+template <int HB, class Sink>
+__device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink& sink,
                                                  const TaskView& tv, uint32_t item, int sub,
                                                  const uint64_t* peq, int A, const DevAdapter& ad,
                                                  const int8_t* acc, const int8_t* pacc,
@@ -316,16 +365,20 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const CandS
 
 #define DMX_CAND_STEP(q)                                                                  \
     {                                                                                     \
-        const uint32_t code = ((codes >> (2 * (q))) & 3u) | (((nb >> (q)) & 1u) << 2);    \
-        myers_step<HB>(peq[code * kMaxAdapters], pv, mv, d, hbit);                                       \
+        myers_step<HB>(eqv[q], pv, mv, d, hbit);                                          \
         if (d <= kk) {                                                                    \
             const uint32_t j = p0 + (q) + 1;                                              \
-            const int lr = min(m, (int)j + d);                                            \
-            if (j >= jlo && d <= (int)pacc[lr]) {                                         \
-                {   /* certainly accepted: aligned length >= L0 and acc is monotone */       \
-                    const int L0 = min(m, (int)j - d);                                    \
-                    if (L0 >= 0 && d <= (int)acc[L0]) lbk = max(lbk, lb_key(L0 - 3 * d, d)); \
-                }                                                                         \
+            bool ok = j >= jlo;                                                           \
+            int L0 = m;                                                                   \
+            if (ok && (int)j < m + kk) {   /* near column 0: the acceptance tables */      \
+                ok = d <= (int)pacc[min(m, (int)j + d)];                                  \
+                L0 = min(m, (int)j - d);                                                  \
+                if (ok && !(L0 >= 0 && d <= (int)acc[L0])) L0 = -1;                       \
+            }                                                                             \
+            if (ok) {                                                                     \
+                /* certainly accepted: aligned length >= L0 and acc is monotone (far from \
+                   column 0, L0 = m and acc[m] = k >= d) */                               \
+                if (L0 >= 0) lbk = max(lbk, lb_key(L0 - 3 * d, d));                       \
                 if (!segset) {                                                            \
                     segset = true;                                                        \
                     seg = j;                                                              \
@@ -338,6 +391,10 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const CandS
             }                                                                             \
         }                                                                                 \
     }
+#define DMX_CAND_EQ                                                                       \
+    uint64_t eqv[16];                                                                     \
+    _Pragma("unroll") for (int q = 0; q < 16; ++q)                                        \
+        eqv[q] = peq[(((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)) * kMaxAdapters];
 
     uint32_t p0 = js;
     uint32_t ncodes, nnb;             // next chunk, prefetched one chunk ahead
@@ -351,6 +408,7 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const CandS
             segset = false;
             cm = c0 = c1 = c2 = 0;
         }
+        DMX_CAND_EQ
 #pragma unroll
         for (int q = 0; q < 16; ++q) DMX_CAND_STEP(q)
     }
@@ -361,10 +419,14 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const CandS
             segset = false;
             cm = c0 = c1 = c2 = 0;
         }
+        DMX_CAND_EQ
         const int cnt = (int)(jhi - p0);
-        for (int q = 0; q < cnt; ++q) DMX_CAND_STEP(q)
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (q < cnt) DMX_CAND_STEP(q)
     }
 #undef DMX_CAND_STEP
+#undef DMX_CAND_EQ
     // 3' adapters: last-column cells (adapter prefix aligned at the read end)
     uint64_t rows = 0;
     const uint32_t len = tv.len;
@@ -393,16 +455,17 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const CandS
 
 // The last adapter row's bit sits in the low or the high word of the 64-bit vectors; both
 // variants are compiled so the step needs no per-column select.
-__device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const CandSink& sink,
+template <class Sink>
+__device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const Sink& sink,
                                               const TaskView& tv, uint32_t item, int sub,
                                               const uint64_t* peq, int A, const DevAdapter& ad,
                                               const int8_t* acc, const int8_t* pacc,
                                               uint32_t js, bool real, uint32_t jlo,
                                               uint32_t jhi, bool lastcol) {
     if (ad.m > 32)
-        return scan_task_cand_hb<1>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real, jlo,
+        return scan_task_cand_hb<1, Sink>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real, jlo,
                                     jhi, lastcol);
-    return scan_task_cand_hb<0>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real, jlo, jhi,
+    return scan_task_cand_hb<0, Sink>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real, jlo, jhi,
                                 lastcol);
 }
 
@@ -1096,7 +1159,20 @@ __global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kMaxAdapters];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
     __shared__ int8_t s_pacc[72 * kMaxAdapters];
-    DMX_STAGES
+    __shared__ Cluster s_cl[BAND ? 1 : kStageCap];
+    __shared__ uint32_t s_clcnt, s_clbase;
+    __shared__ Cand s_wcand[BAND ? kScanBlock / 64 : 1][2][kWaveCandCap];
+    __shared__ uint32_t s_wcn[kScanBlock / 64][2];
+    if (threadIdx.x == 0) s_clcnt = 0;
+    if (threadIdx.x < 2 * (kScanBlock / 64)) (&s_wcn[0][0])[threadIdx.x] = 0;
+    const Stage<Cluster> st{s_cl, &s_clcnt, &s_clbase, R.cl, R.cl_count, R.cl_cap, R.flags, 1u};
+    const uint32_t wv = BAND ? threadIdx.x >> 6 : 0u;
+    const WaveCandSink sink{{WaveStage<Cand, kWaveCandCap>{s_wcand[wv][0], &s_wcn[wv][0],
+                                                           R.cand[0], R.cand_count, R.cand_cap,
+                                                           R.flags, 8u},
+                             WaveStage<Cand, kWaveCandCap>{s_wcand[wv][1], &s_wcn[wv][1],
+                                                           R.cand[1], R.cand_count + 1,
+                                                           R.cand_cap, R.flags, 8u}}};
     load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
     __syncthreads();
 
@@ -1146,17 +1222,17 @@ __global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
                                s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2, w.lastcol != 0);
             if (lb > 0) atomicMax(&R.lb[slot_of(R, w.item, sub)], lb);
         }
-        __syncthreads();                             // make the staged counts block-uniform
-        if constexpr (BAND) {
-            if (s_ccnt[0] > kCandStageCap / 2 || s_ccnt[1] > kCandStageCap / 2) {
-                sink.st[0].flush();
-                sink.st[1].flush();
-            }
+        if constexpr (BAND) {                        // wave-uniform: no block barrier
+            __builtin_amdgcn_wave_barrier();
+            if (sink.st[0].count() > kWaveCandCap / 2) sink.st[0].flush();
+            if (sink.st[1].count() > kWaveCandCap / 2) sink.st[1].flush();
         } else {
+            __syncthreads();                         // make the staged counts block-uniform
             if (s_clcnt > kStageCap / 2) st.flush();
         }
     }
     if constexpr (BAND) {
+        __builtin_amdgcn_wave_barrier();
         sink.st[0].flush();
         sink.st[1].flush();
     } else {
