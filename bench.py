@@ -29,6 +29,8 @@ sys.path.insert(0, os.path.join(ROOT, "nanopore-barcoding-orc_amd"))
 METRIC = "Mreads/s two-round SP5×SP27 demux; % HBM roofline; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CUs x 4 SIMD32 x 2.4 GHz, 32-bit lane-ops
+VALU_CEILING = 48.5e12       # measured: v_bitop3 chains, full occupancy (tools/microbench)
+FILTER_OPS_PER_COLUMN = 30.7  # PMC: SQ_INSTS_VALU x 64 / filter columns (profiles/r1_pmc_*)
 
 
 def filter_algorithmic_bytes(lengths: np.ndarray, n_windows: int) -> float:
@@ -191,6 +193,7 @@ def main():
     traffic, traffic_src = pmc_traffic(args.workload, args.reads)
     A0, A1 = ctx.panel_sizes
     cols = float(lengths.sum()) * 2 + float(len2.sum()) * 2     # filter columns, both strands
+    col_rate = cols / ((stage["filter0"] + stage["filter1"]) / K / 1e3)
 
     out = {
         "metric": METRIC, "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
@@ -209,9 +212,15 @@ def main():
                      "kernel": "dmx::filter_kernel", "avg_launch_ms": round(filt_ms, 3),
                      "note": "the bit-vector filter is VALU-bound by construction "
                              "(DESIGN.md §5): see 'valu' for its issue-rate fraction"},
-        "valu": {"filter_columns_per_s": cols / ((stage["filter0"] + stage["filter1"]) / K / 1e3),
-                 "filter_lane_ops_per_column": 20,
-                 "peak_lane_ops_per_s": VALU_PEAK_TOPS * 1e12},
+        "valu": {"filter_columns_per_s": col_rate,
+                 "filter_lane_ops_per_column": FILTER_OPS_PER_COLUMN,
+                 "filter_lane_ops_per_s": col_rate * FILTER_OPS_PER_COLUMN,
+                 "frac_of_measured_ceiling": col_rate * FILTER_OPS_PER_COLUMN / VALU_CEILING,
+                 "measured_ceiling_lane_ops_per_s": VALU_CEILING,
+                 "nominal_peak_lane_ops_per_s": VALU_PEAK_TOPS * 1e12,
+                 "source": "ops/column = SQ_INSTS_VALU x 64 / columns of the filter launch "
+                           "(profiles/r1_pmc_summary_c2x24_2M.txt); ceiling = independent "
+                           "v_bitop3 chains at full occupancy (tools/microbench/myers_ilp.hip)"},
         "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
         "clusters_per_step": (clusters / K).tolist(),
         "filter_windows_per_step": (windows / K).tolist(),

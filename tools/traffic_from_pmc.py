@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the filter kernel from rocprofv3 PMC passes (FETCH_SIZE and
+WRITE_SIZE collected in separate runs of `bench.py --steps 1 --warmup 0`).
+
+Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced read, so it
+is doubled (the filter's loads are 16-B and 8-B per lane); WRITE_SIZE is taken as reported.
+usage: traffic_from_pmc.py FETCH_DIR WRITE_DIR WORKLOAD READS OUT_JSON
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def per_dispatch(d, counter):
+    acc = collections.OrderedDict()
+    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+        if r["Counter_Name"] != counter or "filter_kernel" not in r["Kernel_Name"]:
+            continue
+        acc[int(r["Dispatch_Id"])] = acc.get(int(r["Dispatch_Id"]), 0.0) + float(
+            r["Counter_Value"])
+    return list(acc.values())
+
+
+def main():
+    fdir, wdir, workload, reads, out = sys.argv[1:6]
+    fetch = per_dispatch(fdir, "FETCH_SIZE")
+    write = per_dispatch(wdir, "WRITE_SIZE")
+    n = min(len(fetch), len(write))
+    per_launch = [2.0 * fetch[i] * 1024 + write[i] * 1024 for i in range(n)]
+    data = {}
+    if os.path.exists(out):
+        data = json.load(open(out))
+    data[f"{workload}:{reads}"] = {
+        "bytes_per_launch": sum(per_launch) / n,
+        "launches": [{"fetch_kib_raw": fetch[i], "write_kib": write[i],
+                      "bytes": per_launch[i]} for i in range(n)],
+        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), filter_kernel, "
+                  "FETCH_SIZE x2 (gfx950 wide-read correction), averaged over the round-1 and "
+                  "round-2 launches of one step",
+    }
+    with open(out, "w") as fh:
+        json.dump(data, fh, indent=1)
+        fh.write("\n")
+    print(json.dumps(data[f"{workload}:{reads}"]))
+
+
+if __name__ == "__main__":
+    main()
