@@ -222,8 +222,8 @@ int dmx_open(int device, dmx_ctx** out) {
     c->no_verify = nv && nv[0] == '1';
     const char* rs = std::getenv("DMX_RESOLVE");
     c->force_ring = rs && std::strcmp(rs, "ring") == 0;
-    const char* ns = std::getenv("DMX_SIEVE");   // experimental window sieve (default off)
-    c->no_sieve = !(ns && ns[0] == '1');
+    const char* ns = std::getenv("DMX_SCREEN");   // index screen before the window scan
+    c->no_sieve = !(ns && ns[0] == '1');          // (experimental, off by default)
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -418,7 +418,7 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
         }
         dp.kf = kf;
         dp.max_mk = mk;
-        hp.sieve = mk + 16 + 15 <= 112;   // window sieve: >= 16 candidate columns per piece
+
         // shared prefix for the verification pass
         int pre = lens[0];
         int mmin = 1 << 30, mmax = 0;
@@ -436,6 +436,14 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
             dp.off_min = mmin - pre;
             dp.off_max = mmax - pre;
             dp.m_max = mmax;
+            // index screen: every adapter's middle block I_a = rows [pre, m - flen) fits a
+            // 32-bit word, and a piece keeps >= 16 candidate columns
+            int lmin = 64, lmx = 0;
+            for (int a = 0; a < n; ++a) {
+                lmin = std::min(lmin, lens[a] - pre - flen);
+                lmx = std::max(lmx, lens[a] - pre - flen);
+            }
+            hp.sieve = lmin >= 1 && lmx <= 32 && 128 - 15 - 4 * kf - lmx - pre - flen - 1 >= 16;
             for (int i = 0; i < pre; ++i) {
                 const uint8_t mask = iupac_mask(seqs[0][i]);
                 for (int code = 0; code < 4; ++code)
@@ -626,10 +634,10 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
     CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
     if (getenv("DMX_DEBUG_STATS"))
         fprintf(stderr,
-                "dmx stats: windows raw %u %u verified %u %u sieve pieces %u %u pairs %u %u cand %u %u "
-                "%u %u\n",
-                cnt[4], cnt[5], cnt[10], cnt[11], cnt[18], cnt[22], cnt[12], cnt[13], cnt[6],
-                cnt[7], cnt[8], cnt[9]);
+                "dmx stats: windows raw %u %u verified %u %u screen pieces %u %u (all-pass %u %u) "
+                "pairs %u %u cand %u %u %u %u\n",
+                cnt[4], cnt[5], cnt[10], cnt[11], cnt[18], cnt[22], cnt[19], cnt[23], cnt[12],
+                cnt[13], cnt[6], cnt[7], cnt[8], cnt[9]);
     if (counts) {
         const bool b0 = c->band_ok[0] && !c->force_ring, b1 = c->band_ok[1] && !c->force_ring;
         const uint64_t v[10] = {cnt[0],

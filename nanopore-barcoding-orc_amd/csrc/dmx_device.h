@@ -86,15 +86,15 @@ struct Window {
 };
 static_assert(sizeof(Window) == 40, "Window layout");
 
-// A (window, adapter) pair that survived the window sieve, with the candidate column range
-// [jlo, jhi] (a piece of the window's [j1, j2]); the window scan runs only these.
+// A window piece with the candidate column range [jlo, jhi] (a piece of the window's [j1, j2])
+// and the adapters that survived the index screen (bit a); the window scan runs only those.
 struct Pair {
     uint32_t win;
     uint32_t jlo, jhi;
-    uint16_t a;
-    uint16_t pad;
+    uint32_t pad;
+    uint64_t mask;
 };
-static_assert(sizeof(Pair) == 16, "Pair layout");
+static_assert(sizeof(Pair) == 24, "Pair layout");
 
 constexpr int kStageCap = 256;    // LDS staging of emitted records per block
 constexpr int kCandStageCap = 128; // per candidate list

@@ -11,7 +11,7 @@
 namespace dmx {
 
 struct HostPanel {
-    bool sieve = false;       // window sieve usable (band mode, max_mk small enough)
+    bool sieve = false;       // index screen usable (filter + verify, index blocks <= 32)
     int n = 0;
     int n_orient = 1;
     bool set = false;
@@ -66,7 +66,7 @@ struct Ctx {
     unsigned long long* d_linked = nullptr;
     Pair* d_pairs = nullptr;             // window sieve survivors
     size_t pair_cap = 0;
-    bool no_sieve = true;                // window sieve off unless DMX_SIEVE=1   // linked mode: best pair key per read
+    bool no_sieve = true;                // index screen on only with DMX_SCREEN=1   // linked mode: best pair key per read
     size_t n_counts = 0;
     hipEvent_t ev[13] = {};   // [3r..3r+2] round r stages, [6+r] finalize, [8] start,
                               // [9+2r] after filter, [10+2r] after verify

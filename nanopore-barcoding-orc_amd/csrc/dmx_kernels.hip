@@ -979,50 +979,61 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
 // Window scan: one lane per (window, adapter); block-uniform grid-stride over the device-side
 // window count so that the block can flush its staged records between strides.
 // ---------------------------------------------------------------------------------------------
-// window sieve: one lane per window, adapters in a block-uniform loop (their parameters are
-// scalar, their match vectors an LDS broadcast).  Each adapter's 64-bit Myers runs over the
-// window's columns with branch-free steps; a (window piece, adapter) pair survives when some
-// candidate column j in [jlo, jhi] has cost d <= thr(j) = the largest d <= kk with
-// d <= pacc[min(m, j + d)] (a superset of the window scan's candidate test), or, for a 3'
-// window at the view end, when some last-column row is accepted.  Only survivors reach the
-// window scan, which then decides every cell exactly.  A window longer than kSieveSpan columns
-// is cut into pieces [jlo, jhi] of at most sieve_cr candidate columns.
+// index screen (before the window scan).  Every adapter of a filtered + verified panel is
+// P + I_a + S: the shared prefix P (pre_len rows), its own index block I_a (l_a <= 32 rows) and
+// the shared suffix S (filter_len rows).  A candidate cell of adapter a at column j in [jlo, jhi]
+// with cost d <= kk_a restricts to an alignment of I_a ending at a column x2 in
+// [j - s - kf, j - s + kf] (S spans s +- c_S read characters, c_S <= d <= kf) with cost
+// <= d - c_S <= kk_a - bmin (c_S >= b(j) >= the window's bmin).  So a 32-bit Myers of I_a alone
+// (free start in the read; FRONT windows at the view start with the zero column, which also
+// covers alignments that skip into or past I_a) over [x_lo, x_hi] = [jlo - s - kf, jhi - s + kf]
+// must reach cost <= kk_a - bmin somewhere, or adapter a has no candidate in the piece.
+// 3' windows at the view end (last-column cells (i, len), S or I_a cut by the read end) use
+// threshold kk_a, test the index block's last column rows too, and let every adapter through
+// when a prefix-only cell (i <= pre_len, identical for all adapters) may be accepted.
+// Survivors (window piece, adapter) go to the window scan, which decides every cell exactly.
+// One lane per window piece; adapters in a block-uniform loop (LDS broadcast of the index
+// vectors); the piece's read codes sit in a lane-private LDS column.
 // ---------------------------------------------------------------------------------------------
-constexpr int kSieveChunks = 7;
+constexpr int kSieveChunks = 8;
 constexpr int kSieveSpan = 16 * kSieveChunks;     // view positions held per lane
 
 __global__ __launch_bounds__(kScanBlock) void sieve_kernel(RoundArgs R) {
-    __shared__ uint64_t s_peq[8 * kMaxAdapters];
-    __shared__ __attribute__((aligned(16))) int8_t s_thr[kMaxAdapters * 128];
+    __shared__ uint32_t s_ipeq[kMaxAdapters * 8];  // index block I_a: bit r = row p + r
     __shared__ Pair s_pair[kStageCap];
     __shared__ uint32_t s_pc, s_pb;
     __shared__ uint2 s_code[kSieveChunks][kScanBlock];
-    __shared__ int s_m[kMaxAdapters];
+    __shared__ int s_l[kMaxAdapters], s_kk[kMaxAdapters];
+    __shared__ int8_t s_acc0[72];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
+    __shared__ uint32_t s_ppeq[8];
     __shared__ uint32_t s_pfx[kScanBlock];
     const DevPanel* P = R.panel;
     const int A = P->n_adapters;
-    for (int x = threadIdx.x; x < 8 * A; x += blockDim.x)
-        s_peq[(x / A) * kMaxAdapters + x % A] = P->ad[x % A].peq[x / A];
-    for (int x = threadIdx.x; x < A; x += blockDim.x) s_m[x] = P->ad[x].m;
-    for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
-    for (int x = threadIdx.x; x < 128 * A; x += blockDim.x) {
-        const DevAdapter& ad = P->ad[x >> 7];
-        const int j = (x & 127) + 1;                   // column after view position x & 127
-        int t = -1;
-        for (int d = 0; d <= ad.kk; ++d)
-            if (d <= (int)ad.pacc[min((int)ad.m, j + d)]) t = d;
-        s_thr[x] = (int8_t)t;
+    const int pl = P->pre_len, sl = P->filter_len, kf = P->kf;
+    for (int x = threadIdx.x; x < 8 * A; x += blockDim.x) {
+        const int a = x >> 3, c = x & 7;
+        const int l = (int)P->ad[a].m - pl - sl;
+        const uint64_t v = c < 4 ? (P->ad[a].peq[c] >> pl) : 0ull;
+        s_ipeq[x] = (uint32_t)(l >= 32 ? v : (v & ((1ull << l) - 1ull)));
     }
+    int lmax = 0;
+    for (int a = 0; a < A; ++a) lmax = max(lmax, (int)P->ad[a].m - pl - sl);
+    for (int x = threadIdx.x; x < A; x += blockDim.x) {
+        s_l[x] = (int)P->ad[x].m - pl - sl;
+        s_kk[x] = P->ad[x].kk;
+    }
+    if (threadIdx.x < 72) s_acc0[threadIdx.x] = P->ad[0].acc[threadIdx.x];
+    for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
+    if (threadIdx.x < 8) s_ppeq[threadIdx.x] = P->pre_peq[threadIdx.x];
     if (threadIdx.x == 0) s_pc = 0;
     __syncthreads();
     const Stage<Pair> st{s_pair, &s_pc, &s_pb, R.pairs, R.pair_count, R.pair_cap, R.flags, 4u};
-    const Window* wl = P->pre_len ? R.win2 : R.win;
-    const uint32_t* wc = P->pre_len ? R.win2_count : R.win_count;
-    const uint32_t total = min(*wc, R.win_cap);
+    const Window* wl = R.win2;                        // screen runs only with verification
+    const uint32_t total = min(*R.win2_count, R.win_cap);
     const bool front = P->where == kFront;
-    const int max_mk = P->max_mk;
-    const int cr = kSieveSpan - 15 - max_mk;           // candidate columns per piece (host: >= 16)
+    // candidate columns per piece: x_hi - xs + 15 <= kSieveSpan (host checks cr >= 16)
+    const int cr = kSieveSpan - 15 - 4 * kf - lmax - pl - sl - 1;
 
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
         // pieces of this block's windows, flattened so every lane takes one piece per round
@@ -1044,114 +1055,194 @@ __global__ __launch_bounds__(kScanBlock) void sieve_kernel(RoundArgs R) {
         }
         const uint32_t npieces = s_pfx[kScanBlock - 1];
         for (uint32_t pb = 0; pb < npieces; pb += kScanBlock) {
-        const uint32_t pi = pb + threadIdx.x;
-        const bool act = pi < npieces;
-        Window w;
-        uint32_t wi = 0, jlo = 1, jhi = 0;
-        if (act) {
-            uint32_t lo = 0, hi = kScanBlock - 1;      // first lane with inclusive prefix > pi
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_pfx[mid] > pi) hi = mid;
-                else lo = mid + 1;
-            }
-            const uint32_t before = lo ? s_pfx[lo - 1] : 0u;
-            wi = base + lo;
-            w = wl[wi];
-            jlo = w.j1 + (pi - before) * (uint32_t)cr;
-            jhi = min(w.j2, jlo + (uint32_t)cr - 1);
-        } else {
-            w.j1 = 1;
-            w.j2 = 0;
-            w.lastcol = 0;
-            w.len = 0;
-        }
-        {
-            const int s0 = max(0, (int)jlo - max_mk);
-            const bool lastc = !front && w.lastcol && jhi == w.j2;
-            // chunk grid: 16-aligned from `start`; a 3' window at the view end is aligned to end
-            // exactly at jhi (its last-column state is then the state after the chunk loop)
-            uint32_t start = s0 <= 0 ? 0u : ((uint32_t)s0 & ~15u);
-            int nch = (int)((jhi - start + 15) / 16);
-            bool fallback = false;
-            if (lastc) {
-                const int n2 = (int)((jhi - (uint32_t)s0 + 15) / 16);
-                const int st2 = (int)jhi - 16 * n2;
-                if (st2 >= 64) {                       // thresholds are kk that far from 0
-                    start = (uint32_t)st2;
-                    nch = n2;
-                } else {
-                    fallback = true;                   // short view: the window scan decides
+            const uint32_t pi = pb + threadIdx.x;
+            const bool act = pi < npieces;
+            Window w;
+            uint32_t wi = 0, jlo = 1, jhi = 0;
+            if (act) {
+                uint32_t lo = 0, hi = kScanBlock - 1;  // first lane with inclusive prefix > pi
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_pfx[mid] > pi) hi = mid;
+                    else lo = mid + 1;
                 }
+                const uint32_t before = lo ? s_pfx[lo - 1] : 0u;
+                wi = base + lo;
+                w = wl[wi];
+                jlo = w.j1 + (pi - before) * (uint32_t)cr;
+                jhi = min(w.j2, jlo + (uint32_t)cr - 1);
+            } else {
+                w.j1 = 1;
+                w.j2 = 0;
+                w.lastcol = 0;
+                w.len = 0;
+                w.bmin = 255;
             }
-            if (!act) nch = 0;
-            const bool real = start == 0;
-            // the piece's codes stay in a lane-private LDS column for all adapters
+            const int len = (int)w.len;
+            const bool lastc = act && !front && w.lastcol && jhi == w.j2;
+            const int bm = w.bmin == 255 ? 0 : (int)w.bmin;
+            bool all = false;
+            // FRONT columns j <= s + kf may hold S-only partial alignments (P and I_a skipped at
+            // column 0): identical for every adapter, so every adapter keeps that sub-range
+            if (act && front && (int)jlo <= sl + kf) {
+                const uint32_t jh = min(jhi, (uint32_t)(sl + kf));
+                Pair pr;
+                pr.win = wi;
+                pr.jlo = jlo;
+                pr.jhi = jh;
+                pr.pad = 0;
+                pr.mask = A >= 64 ? ~0ull : ((1ull << A) - 1ull);
+                st.push(pr);
+                jlo = jh + 1;
+            }
+            const bool act2 = act && jlo <= jhi;
+            const int x_lo = (int)jlo - sl - kf;               // index end columns
+            const int x_hi = lastc ? len : min(len, (int)jhi - sl + kf);
+            const int xp_lo = x_lo - lmax - kf;                // P end columns from here
+            const int xs = max(0, xp_lo - pl - kf - 1);        // restricted start (or column 0)
+            const bool zero = front && xs == 0;                // FRONT view start: zero column
+            const int nch = (act2 && x_hi > xs) ? (x_hi - xs + 15) / 16 : 0;
+            const int start = x_hi - 16 * nch;                 // chunk grid ends exactly at x_hi
             for (int c = 0; c < nch; ++c) {
                 uint32_t cc, nn;
-                fetch16(R.seq, R.nmask, w.off, w.n, w.strand, w.start, start + 16u * c, cc, nn);
+                TaskView tv;
+                tv.n = w.n;
+                tv.strand = w.strand;
+                tv.start = w.start;
+                tv.len = w.len;
+                tv.off = w.off;
+                fetch16s(R.seq, R.nmask, tv, start + 16 * c, cc, nn);
                 s_code[c][threadIdx.x] = make_uint2(cc, nn);
             }
-            for (int a = 0; a < A; ++a) {
-                const int m = __builtin_amdgcn_readfirstlane(s_m[a]);   // LDS: no byte loads
-                const uint32_t hbit = (uint32_t)(m - 1);
-                const bool zero = real && front;
-                uint64_t pv = zero ? 0ull : ~0ull, mv = 0ull;
-                int d = zero ? 0 : m;
-                bool surv = fallback;
-                const int8_t* thr_row = s_thr + 128 * a;
+            // shared prefix P: cP = min D_P(pl, x) over x in [xp_lo, x_hi] bounds the P part of
+            // every alignment in the piece; with 3' last-column cells also the rows at len
+            int cP = 1 << 20, cPe = 1 << 20;   // cPe: P ending within lmax + kf of len
+            {
+                const uint32_t neutral = zero ? ~0u : 0u;
+                uint32_t pv = zero ? 0u : ~0u, mv = 0u;
+                int d = zero ? 0 : pl;
+                if (zero && xp_lo <= 0) cP = 0;                // column 0 of the zero column
+                const int xe_lo = len - lmax - kf;
                 for (int c = 0; c < nch; ++c) {
-                    {
-                        const uint32_t p0 = start + 16u * (uint32_t)c;
-                        const uint2 cn = s_code[c][threadIdx.x];
-                        const uint32_t codes = cn.x, nb = cn.y;
-                        // thresholds: the table below column 64 (16-aligned there), kk beyond
-                        const uint4 tw =
-                            *reinterpret_cast<const uint4*>(thr_row + (p0 < 64u ? p0 : 112u));
-                        uint32_t hits = 0;
+                    const int p0 = start + 16 * c;
+                    const uint2 cn = s_code[c][threadIdx.x];
+                    uint32_t e[16];
 #pragma unroll
-                        for (int q = 0; q < 16; ++q) {
-                            const uint32_t code =
-                                ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
-                            myers_step(s_peq[code * kMaxAdapters + a], pv, mv, d, hbit);
-                            const uint32_t wd = q < 4 ? tw.x : q < 8 ? tw.y : q < 12 ? tw.z : tw.w;
-                            const int t = __builtin_amdgcn_sbfe((int)wd, 8 * (q & 3), 8);
-                            hits |= d <= t ? (1u << q) : 0u;
-                        }
-                        // candidate columns j = p0 + q + 1 in [jlo, jhi]
-                        const int lo = (int)jlo - (int)p0 - 1, hi = (int)jhi - (int)p0 - 1;
-                        const uint32_t mlo = lo <= 0 ? 0xFFFFu : (lo >= 16 ? 0u : (0xFFFFu << lo));
-                        const uint32_t mhi =
-                            hi >= 15 ? 0xFFFFu : (hi < 0 ? 0u : (0xFFFFu >> (15 - hi)));
-                        surv |= (hits & mlo & mhi & 0xFFFFu) != 0u;
+                    for (int q = 0; q < 16; ++q) {
+                        e[q] = s_ppeq[((cn.x >> (2 * q)) & 3u) | (((cn.y >> q) & 1u) << 2)];
+                        if (p0 + q < xs) e[q] = neutral;
                     }
+                    int mr = 1 << 20, me = 1 << 20;
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        myers_step32(e[q], pv, mv, d, (uint32_t)(pl - 1));
+                        const int x = p0 + q + 1;
+                        mr = min(mr, x >= xp_lo ? d : (1 << 20));
+                        me = min(me, x >= xe_lo ? d : (1 << 20));
+                    }
+                    cP = min(cP, mr);
+                    cPe = min(cPe, me);
                 }
-                if (lastc && !surv) {
-                    // last-column rows i < m at column len: cost D(i, len) <= acc[i]
+                if (lastc && nch) {                    // prefix-only cells (i <= pl, at len)
                     int dd = 0;
-                    for (int i = 1; i < m; ++i) {
-                        dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
-                        surv |= dd <= (int)s_acc[72 * a + i];
+                    for (int i = 1; i <= pl; ++i) {
+                        dd += (int)((pv >> (i - 1)) & 1u) - (int)((mv >> (i - 1)) & 1u);
+                        all |= dd <= (int)s_acc0[i];
                     }
-                }
-                if (act && surv) {
-                    Pair pr;
-                    pr.win = wi;
-                    pr.jlo = jlo;
-                    pr.jhi = jhi;
-                    pr.a = (uint16_t)a;
-                    pr.pad = 0;
-                    st.push(pr);
                 }
             }
-        }
-        const int np = __syncthreads_count(act);       // also orders the staged count
-        if (threadIdx.x == 0) atomicAdd(&R.diag[2], (uint32_t)np);   // pieces (diagnostic)
-        if (s_pc > kStageCap / 2) st.flush();
+            uint64_t smask = 0;
+            for (int a = 0; a < A; ++a) {
+                const int l = s_l[a];
+                const uint32_t hbit = (uint32_t)(l - 1);
+                const int thr = (lastc ? s_kk[a] : s_kk[a] - bm) - cP;
+                const uint32_t* ip = s_ipeq + 8 * a;
+                const uint32_t neutral = zero ? ~0u : 0u;      // keeps the initial column
+                uint32_t pv = zero ? 0u : ~0u, mv = 0u;
+                int d = zero ? 0 : l;
+                bool surv = all || (zero && x_lo <= 0 && thr >= 0);
+                for (int c = 0; c < nch; ++c) {
+                    const int p0 = start + 16 * c;
+                    const uint2 cn = s_code[c][threadIdx.x];
+                    uint32_t eq[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        eq[q] = ip[((cn.x >> (2 * q)) & 3u) | (((cn.y >> q) & 1u) << 2)];
+                        if (p0 + q < xs) eq[q] = neutral;
+                    }
+                    uint32_t hits = 0;
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        myers_step32(eq[q], pv, mv, d, hbit);
+                        hits |= d <= thr ? (1u << q) : 0u;
+                    }
+                    // index end columns x = p0 + q + 1 in [x_lo, x_hi]
+                    const int lo = x_lo - p0 - 1, hi = x_hi - p0 - 1;
+                    const uint32_t mlo = lo <= 0 ? 0xFFFFu : (lo >= 16 ? 0u : (0xFFFFu << lo));
+                    const uint32_t mhi =
+                        hi >= 15 ? 0xFFFFu : (hi < 0 ? 0u : (0xFFFFu >> (15 - hi)));
+                    surv |= (hits & mlo & mhi & 0xFFFFu) != 0u;
+                }
+                if (lastc && !surv && nch) {           // cells (pl + r, len): P + part of I_a
+                    int dd = 0;
+                    for (int r = 1; r < l; ++r) {
+                        dd += (int)((pv >> (r - 1)) & 1u) - (int)((mv >> (r - 1)) & 1u);
+                        surv |= cPe + dd <= (int)s_acc[a * 72 + pl + r];
+                    }
+                }
+                if (surv) smask |= 1ull << a;
+            }
+            if (act2 && smask) {
+                Pair pr;
+                pr.win = wi;
+                pr.jlo = jlo;
+                pr.jhi = jhi;
+                pr.pad = 0;
+                pr.mask = smask;
+                st.push(pr);
+            }
+            const int np = __syncthreads_count(act);   // also orders the staged count
+            const int na = __syncthreads_count(all);
+            if (threadIdx.x == 0) {
+                atomicAdd(&R.diag[2], (uint32_t)np);   // pieces (diagnostic)
+                atomicAdd(&R.diag[3], (uint32_t)na);   // pieces passing every adapter
+            }
+            if (s_pc > kStageCap / 2) st.flush();
         }
         __syncthreads();                               // s_pfx is rewritten next
     }
     st.flush();
+}
+
+// One (window or piece, adapter) task of the window scan.
+template <bool BAND, class ClStage, class Sink>
+__device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, int a, int A,
+                                           const uint64_t* s_peq, const int8_t* s_acc,
+                                           const int8_t* s_pacc, const ClStage& st,
+                                           const Sink& sink) {
+    const int sub = w.o * A + a;
+    TaskView tv;
+    tv.read = 0;
+    tv.n = w.n;
+    tv.strand = w.strand;
+    tv.start = w.start;
+    tv.len = w.len;
+    tv.off = w.off;
+    tv.o = w.o;
+    tv.a = a;
+    const DevAdapter& ad = R.panel->ad[a];
+    int js = (int)w.j1 - (int)ad.m - (int)ad.k - 1;
+    const bool real = js <= 0;
+    if (real) js = 0;
+    int lb;
+    if constexpr (BAND)
+        lb = scan_task_cand(R, sink, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
+                            s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2,
+                            w.lastcol != 0);
+    else
+        lb = scan_task(R, st, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
+                       s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2, w.lastcol != 0);
+    if (lb > 0) atomicMax(&R.lb[slot_of(R, w.item, sub)], lb);
 }
 
 template <bool BAND>
@@ -1179,48 +1270,70 @@ __global__ __launch_bounds__(kScanBlock) void wscan_kernel(RoundArgs R) {
     const int A = R.panel->n_adapters;
     const Window* wl = R.panel->pre_len ? R.win2 : R.win;
     const uint32_t* wc = R.panel->pre_len ? R.win2_count : R.win_count;
-    const uint64_t total = R.sieve ? (uint64_t)min(*R.pair_count, R.pair_cap)
-                                   : (uint64_t)min(*wc, R.win_cap) * (uint64_t)A;
+    if (R.sieve) {
+        // screened pieces: block-wise flattening of the survivor masks into (piece, adapter)
+        __shared__ uint32_t s_pre[kScanBlock];
+        const uint32_t np = min(*R.pair_count, R.pair_cap);
+        for (uint32_t base = blockIdx.x * blockDim.x; base < np; base += gridDim.x * blockDim.x) {
+            const uint32_t pi = base + threadIdx.x;
+            const uint64_t mk = pi < np ? R.pairs[pi].mask : 0ull;
+            s_pre[threadIdx.x] = (uint32_t)__popcll(mk);
+            __syncthreads();
+            for (uint32_t dlt = 1; dlt < kScanBlock; dlt <<= 1) {
+                const uint32_t x = threadIdx.x >= dlt ? s_pre[threadIdx.x - dlt] : 0u;
+                __syncthreads();
+                s_pre[threadIdx.x] += x;
+                __syncthreads();
+            }
+            const uint32_t ntask = s_pre[kScanBlock - 1];
+            for (uint32_t tb = 0; tb < ntask; tb += kScanBlock) {
+                const uint32_t ti = tb + threadIdx.x;
+                if (ti < ntask) {
+                    uint32_t lo = 0, hi = kScanBlock - 1;   // first record with prefix > ti
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_pre[mid] > ti) hi = mid;
+                        else lo = mid + 1;
+                    }
+                    const Pair pr = R.pairs[base + lo];
+                    uint32_t k = ti - (lo ? s_pre[lo - 1] : 0u);   // k-th set bit of the mask
+                    uint64_t mk2 = pr.mask;
+                    while (k--) mk2 &= mk2 - 1ull;
+                    const int a = __ffsll((unsigned long long)mk2) - 1;
+                    Window w = wl[pr.win];
+                    w.lastcol = (w.lastcol && pr.jhi == w.j2) ? 1 : 0;
+                    w.j1 = pr.jlo;
+                    w.j2 = pr.jhi;
+                    wscan_task<BAND>(R, w, a, A, s_peq, s_acc, s_pacc, st, sink);
+                }
+                if constexpr (BAND) {
+                    __builtin_amdgcn_wave_barrier();
+                    if (sink.st[0].count() > kWaveCandCap / 2) sink.st[0].flush();
+                    if (sink.st[1].count() > kWaveCandCap / 2) sink.st[1].flush();
+                } else {
+                    __syncthreads();
+                    if (s_clcnt > kStageCap / 2) st.flush();
+                }
+            }
+            __syncthreads();                           // s_pre is rewritten next
+        }
+        if constexpr (BAND) {
+            __builtin_amdgcn_wave_barrier();
+            sink.st[0].flush();
+            sink.st[1].flush();
+        } else {
+            st.flush();
+        }
+        return;
+    }
+    const uint64_t total = (uint64_t)min(*wc, R.win_cap) * (uint64_t)A;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < total;
          base += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t t = base + threadIdx.x;
         if (t < total) {
-            Window w;
-            int a;
-            if (R.sieve) {   // one surviving (window piece, adapter) pair
-                const Pair pr = R.pairs[t];
-                w = wl[pr.win];
-                a = pr.a;
-                w.lastcol = (w.lastcol && pr.jhi == w.j2) ? 1 : 0;
-                w.j1 = pr.jlo;
-                w.j2 = pr.jhi;
-            } else {
-                w = wl[t / A];
-                a = (int)(t % A);
-            }
-            const int sub = w.o * A + a;
-            TaskView tv;
-            tv.read = 0;
-            tv.n = w.n;
-            tv.strand = w.strand;
-            tv.start = w.start;
-            tv.len = w.len;
-            tv.off = w.off;
-            tv.o = w.o;
-            tv.a = a;
-            const DevAdapter& ad = R.panel->ad[a];
-            int js = (int)w.j1 - (int)ad.m - (int)ad.k - 1;
-            const bool real = js <= 0;
-            if (real) js = 0;
-            int lb;
-            if constexpr (BAND)
-                lb = scan_task_cand(R, sink, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
-                                    s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2,
-                                    w.lastcol != 0);
-            else
-                lb = scan_task(R, st, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
-                               s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2, w.lastcol != 0);
-            if (lb > 0) atomicMax(&R.lb[slot_of(R, w.item, sub)], lb);
+            const Window w = wl[t / A];
+            const int a = (int)(t % A);
+            wscan_task<BAND>(R, w, a, A, s_peq, s_acc, s_pacc, st, sink);
         }
         if constexpr (BAND) {                        // wave-uniform: no block barrier
             __builtin_amdgcn_wave_barrier();
@@ -1981,7 +2094,7 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     }
     R.cand_count = c->d_counters + 6 + 2 * round;
     R.cand_cap = (uint32_t)c->cand_cap;
-    R.sieve = (band && hp.filter && hp.sieve && !linked && !c->no_sieve) ? 1 : 0;
+    R.sieve = (band && hp.filter && hp.verify && hp.sieve && !linked && !c->no_sieve) ? 1 : 0;
     R.pairs = c->d_pairs;
     R.pair_count = c->d_counters + 12 + round;
     R.pair_cap = (uint32_t)c->pair_cap;
