@@ -898,9 +898,11 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
     __shared__ Window s_w[kStageCap];
     __shared__ uint32_t s_wc, s_wb;
     __shared__ int8_t s_pf[72];
+    __shared__ uint32_t s_ppeq[8];
     if (threadIdx.x == 0) s_wc = 0;
     const DevPanel* P = R.panel;
     if (threadIdx.x < 72) s_pf[threadIdx.x] = P->pf[threadIdx.x];
+    if (threadIdx.x < 8) s_ppeq[threadIdx.x] = P->pre_peq[threadIdx.x];
     __syncthreads();
     const Stage<Window> st{s_w, &s_wc, &s_wb, R.win2, R.win2_count, R.win_cap, R.flags, 4u};
     const bool front = P->where == kFront;
@@ -951,7 +953,7 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
                     const int cnt = min(16, hi - p0);
                     for (int q = 0; q < cnt; ++q) {
                         const uint32_t code = ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
-                        myers_step32(P->pre_peq[code], pv, mv, d, hbit);
+                        myers_step32(s_ppeq[code], pv, mv, d, hbit);
                         const int j = p0 + q + 1;
                         if (j >= rlo && j <= rhi) dmin_rows = min(dmin_rows, d);
                         if (j >= end_lo) dmin_end = min(dmin_end, d);
@@ -1954,10 +1956,14 @@ __global__ __launch_bounds__(256) void finalize2_linked_kernel(FinalArgs F) {
 // round-0-trimmed sequence: FRONT -> view[rstop:], BACK -> view[:rstart]) and queue it.
 __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
     __shared__ unsigned int s_hist[2 * (kMaxAdapters + 1) + 1];
+    __shared__ uint32_t s_nq, s_qbase;
     const int nh = F.A0 + 1;
     for (int x = threadIdx.x; x < nh + 1; x += blockDim.x) s_hist[x] = 0;
+    if (threadIdx.x == 0) s_nq = 0;
     __syncthreads();
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    ItemView v;
+    uint32_t qi = ~0u;                 // this read's slot in the block's share of the item list
     if (r < F.n_reads) {
         dmx_result out;
         out.bin1 = -1;
@@ -1975,7 +1981,6 @@ __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
             out.bin1 = (int16_t)a;
             out.rc1 = (uint8_t)o;
             if (F.mode == DMX_MODE_TWO_ROUND) {
-                ItemView v;
                 v.read = r;
                 v.strand = (uint8_t)o;
                 v.pad = 0;
@@ -1987,8 +1992,7 @@ __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
                     v.start = 0;
                     v.len = (uint32_t)out.m1.rstart;
                 }
-                const uint32_t idx = atomicAdd(F.n_items, 1u);
-                F.items[idx] = v;
+                qi = atomicAdd(&s_nq, 1u);    // LDS; one global atomic per block below
             } else {
                 atomicAdd(&s_hist[a + 1], 1u);
             }
@@ -1999,6 +2003,9 @@ __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
         F.res[r] = out;
     }
     __syncthreads();
+    if (threadIdx.x == 0) s_qbase = s_nq ? atomicAdd(F.n_items, s_nq) : 0u;
+    __syncthreads();
+    if (qi != ~0u) F.items[s_qbase + qi] = v;
     const int stride1 = F.mode == DMX_MODE_TWO_ROUND ? F.A1 + 1 : 1;
     const int ncounts = (F.A0 + 1) * stride1;
     for (int x = threadIdx.x; x < nh + 1; x += blockDim.x) {
