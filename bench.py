@@ -63,22 +63,110 @@ def cpu_baseline(workload: str, threads: int, target_s: float = 12.0):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: timed CPU baseline only
     from dmx import synth
+    linked = workload == "c5"
+    mode, rc = (2, False) if linked else (1, True)
     pilot = synth.generate(workload, n=400 * threads, seed=99)
     p1 = oracle.Panel(pilot["sp5"], oracle.FRONT)
     p2 = oracle.Panel(pilot["sp27"], oracle.BACK)
     t = time.perf_counter()
-    oracle.run_batch(p1, p2, pilot["blob"], pilot["offsets"], pilot["lengths"], 1, True, threads)
+    oracle.run_batch(p1, p2, pilot["blob"], pilot["offsets"], pilot["lengths"], mode, rc, threads)
     rate = len(pilot["lengths"]) / (time.perf_counter() - t)
     n = int(max(1000, min(2_000_000, rate * target_s)))
     d = synth.generate(workload, n=n, seed=98)
     t = time.perf_counter()
-    oracle.run_batch(p1, p2, d["blob"], d["offsets"], d["lengths"], 1, True, threads)
+    oracle.run_batch(p1, p2, d["blob"], d["offsets"], d["lengths"], mode, rc, threads)
     dt = time.perf_counter() - t
+    what = "linked -g F...R, no --rc" if linked else "two rounds, --rc"
     return {"value": n / dt / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "port",
-            "sample": f"{n} reads of workload {workload} (seed 98), two rounds, --rc, -e 0.1, "
+            "sample": f"{n} reads of workload {workload} (seed 98), {what}, -e 0.1, "
                       f"{dt:.1f} s wall on {threads} host threads (oracle/cutadapt_oracle.c, "
                       "a C restatement of cutadapt 4.9's Ukkonen-banded DP; cutadapt itself is "
                       "not installed)"}
+
+
+def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s,
+                   clusters, windows, windows_raw, resolved, traces):
+    # roofline of the dominant kernel: the shared-suffix filter (reads every base of every
+    # view; two launches per step, round 1 over the reads, round 2 over the round-1 tails)
+    filt_ms = (stage["filter0"] + stage["filter1"]) / (2 * K)
+    res = ctx.fetch()
+    m2 = res["bin1"] >= 0
+    n2 = int(m2.sum())
+    len2 = (lengths[m2] - res["m1_rstop"][m2]).astype(np.int64)
+    bytes0 = filter_algorithmic_bytes(lengths, int(windows_raw[0] / K))
+    bytes1 = filter_algorithmic_bytes(len2, int(windows_raw[1] / K))
+    alg_bytes = (bytes0 + bytes1) / 2
+    achieved = alg_bytes / (filt_ms / 1e3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.workload, args.reads)
+    A0, A1 = ctx.panel_sizes
+    cols = float(lengths.sum()) * 2 + float(len2.sum()) * 2     # filter columns, both strands
+    col_rate = cols / ((stage["filter0"] + stage["filter1"]) / K / 1e3)
+    return {
+        "metric": METRIC, "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
+        "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic",
+        "config": {"workload": f"{args.workload}: {args.reads} synthetic ONT reads per GPU "
+                               "(SURVEY.md §8d), two-round SP5 x SP27 demux, -e 0.1 --rc, "
+                               "inputs resident in HBM",
+                   "panel": f"{A0}x{A1}", "reads_per_gpu": args.reads,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": round(alg_bytes),
+                     "kernel": "dmx::filter_kernel", "avg_launch_ms": round(filt_ms, 3),
+                     "note": "the bit-vector filter is VALU-bound by construction "
+                             "(DESIGN.md §5): see 'valu' for its issue-rate fraction"},
+        "valu": {"filter_columns_per_s": col_rate,
+                 "filter_lane_ops_per_column": FILTER_OPS_PER_COLUMN,
+                 "filter_lane_ops_per_s": col_rate * FILTER_OPS_PER_COLUMN,
+                 "frac_of_measured_ceiling": col_rate * FILTER_OPS_PER_COLUMN / VALU_CEILING,
+                 "measured_ceiling_lane_ops_per_s": VALU_CEILING,
+                 "nominal_peak_lane_ops_per_s": VALU_PEAK_TOPS * 1e12,
+                 "source": "ops/column = SQ_INSTS_VALU x 64 / columns of the filter launch "
+                           "(profiles/r1_pmc_summary_c2x24_2M.txt); ceiling = independent "
+                           "v_bitop3 chains at full occupancy (tools/microbench/myers_ilp.hip)"},
+        "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
+        "clusters_per_step": (clusters / K).tolist(),
+        "filter_windows_per_step": (windows / K).tolist(),
+        "resolved_clusters_per_step": (resolved / K).tolist(),
+        "tracebacks_per_step": (traces / K).tolist(),
+        "reads_round2_per_gpu": n2,
+        "unknown_round1": int(counts[0]) if counts is not None else None,
+        "gen_s": round(gen_s, 1),
+    }
+
+
+def linked_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s):
+    """Config 5: linked primers.  Dominant kernel: round 1's full scan (every front primer over
+    every consensus: one lane per (read, pair))."""
+    res = ctx.fetch()
+    trimmed = int((res["bin1"] >= 0).sum())
+    scan_ms = stage["scan0"] / K
+    A0, _ = ctx.panel_sizes
+    L = lengths.astype(np.float64)
+    alg_bytes = float(np.sum(np.ceil(L / 4) + np.ceil(L / 8) + 12.0))
+    achieved = alg_bytes / (scan_ms / 1e3) / 1e9
+    return {
+        "metric": "Mreads/s linked-primer trimming (config 5, cutadapt -g F...R per pair)",
+        "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
+        "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic",
+        "config": {"workload": f"c5: {args.reads} synthetic COI consensuses per GPU (SURVEY.md "
+                               "§8d config 5), linked COI_primers.fa pairs, -e 0.1, no --rc, "
+                               "inputs resident in HBM",
+                   "pairs": A0, "reads_per_gpu": args.reads, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "algorithmic_bytes_per_launch": round(alg_bytes),
+                     "kernel": "dmx::scan_kernel<true>", "avg_launch_ms": round(scan_ms, 3),
+                     "note": "VALU-bound bit-vector scan (DESIGN.md §5)"},
+        "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
+        "trimmed_fraction": round(trimmed / max(1, len(lengths)), 4),
+        "gen_s": round(gen_s, 1),
+    }
 
 
 def main():
@@ -86,7 +174,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="c2x24", choices=["c2x24", "c2", "c4", "c1"])
+    ap.add_argument("--workload", default="c2x24", choices=["c2x24", "c2", "c4", "c1", "c5"],
+                    help="c5 = config 5, linked COI primers (-g F...R) on consensus FASTA")
     ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -113,10 +202,16 @@ def main():
     del d["blob"]
     gen_s = time.perf_counter() - t0
 
+    linked = args.workload == "c5"
     ctx = lib.Context(local_rank if world > 1 else 0)
-    ctx.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC, 0.1)
-    ctx.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC, 0.1)
-    ctx.set_mode(lib.MODE_TWO_ROUND)
+    if linked:   # 04_cleaning_primers.sh:377: -g F...R per pair, no --rc
+        ctx.set_panel(0, d["sp5"], lib.DMX_FRONT, 0.1)
+        ctx.set_panel(1, d["sp27"], lib.DMX_BACK, 0.1)
+        ctx.set_mode(lib.MODE_LINKED)
+    else:
+        ctx.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC, 0.1)
+        ctx.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC, 0.1)
+        ctx.set_mode(lib.MODE_TWO_ROUND)
     ctx.load(packed)
     del packed
 
@@ -179,57 +274,11 @@ def main():
     K = args.steps
     total_reads = args.reads * world * K
     value = total_reads / elapsed / 1e6
-    # roofline of the dominant kernel: the shared-suffix filter (reads every base of every
-    # view; two launches per step, round 1 over the reads, round 2 over the round-1 tails)
-    filt_ms = (stage["filter0"] + stage["filter1"]) / (2 * K)
-    res = ctx.fetch()
-    m2 = res["bin1"] >= 0
-    n2 = int(m2.sum())
-    len2 = (lengths[m2] - res["m1_rstop"][m2]).astype(np.int64)
-    bytes0 = filter_algorithmic_bytes(lengths, int(windows_raw[0] / K))
-    bytes1 = filter_algorithmic_bytes(len2, int(windows_raw[1] / K))
-    alg_bytes = (bytes0 + bytes1) / 2
-    achieved = alg_bytes / (filt_ms / 1e3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.workload, args.reads)
-    A0, A1 = ctx.panel_sizes
-    cols = float(lengths.sum()) * 2 + float(len2.sum()) * 2     # filter columns, both strands
-    col_rate = cols / ((stage["filter0"] + stage["filter1"]) / K / 1e3)
-
-    out = {
-        "metric": METRIC, "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
-        "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-        "data": "synthetic",
-        "config": {"workload": f"{args.workload}: {args.reads} synthetic ONT reads per GPU "
-                               "(SURVEY.md §8d), two-round SP5 x SP27 demux, -e 0.1 --rc, "
-                               "inputs resident in HBM",
-                   "panel": f"{A0}x{A1}", "reads_per_gpu": args.reads,
-                   "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": round(alg_bytes),
-                     "kernel": "dmx::filter_kernel", "avg_launch_ms": round(filt_ms, 3),
-                     "note": "the bit-vector filter is VALU-bound by construction "
-                             "(DESIGN.md §5): see 'valu' for its issue-rate fraction"},
-        "valu": {"filter_columns_per_s": col_rate,
-                 "filter_lane_ops_per_column": FILTER_OPS_PER_COLUMN,
-                 "filter_lane_ops_per_s": col_rate * FILTER_OPS_PER_COLUMN,
-                 "frac_of_measured_ceiling": col_rate * FILTER_OPS_PER_COLUMN / VALU_CEILING,
-                 "measured_ceiling_lane_ops_per_s": VALU_CEILING,
-                 "nominal_peak_lane_ops_per_s": VALU_PEAK_TOPS * 1e12,
-                 "source": "ops/column = SQ_INSTS_VALU x 64 / columns of the filter launch "
-                           "(profiles/r1_pmc_summary_c2x24_2M.txt); ceiling = independent "
-                           "v_bitop3 chains at full occupancy (tools/microbench/myers_ilp.hip)"},
-        "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
-        "clusters_per_step": (clusters / K).tolist(),
-        "filter_windows_per_step": (windows / K).tolist(),
-        "resolved_clusters_per_step": (resolved / K).tolist(),
-        "tracebacks_per_step": (traces / K).tolist(),
-        "reads_round2_per_gpu": n2,
-        "unknown_round1": int(counts[0]) if counts is not None else None,
-        "gen_s": round(gen_s, 1),
-    }
+    if linked:
+        out = linked_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s)
+    else:
+        out = two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s,
+                             clusters, windows, windows_raw, resolved, traces)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_threads)
     if rank == 0:

@@ -1880,33 +1880,46 @@ struct FinalArgs {
 //   combine: best pair by summed score, then summed errors, then pair order.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void finalize0_linked_kernel(FinalArgs F) {
+    __shared__ uint32_t s_nq, s_qbase;
+    if (threadIdx.x == 0) s_nq = 0;
+    __syncthreads();
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= F.n_reads) return;
-    dmx_result out;
-    out.bin1 = out.bin2 = -1;
-    out.rc1 = out.rc2 = 0;
-    out.flags = 0;
-    out._pad = 0;
-    out.m1 = dmx_match{0, 0, 0, 0, 0, 0};
-    out.m2 = out.m1;
-    F.res[r] = out;
-    F.linked_best[r] = ~0ull;
-    const uint32_t n = F.lens[r];
-    for (int a = 0; a < F.A0; ++a) {
-        const uint64_t key = F.winner[(size_t)r * F.A0 + a];
-        if (key == ~0ull) continue;
-        dmx_match m;
-        int aa, o;
-        decode_match(key, F.origin[(size_t)r * F.A0 + a], n, F.p0, m, aa, o);
-        ItemView v;
-        v.read = r;
-        v.strand = 0;
-        v.pad = 0;
-        v.only_adapter = (int16_t)a;
-        v.start = (uint32_t)m.rstop;
-        v.len = n - (uint32_t)m.rstop;
-        const uint32_t idx = atomicAdd(F.n_items, 1u);
-        F.items[idx] = v;
+    uint32_t nmine = 0, qi = 0;
+    uint32_t n = 0;
+    if (r < F.n_reads) {
+        dmx_result out;
+        out.bin1 = out.bin2 = -1;
+        out.rc1 = out.rc2 = 0;
+        out.flags = 0;
+        out._pad = 0;
+        out.m1 = dmx_match{0, 0, 0, 0, 0, 0};
+        out.m2 = out.m1;
+        F.res[r] = out;
+        F.linked_best[r] = ~0ull;
+        n = F.lens[r];
+        for (int a = 0; a < F.A0; ++a) nmine += F.winner[(size_t)r * F.A0 + a] != ~0ull;
+        if (nmine) qi = atomicAdd(&s_nq, nmine);   // LDS; one global atomic per block below
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_qbase = s_nq ? atomicAdd(F.n_items, s_nq) : 0u;
+    __syncthreads();
+    if (nmine) {
+        uint32_t idx = s_qbase + qi;
+        for (int a = 0; a < F.A0; ++a) {
+            const uint64_t key = F.winner[(size_t)r * F.A0 + a];
+            if (key == ~0ull) continue;
+            dmx_match m;
+            int aa, o;
+            decode_match(key, F.origin[(size_t)r * F.A0 + a], n, F.p0, m, aa, o);
+            ItemView v;
+            v.read = r;
+            v.strand = 0;
+            v.pad = 0;
+            v.only_adapter = (int16_t)a;
+            v.start = (uint32_t)m.rstop;
+            v.len = n - (uint32_t)m.rstop;
+            F.items[idx++] = v;
+        }
     }
 }
 

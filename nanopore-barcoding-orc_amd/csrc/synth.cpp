@@ -58,6 +58,8 @@ struct SynthParams {
     double n_fraction;         // per insert base: an 'N'
     int32_t n1_used, n2_used;  // adapters drawn from the first n*_used of each panel
     int32_t flank_max;         // random flank length U[0, flank_max] on both ends
+    int32_t linked;            // 1: pair i of both panels (linked primers, config 5)
+    double missing_fraction;   // linked: one primer (front or back, equally) left out
 };
 
 static uint32_t draw_length(const SynthParams& p, Rng& g) {
@@ -67,9 +69,11 @@ static uint32_t draw_length(const SynthParams& p, Rng& g) {
     } else if (p.length_model == 1) {
         const double mu = std::log(p.len_mean) - 0.5 * p.len_sigma_log * p.len_sigma_log;
         L = std::exp(mu + p.len_sigma_log * g.normal());
-    } else {   // 70% COI insert U[300,900], 30% rRNA insert N(3000,150); + ~116 nt of adapters
-        if (g.uni() < 0.7) L = 300 + g.uni() * 600 + 116;
+    } else if (p.length_model == 2) {   // 70% COI insert U[300,900], 30% rRNA N(3000,150)
+        if (g.uni() < 0.7) L = 300 + g.uni() * 600 + 116;   // + ~116 nt of adapters
         else L = 3000 + 150 * g.normal() + 116;
+    } else {   // 3: COI amplicon consensus: insert U[300,900] + two ~26-nt primers
+        L = 300 + g.uni() * 600 + 52;
     }
     if (L < p.len_min) L = p.len_min;
     if (L > p.len_max) L = p.len_max;
@@ -90,20 +94,41 @@ void synth_lengths(const SynthParams* p, uint64_t seed, uint64_t first, size_t n
     }
 }
 
+// One base of an IUPAC code (degenerate primer positions are instantiated at random).
+static char instantiate(char c, Rng& g) {
+    const char* set;
+    switch (c) {
+        case 'A': case 'C': case 'G': case 'T': return c;
+        case 'R': set = "AG"; break;
+        case 'Y': set = "CT"; break;
+        case 'S': set = "CG"; break;
+        case 'W': set = "AT"; break;
+        case 'K': set = "GT"; break;
+        case 'M': set = "AC"; break;
+        case 'B': set = "CGT"; break;
+        case 'D': set = "AGT"; break;
+        case 'H': set = "ACT"; break;
+        case 'V': set = "ACG"; break;
+        default: set = "ACGT"; break;
+    }
+    return set[g.below((uint32_t)strlen(set))];
+}
+
 static void mutate_into(const char* a, int m, double e, Rng& g, std::vector<char>& out) {
     for (int i = 0; i < m; ++i) {
+        const char ai = instantiate(a[i], g);
         if (g.uni() < e) {
             const double k = g.uni();
             if (k < 0.6) {
                 char c;
-                do c = kBases[g.below(4)]; while (c == a[i]);
+                do c = kBases[g.below(4)]; while (c == ai);
                 out.push_back(c);
             } else if (k < 0.8) {
                 out.push_back(kBases[g.below(4)]);
-                out.push_back(a[i]);
+                out.push_back(ai);
             }   // else deletion
         } else {
-            out.push_back(a[i]);
+            out.push_back(ai);
         }
     }
 }
@@ -122,15 +147,22 @@ static void gen_one(const SynthParams& p, const char* const* p1, const int* l1,
         for (uint32_t x = 0; x < L; ++x) s.push_back(kBases[g.below(4)]);
     } else {
         i = (int)g.below((uint32_t)p.n1_used);
-        j = (int)g.below((uint32_t)p.n2_used);
+        j = p.linked ? i : (int)g.below((uint32_t)p.n2_used);
+        bool no1 = false, no2 = false;   // linked: one primer missing
+        if (p.linked && g.uni() < p.missing_fraction) {
+            if (g.uni() < 0.5) no1 = true;
+            else no2 = true;
+        }
         const int f1 = p.flank_max ? (int)g.below((uint32_t)p.flank_max + 1) : 0;
         const int f2 = p.flank_max ? (int)g.below((uint32_t)p.flank_max + 1) : 0;
         for (int x = 0; x < f1; ++x) s.push_back(kBases[g.below(4)]);
-        mutate_into(p1[i], l1[i], p.adapter_error, g, s);
+        if (!no1) mutate_into(p1[i], l1[i], p.adapter_error, g, s);
         const int ins = (int)L - l1[i] - l2[j];
         for (int x = 0; x < ins; ++x)
             s.push_back(g.uni() < p.n_fraction ? 'N' : kBases[g.below(4)]);
-        mutate_into(p2[j], l2[j], p.adapter_error, g, s);
+        if (!no2) mutate_into(p2[j], l2[j], p.adapter_error, g, s);
+        if (no1) i = -1;
+        if (no2) j = -1;
         for (int x = 0; x < f2; ++x) s.push_back(kBases[g.below(4)]);
     }
     const size_t n = s.size();

@@ -23,7 +23,8 @@ class SynthParams(ctypes.Structure):
                 ("len_max", ctypes.c_int32), ("adapter_error", ctypes.c_double),
                 ("rc_fraction", ctypes.c_double), ("adapterless_fraction", ctypes.c_double),
                 ("n_fraction", ctypes.c_double), ("n1_used", ctypes.c_int32),
-                ("n2_used", ctypes.c_int32), ("flank_max", ctypes.c_int32)]
+                ("n2_used", ctypes.c_int32), ("flank_max", ctypes.c_int32),
+                ("linked", ctypes.c_int32), ("missing_fraction", ctypes.c_double)]
 
 
 # name -> (params, n_sp5, n_sp27, panel kind)
@@ -45,7 +46,21 @@ CONFIGS = {
     "c4": dict(length_model=2, len_mean=0, len_sigma_log=0, len_min=300, len_max=6000,
                adapter_error=0.15, rc_fraction=0.10, adapterless_fraction=0.02, n_fraction=0.001,
                panel=(12, 12), flank_max=8, default_n=50_000_000, seed=4),
+    # config 5: amplicon_sorter consensuses (FASTA) framed by the linked COI primer pairs of
+    # COI_primers.fa (IUPAC positions instantiated at random), 5% primer error, 10% with one
+    # primer missing (these must stay untrimmed), no RC (04_cleaning_primers.sh:377)
+    "c5": dict(length_model=3, len_mean=0, len_sigma_log=0, len_min=100, len_max=2000,
+               adapter_error=0.05, rc_fraction=0.0, adapterless_fraction=0.0, n_fraction=0.0,
+               panel=(2, 2), flank_max=4, default_n=10_000_000, seed=5, linked=1,
+               missing_fraction=0.10),
 }
+
+
+def linked_panels():
+    """(pair ids, forward primers, reverse primers) of the config-5 linked pairs."""
+    from . import panel
+    pairs = panel.primer_pairs(os.path.join(os.path.dirname(panel.SP5_FASTA), "COI_primers.fa"))
+    return [p[0] for p in pairs], [p[1] for p in pairs], [p[2] for p in pairs]
 
 _lib = None
 
@@ -111,7 +126,11 @@ def generate(config: str, n: int | None = None, seed: int | None = None, first: 
     seed = cfg.pop("seed") if seed is None else seed
     cfg.pop("seed", None)
     n1, n2 = cfg.pop("panel")
-    names1, sp5, names2, sp27 = panels(n1, n2)
+    if cfg.get("linked"):
+        names1, sp5, sp27 = linked_panels()
+        names2 = list(names1)
+    else:
+        names1, sp5, names2, sp27 = panels(n1, n2)
     p = SynthParams(n1_used=n1, n2_used=n2, **cfg)
     L = lib()
     caps = np.empty(n, dtype=np.uint32)

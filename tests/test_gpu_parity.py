@@ -189,3 +189,17 @@ def test_linked_matches_oracle(ctx, kind):
     for a in range(A):
         assert c[(a + 1) * (A + 1) + a + 1] == (exp["bin1"] == a).sum()
     assert c[0] == (exp["bin1"] < 0).sum()
+
+
+def test_config5_linked_matches_oracle(ctx):
+    """SURVEY.md §8d config 5 (synthetic COI consensuses, linked pairs, IUPAC instantiated,
+    10% with one primer missing) on the GPU vs the oracle."""
+    d = synth.generate("c5", n=20000)
+    exp = oracle.run_batch(oracle.Panel(d["sp5"], oracle.FRONT), oracle.Panel(d["sp27"], oracle.BACK),
+                           d["blob"], d["offsets"], d["lengths"], mode=2, use_rc=False, threads=8)
+    untrimmed = (exp["bin1"] < 0).mean()
+    assert 0.05 < untrimmed < 0.25
+    ctx.set_panel(0, d["sp5"], lib.DMX_FRONT)
+    ctx.set_panel(1, d["sp27"], lib.DMX_BACK)
+    ctx.set_mode(lib.MODE_LINKED)
+    _assert_same(ctx.run(lib.pack(d["blob"], d["offsets"], d["lengths"])), exp)

@@ -101,3 +101,15 @@ def test_primer_pairs_follow_04_header_convention(tmp_path):
     f.write_text(">x|Forward_A\nACGT\nACGT\n\n>y|Forward_C\nGGGG\n>z|Reverse_A_C_D\nTTTT\n"
                  ">w|Forward_A\nCCCCAAAA\n")
     assert panel.primer_pairs(str(f)) == [("A", "CCCCAAAA", "TTTT"), ("C", "GGGG", "TTTT")]
+
+
+def test_synth_config5_linked_shape():
+    d = synth.generate("c5", n=2000)
+    t = d["truth"]
+    miss = (t[:, 0] < 0) | (t[:, 1] < 0)
+    assert 0.05 < miss.mean() < 0.16                 # one primer missing in ~10%
+    assert ((t[:, 0] == t[:, 1]) | miss).all()       # linked: the same pair at both ends
+    assert set(np.unique(t[~miss, 0])) <= {0, 1}
+    assert 300 < d["lengths"].mean() < 800
+    e = synth.generate("c5", n=100, first=1900)
+    assert (e["lengths"] == d["lengths"][1900:]).all()
