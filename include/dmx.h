@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define DMX_ABI_VERSION 2
+#define DMX_ABI_VERSION 3
 
 /* Panel flags (dmx_set_panel.flags). */
 #define DMX_FRONT 0x01  /* -g ADAPTER: 5' adapter, Where.FRONT (prefix of adapter may be skipped at read start) */
@@ -97,6 +97,20 @@ int dmx_pack(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens
  * input.  Synchronous: uploads, runs both rounds on the GPU, downloads `out`. */
 int dmx_run(dmx_ctx* ctx, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
             const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out);
+
+/* Number of visible HIP devices (0 if none). */
+int dmx_device_count(void);
+
+/* Multi-GPU form of dmx_run: the batch (dmx_pack layout) is split into
+ * n_ctx contiguous read ranges balanced by total length, each range runs on its own context
+ * (one device each) from its own host thread, and results land in `out` in input order.
+ * out_counts (optional, n_counts entries) receives the per-bin counts summed over the shards
+ * (the exchange is a few hundred integers; the per-read results come to the host anyway).
+ * Returns the number of count entries (or DMX_OK without out_counts), negative on error
+ * (message via dmx_last_error(ctxs[0])).  Contexts must share mode and panels. */
+int dmx_run_multi(dmx_ctx* const* ctxs, int n_ctx, const uint32_t* seq2b, const uint32_t* nmask,
+                  const uint64_t* offsets, const uint32_t* lens, size_t n_words, size_t n_reads,
+                  dmx_result* out, uint64_t* out_counts, size_t n_counts);
 
 /* Device-resident form (benchmarks / pipelined hosts): dmx_load copies a packed batch to HBM
  * once; dmx_exec enqueues the full pipeline on the context's stream (asynchronous); dmx_sync

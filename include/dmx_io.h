@@ -1,0 +1,84 @@
+/*
+ * dmx_io.h — C-ABI of libdmx_io.so: native FASTQ/FASTA(.gz) ingest fused with the 2-bit
+ * packer, and per-bin (demultiplexed) FASTQ/FASTA(.gz) writers.  Host-only (no GPU).
+ *
+ * Replaces the record I/O around cutadapt's hot loop: dnaio's FASTQ/FASTA
+ * parser and xopen's gzip reader/writers for `IN.fastq.gz` and `-o OUT/{name}_X.fastq.gz`
+ * (scripts/02_cutadapt_loop.sh:70-71,100-101; scripts/04_cleaning_primers.sh:377-388).
+ * dnaio/xopen are not vendored in /root/reference; conventions restated in dmx_io.cpp.
+ *
+ * Reader: a background thread inflates (zlib; multi-member gzip accepted) and a pool of
+ * `threads` workers indexes lines, validates records and packs sequences into the libdmx device
+ * layout (include/dmx.h, DMX_PACK_PAD), one batch of about `batch_bytes` of text at a time, up
+ * to two batches ahead of the consumer.  Writer ("sink"): dmx_sink_write renders the records of
+ * a batch into per-output buffers and compresses them as independent gzip members on
+ * `threads` workers, in the background, while the caller moves on to the next batch; records
+ * keep input order within every output.
+ * Status 0 = OK, negative = error (message via dmx_reader_error / dmx_sink_error).
+ */
+#ifndef DMX_IO_H
+#define DMX_IO_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DMX_IO_ABI_VERSION 1
+
+/* One batch of records (library-owned; valid until dmx_batch_free). Spans are [start, end). */
+typedef struct dmx_batch {
+    size_t n_reads;
+    int32_t fasta;          /* 1: FASTA input (no qualities)                                   */
+    int32_t _pad;
+    const uint8_t* text;    /* record text as read (after decompression)                        */
+    const uint64_t* head;   /* n x {start, end}: name line without '@' / '>' (and without '\r') */
+    const uint8_t* seqtext; /* FASTQ: == text; FASTA: the records' sequence lines joined         */
+    const uint64_t* seq;    /* n x {start, end} into seqtext                                     */
+    const uint64_t* qual;   /* n x {start, end} into text; NULL for FASTA                        */
+    const uint32_t* lens;   /* n sequence lengths                                               */
+    /* the same reads in the libdmx device layout (dmx_pack output), ready for dmx_run */
+    const uint32_t* seq2b;
+    const uint32_t* nmask;
+    const uint64_t* offsets;
+    size_t n_words;
+    uint64_t total_nt;
+} dmx_batch;
+
+typedef struct dmx_reader dmx_reader;
+typedef struct dmx_sink dmx_sink;
+
+int dmx_io_abi_version(void);
+
+/* path: a file (gzip detected by its magic bytes) or "-" for stdin. */
+int dmx_reader_open(const char* path, size_t batch_bytes, int threads, dmx_reader** out);
+/* Next batch in input order; *out = NULL at end of input. */
+int dmx_reader_next(dmx_reader* r, dmx_batch** out);
+const char* dmx_reader_error(dmx_reader* r);
+void dmx_reader_close(dmx_reader* r);
+/* Releases the caller's reference (a sink still rendering the batch keeps its own). */
+void dmx_batch_free(dmx_batch* b);
+
+/* Open n_out outputs (created / truncated now, like cutadapt's demultiplexed outputs); a path
+ * ending in ".gz" is gzip-compressed at `level`.  fasta_out: write FASTA records. */
+int dmx_sink_open(const char* const* paths, int n_out, int fasta_out, int level, int threads,
+                  dmx_sink** out);
+/* Queue the records of batch b: read i goes to output out_idx[i] (-1 = not written) as
+ *   name = head + " rc" x n_rc[i],
+ *   sequence = orient(seq, rc[i])[start[i]:stop[i]] (orient = reverse complement if rc[i],
+ *   qualities reversed with it).
+ * Asynchronous: returns once the previous batch has been written; the arrays are copied. */
+int dmx_sink_write(dmx_sink* s, dmx_batch* b, const int32_t* out_idx, const int32_t* start,
+                   const int32_t* stop, const uint8_t* rc, const uint8_t* n_rc);
+/* Wait for pending writes, close every output; n_written / bp_written (n_out entries each,
+ * may be NULL) receive the records and bases written per output. */
+int dmx_sink_close(dmx_sink* s, uint64_t* n_written, uint64_t* bp_written);
+const char* dmx_sink_error(dmx_sink* s);
+/* Free a sink after dmx_sink_close (or to abandon it). */
+void dmx_sink_free(dmx_sink* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DMX_IO_H */

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "dmx_internal.h"
+#include "pack.h"
 
 using namespace dmx;
 
@@ -29,7 +30,6 @@ using namespace dmx;
 
 namespace {
 
-constexpr int kPackAlign = 32;   // every read starts on a 32-nt (one nmask word) boundary
 constexpr int kMinFilterLen = 10; // shortest shared suffix worth a filter pass
 constexpr size_t kGuardWords = 64; // zeroed words before/after the packed device buffers
 
@@ -65,47 +65,6 @@ int dev_alloc(Ctx* c, T** p, size_t count) {
     return DMX_OK;
 }
 
-struct PackTables {
-    uint8_t code[256];
-    uint8_t nflag[256];
-    PackTables() {
-        for (int i = 0; i < 256; ++i) {
-            code[i] = 0;
-            nflag[i] = 1;
-        }
-        const char* s = "ACGT";
-        for (int k = 0; k < 4; ++k) {
-            code[(uint8_t)s[k]] = code[(uint8_t)(s[k] + 32)] = (uint8_t)k;
-            nflag[(uint8_t)s[k]] = nflag[(uint8_t)(s[k] + 32)] = 0;
-        }
-    }
-};
-const PackTables kTables;
-
-void pack_range(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens, size_t lo,
-                size_t hi, const uint64_t* out_offsets, uint32_t* seq, uint32_t* nmask) {
-    for (size_t r = lo; r < hi; ++r) {
-        const uint8_t* src = ascii + offsets[r];
-        const uint32_t n = lens[r];
-        const uint64_t g0 = out_offsets[r];   // multiple of 32
-        uint32_t* sw = seq + g0 / 16;
-        uint32_t* nw = nmask + g0 / 32;
-        for (uint32_t x = 0; x < n; x += 32) {
-            const uint32_t cnt = std::min<uint32_t>(32u, n - x);
-            uint32_t w0 = 0, w1 = 0, nb = 0;
-            for (uint32_t y = 0; y < cnt; ++y) {
-                const uint8_t ch = src[x + y];
-                const uint32_t cd = kTables.code[ch];
-                if (y < 16) w0 |= cd << (2 * y);
-                else w1 |= cd << (2 * (y - 16));
-                nb |= (uint32_t)kTables.nflag[ch] << y;
-            }
-            sw[x / 16] = w0;
-            if (cnt > 16) sw[x / 16 + 1] = w1;
-            nw[x / 32] = nb;
-        }
-    }
-}
 
 int ensure_pipeline(Ctx* c) {
     const size_t n = c->n_reads;
@@ -687,6 +646,106 @@ int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint
     }
     c->err = "candidate cluster buffer overflow";
     return DMX_E_NOMEM;
+}
+
+int dmx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int dmx_run_multi(dmx_ctx* const* ctxs, int n_ctx, const uint32_t* seq2b, const uint32_t* nmask,
+                  const uint64_t* offsets, const uint32_t* lens, size_t n_words, size_t n_reads,
+                  dmx_result* out, uint64_t* out_counts, size_t n_counts) {
+    if (!ctxs || n_ctx <= 0 || !ctxs[0]) return DMX_E_INVALID;
+    dmx_ctx* c0 = ctxs[0];
+    if (n_reads && (!seq2b || !nmask || !offsets || !lens || !out)) return DMX_E_INVALID;
+    for (int k = 1; k < n_ctx; ++k) {
+        if (!ctxs[k] || ctxs[k]->mode != c0->mode || ctxs[k]->panel[0].n != c0->panel[0].n ||
+            ctxs[k]->panel[1].n != c0->panel[1].n) {
+            c0->err = "dmx_run_multi: contexts must share mode and panels";
+            return DMX_E_INVALID;
+        }
+    }
+    // contiguous read ranges balanced by total length; outputs land in place,
+    // so shard order = input order
+    std::vector<size_t> cut(n_ctx + 1, n_reads);
+    cut[0] = 0;
+    {
+        uint64_t total = 0;
+        for (size_t r = 0; r < n_reads; ++r) total += lens[r];
+        uint64_t acc = 0;
+        int k = 1;
+        for (size_t r = 0; r < n_reads && k < n_ctx; ++r) {
+            acc += lens[r];
+            while (k < n_ctx && acc * (uint64_t)n_ctx >= total * (uint64_t)k) cut[k++] = r + 1;
+        }
+        for (int j = 1; j <= n_ctx; ++j) cut[j] = std::max(cut[j], cut[j - 1]);
+    }
+    std::vector<int> rcs(n_ctx, DMX_OK);
+    std::vector<std::vector<uint64_t>> cnt(n_ctx);
+    auto shard = [&](int k) {
+        dmx_ctx* c = ctxs[k];
+        const size_t lo = cut[k], hi = cut[k + 1];
+        const size_t n = hi - lo;
+        if (!n) return;   // nothing to run; its counts are zero
+        uint64_t g0 = 0;
+        {
+            if (offsets[lo] < (uint64_t)DMX_PACK_PAD || offsets[lo] % kPackAlign) {
+                c->err = "dmx_run_multi: offsets must come from dmx_pack";
+                rcs[k] = DMX_E_INVALID;
+                return;
+            }
+            g0 = offsets[lo] - DMX_PACK_PAD;
+        }
+        std::vector<uint64_t> offs(n);
+        uint64_t end = 0;
+        for (size_t r = 0; r < n; ++r) {
+            offs[r] = offsets[lo + r] - g0;
+            end = std::max<uint64_t>(end, offs[r] + lens[lo + r]);
+        }
+        const size_t w0 = (size_t)(g0 / 16);
+        if (w0 >= n_words) {
+            c->err = "dmx_run_multi: offsets beyond the packed buffer";
+            rcs[k] = DMX_E_INVALID;
+            return;
+        }
+        const size_t words =
+            std::min(n_words - w0, (size_t)((end + DMX_PACK_PAD + 31) / 32 * 2 + 4));
+        int rc = dmx_run(c, seq2b + w0, nmask + g0 / 32, offs.data(), lens + lo, words, n, out + lo);
+        if (rc == DMX_OK && out_counts) {
+            cnt[k].assign(c->n_counts, 0);
+            rc = dmx_counts(c, cnt[k].data(), cnt[k].size());
+            if (rc > 0) rc = DMX_OK;
+        }
+        rcs[k] = rc;
+    };
+    if (n_ctx == 1) {
+        shard(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int k = 0; k < n_ctx; ++k) th.emplace_back(shard, k);
+        for (auto& t : th) t.join();
+    }
+    for (int k = 0; k < n_ctx; ++k) {
+        if (rcs[k] != DMX_OK) {
+            if (k) c0->err = "device " + std::to_string(ctxs[k]->device) + ": " + ctxs[k]->err;
+            return rcs[k];
+        }
+    }
+    if (out_counts) {
+        size_t nc = 0;
+        for (int k = 0; k < n_ctx; ++k) nc = std::max(nc, cnt[k].size());
+        if (n_counts < nc) {
+            c0->err = "counts buffer too small";
+            return DMX_E_INVALID;
+        }
+        for (size_t i = 0; i < n_counts; ++i) out_counts[i] = 0;
+        for (int k = 0; k < n_ctx; ++k)
+            for (size_t i = 0; i < cnt[k].size(); ++i) out_counts[i] += cnt[k][i];
+        return (int)nc;
+    }
+    return DMX_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,927 @@
+// dmx_io.cpp — libdmx_io: native FASTQ/FASTA(.gz) ingest fused with the 2-bit packer, and
+// per-bin writers with parallel gzip (include/dmx_io.h).
+//
+// Record conventions restated from dnaio/xopen as cutadapt 4.9 uses them (not vendored in
+// /root/reference):
+//  * FASTQ: 4 lines per record; line 1 starts with '@' and its remainder is the record name;
+//    line 3 starts with '+'; sequence and quality lengths must agree; "\r\n" line ends accepted.
+//    Output records are written as "@name\nSEQ\n+\nQUAL\n".
+//  * FASTA: '>' name line followed by any number of sequence lines, joined (whitespace at line
+//    ends stripped); output records are written on one line, ">name\nSEQ\n".
+//  * A reverse-complemented read (--rc) gets " rc" appended to its name, its sequence reverse
+//    complemented (IUPAC codes complemented, case kept) and its qualities reversed.
+//  * gzip output is written as a series of independent members (a valid gzip file; readers
+//    decompress it as one stream); an output that receives no records is still a valid (empty)
+//    gzip file, like xopen's.
+#include "../../include/dmx_io.h"
+
+#include <fcntl.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pack.h"
+
+namespace {
+
+constexpr uint64_t kPad = 64;   // DMX_PACK_PAD (include/dmx.h)
+
+int clamp_threads(int t) {
+    if (t <= 0) t = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(t, 64));
+}
+
+// Run f(t) for t in [0, nth) on nth threads (the calling thread takes t = 0).
+template <typename F>
+void parallel(int nth, F&& f) {
+    if (nth <= 1) {
+        f(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(nth - 1);
+    for (int t = 1; t < nth; ++t) th.emplace_back([&f, t] { f(t); });
+    f(0);
+    for (auto& x : th) x.join();
+}
+
+// ------------------------------------------------------------------------------------------
+// sources
+
+struct Source {
+    virtual ~Source() = default;
+    virtual long read(uint8_t* dst, size_t cap) = 0;   // bytes read, 0 = end, < 0 = error
+    std::string err;
+};
+
+struct FdSource : Source {
+    int fd = -1;
+    bool own = false;
+    ~FdSource() override {
+        if (own && fd >= 0) ::close(fd);
+    }
+    long read(uint8_t* dst, size_t cap) override {
+        size_t got = 0;
+        while (got < cap) {
+            const ssize_t n = ::read(fd, dst + got, cap - got);
+            if (n < 0) {
+                if (errno == EINTR) continue;
+                err = std::string("read: ") + strerror(errno);
+                return -1;
+            }
+            if (n == 0) break;
+            got += (size_t)n;
+        }
+        return (long)got;
+    }
+};
+
+// Pushed-back first bytes (format sniffing) in front of another source.
+struct PrefixSource : Source {
+    std::unique_ptr<Source> inner;
+    std::vector<uint8_t> head;
+    size_t pos = 0;
+    long read(uint8_t* dst, size_t cap) override {
+        size_t got = 0;
+        if (pos < head.size()) {
+            got = std::min(cap, head.size() - pos);
+            memcpy(dst, head.data() + pos, got);
+            pos += got;
+        }
+        if (got < cap) {
+            const long n = inner->read(dst + got, cap - got);
+            if (n < 0) {
+                err = inner->err;
+                return -1;
+            }
+            got += (size_t)n;
+        }
+        return (long)got;
+    }
+};
+
+// zlib inflate of a gzip file; concatenated members (pigz / bgzip / our own writer) are read
+// as one stream.
+struct GzSource : Source {
+    std::unique_ptr<Source> raw;
+    z_stream zs{};
+    std::vector<uint8_t> in;
+    bool in_eof = false, ended = false, started = false;
+    explicit GzSource(std::unique_ptr<Source> r) : raw(std::move(r)), in(1 << 20) {}
+    ~GzSource() override {
+        if (started) inflateEnd(&zs);
+    }
+    bool refill() {
+        if (zs.avail_in || in_eof) return true;
+        const long n = raw->read(in.data(), in.size());
+        if (n < 0) {
+            err = raw->err;
+            return false;
+        }
+        if (n == 0) in_eof = true;
+        zs.next_in = in.data();
+        zs.avail_in = (uInt)n;
+        return true;
+    }
+    long read(uint8_t* dst, size_t cap) override {
+        if (!started) {
+            if (inflateInit2(&zs, 15 + 16) != Z_OK) {
+                err = "inflateInit2 failed";
+                return -1;
+            }
+            started = true;
+        }
+        size_t got = 0;
+        while (got < cap && !ended) {
+            if (!refill()) return -1;
+            if (zs.avail_in == 0 && in_eof) {
+                err = "truncated gzip input";
+                return -1;
+            }
+            const size_t want = std::min<size_t>(cap - got, 1u << 30);
+            zs.next_out = dst + got;
+            zs.avail_out = (uInt)want;
+            const int ret = inflate(&zs, Z_NO_FLUSH);
+            got += want - zs.avail_out;
+            if (ret == Z_STREAM_END) {
+                // another member may follow (skip zero padding some writers append)
+                for (;;) {
+                    if (!refill()) return -1;
+                    while (zs.avail_in && *zs.next_in == 0) {
+                        ++zs.next_in;
+                        --zs.avail_in;
+                    }
+                    if (zs.avail_in || in_eof) break;
+                }
+                if (zs.avail_in == 0) {
+                    ended = true;
+                } else if (inflateReset(&zs) != Z_OK) {
+                    err = "inflateReset failed";
+                    return -1;
+                }
+            } else if (ret != Z_OK && ret != Z_BUF_ERROR) {
+                err = std::string("gzip: ") + (zs.msg ? zs.msg : "corrupt input");
+                return -1;
+            }
+        }
+        return (long)got;
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// batches
+
+struct Batch : dmx_batch {
+    std::atomic<int> refs{1};
+    std::vector<uint8_t> text_v, seqtext_v;
+    std::vector<uint64_t> head_v, seq_v, qual_v, offs_v;
+    std::vector<uint32_t> lens_v, seq2b_v, nmask_v;
+    void publish() {
+        text = text_v.data();
+        head = head_v.data();
+        seqtext = fasta ? seqtext_v.data() : text_v.data();
+        seq = seq_v.data();
+        qual = fasta ? nullptr : qual_v.data();
+        lens = lens_v.data();
+        seq2b = seq2b_v.data();
+        nmask = nmask_v.data();
+        offsets = offs_v.data();
+        n_words = seq2b_v.size();
+    }
+};
+
+void release(Batch* b) {
+    if (b && b->refs.fetch_sub(1) == 1) delete b;
+}
+
+// Newline positions of buf[0, n) in order, found by nth threads.
+std::vector<uint64_t> newlines(const uint8_t* buf, size_t n, int nth) {
+    nth = (int)std::min<size_t>(nth, std::max<size_t>(1, n >> 20));
+    std::vector<std::vector<uint64_t>> part(nth);
+    parallel(nth, [&](int t) {
+        const size_t lo = n * t / nth, hi = n * (t + 1) / nth;
+        auto& v = part[t];
+        v.reserve((hi - lo) / 64 + 16);
+        const uint8_t* p = buf + lo;
+        const uint8_t* e = buf + hi;
+        while (p < e) {
+            const void* q = memchr(p, '\n', (size_t)(e - p));
+            if (!q) break;
+            v.push_back((uint64_t)((const uint8_t*)q - buf));
+            p = (const uint8_t*)q + 1;
+        }
+    });
+    size_t tot = 0;
+    for (auto& v : part) tot += v.size();
+    std::vector<uint64_t> out;
+    out.reserve(tot);
+    for (auto& v : part) out.insert(out.end(), v.begin(), v.end());
+    return out;
+}
+
+inline uint64_t strip_cr(const uint8_t* buf, uint64_t s, uint64_t e) {
+    return (e > s && buf[e - 1] == '\r') ? e - 1 : e;
+}
+
+size_t pack_words(uint64_t total_nt, size_t n_reads) {   // == dmx_pack_words (dmx_api.cpp)
+    const uint64_t nt = 2 * kPad + total_nt + (uint64_t)dmx::kPackAlign * n_reads;
+    return (size_t)((nt + 31) / 32 * 2 + 4);
+}
+
+// Lay out and pack b's sequences (seqtext spans) in the device layout.
+void pack_batch(Batch* b, int nth) {
+    const size_t n = b->n_reads;
+    b->offs_v.resize(n);
+    uint64_t g = kPad, total = 0;
+    for (size_t r = 0; r < n; ++r) {
+        b->offs_v[r] = g;
+        g += ((uint64_t)b->lens_v[r] + dmx::kPackAlign - 1) / dmx::kPackAlign * dmx::kPackAlign;
+        total += b->lens_v[r];
+    }
+    b->total_nt = total;
+    const size_t words = pack_words(total, n);
+    b->seq2b_v.assign(words, 0u);
+    b->nmask_v.assign(words, 0u);
+    const uint8_t* st = b->fasta ? b->seqtext_v.data() : b->text_v.data();
+    nth = (int)std::min<size_t>(nth, std::max<size_t>(1, n / 2048));
+    parallel(nth, [&](int t) {
+        const size_t lo = n * t / nth, hi = n * (t + 1) / nth;
+        for (size_t r = lo; r < hi; ++r)
+            dmx::pack_one(st + b->seq_v[2 * r], b->lens_v[r], b->offs_v[r], b->seq2b_v.data(),
+                          b->nmask_v.data());
+    });
+}
+
+// FASTQ records of text[0, cut) whose line ends are nl[0, 4n).
+bool parse_fastq(Batch* b, const std::vector<uint64_t>& nl, size_t n, int nth, std::string& err) {
+    const uint8_t* buf = b->text_v.data();
+    b->head_v.resize(2 * n);
+    b->seq_v.resize(2 * n);
+    b->qual_v.resize(2 * n);
+    b->lens_v.resize(n);
+    std::atomic<int64_t> bad{-1};
+    std::atomic<int> why{0};
+    const int nt = (int)std::min<size_t>(nth, std::max<size_t>(1, n / 4096));
+    parallel(nt, [&](int t) {
+        const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+        for (size_t r = lo; r < hi; ++r) {
+            uint64_t s[4], e[4];
+            for (int k = 0; k < 4; ++k) {
+                const size_t li = 4 * r + k;
+                s[k] = li ? nl[li - 1] + 1 : 0;
+                e[k] = strip_cr(buf, s[k], nl[li]);
+            }
+            int w = 0;
+            if (e[0] == s[0] || buf[s[0]] != '@') w = 1;
+            else if (e[2] == s[2] || buf[s[2]] != '+') w = 2;
+            else if (e[1] - s[1] != e[3] - s[3]) w = 3;
+            if (w) {
+                int64_t cur = bad.load();
+                while ((cur < 0 || (int64_t)r < cur) && !bad.compare_exchange_weak(cur, (int64_t)r)) {}
+                if (bad.load() == (int64_t)r) why = w;
+                continue;
+            }
+            b->head_v[2 * r] = s[0] + 1;
+            b->head_v[2 * r + 1] = e[0];
+            b->seq_v[2 * r] = s[1];
+            b->seq_v[2 * r + 1] = e[1];
+            b->qual_v[2 * r] = s[3];
+            b->qual_v[2 * r + 1] = e[3];
+            b->lens_v[r] = (uint32_t)(e[1] - s[1]);
+        }
+    });
+    if (bad.load() >= 0) {
+        static const char* msg[] = {"", "FASTQ record does not start with '@'",
+                                    "FASTQ record third line does not start with '+'",
+                                    "FASTQ sequence and quality lengths differ"};
+        err = std::string(msg[why.load()]) + " (record " + std::to_string(bad.load() + 1) +
+              " of the batch)";
+        return false;
+    }
+    return true;
+}
+
+inline bool is_space(uint8_t c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
+
+// FASTA records of text[0, cut): starts[] are the '>' positions, nl[] the newlines.
+bool parse_fasta(Batch* b, const std::vector<uint64_t>& starts, const std::vector<uint64_t>& nl,
+                 uint64_t cut, int nth, std::string& err) {
+    const uint8_t* buf = b->text_v.data();
+    const size_t n = starts.size();
+    b->head_v.resize(2 * n);
+    b->seq_v.resize(2 * n);
+    b->lens_v.resize(n);
+    std::vector<uint64_t> slen(n);
+    const int nt = (int)std::min<size_t>(nth, std::max<size_t>(1, n / 1024));
+    // pass 1: header span and sequence length of each record
+    parallel(nt, [&](int t) {
+        const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+        for (size_t r = lo; r < hi; ++r) {
+            const uint64_t s = starts[r];
+            const uint64_t end = r + 1 < n ? starts[r + 1] : cut;
+            auto it = std::lower_bound(nl.begin(), nl.end(), s);
+            const uint64_t he = (it != nl.end() && *it < end) ? *it : end;
+            b->head_v[2 * r] = s + 1;
+            b->head_v[2 * r + 1] = strip_cr(buf, s + 1, he);
+            uint64_t L = 0, p = he + 1;
+            while (p < end) {
+                const uint8_t* q = (const uint8_t*)memchr(buf + p, '\n', (size_t)(end - p));
+                uint64_t le = q ? (uint64_t)(q - buf) : end;
+                uint64_t ls = p, lz = le;
+                while (ls < lz && is_space(buf[ls])) ++ls;
+                while (lz > ls && is_space(buf[lz - 1])) --lz;
+                L += lz - ls;
+                p = le + 1;
+            }
+            slen[r] = L;
+        }
+    });
+    uint64_t tot = 0;
+    for (size_t r = 0; r < n; ++r) {
+        b->seq_v[2 * r] = tot;
+        tot += slen[r];
+        b->seq_v[2 * r + 1] = tot;
+        if (slen[r] >= (1ull << 31)) {
+            err = "FASTA record longer than 2^31 nt";
+            return false;
+        }
+        b->lens_v[r] = (uint32_t)slen[r];
+    }
+    b->seqtext_v.resize(tot + 1);
+    // pass 2: join the sequence lines
+    parallel(nt, [&](int t) {
+        const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+        for (size_t r = lo; r < hi; ++r) {
+            const uint64_t end = r + 1 < n ? starts[r + 1] : cut;
+            uint64_t p = b->head_v[2 * r + 1];
+            while (p < end && buf[p] != '\n') ++p;
+            ++p;
+            uint8_t* dst = b->seqtext_v.data() + b->seq_v[2 * r];
+            while (p < end) {
+                const uint8_t* q = (const uint8_t*)memchr(buf + p, '\n', (size_t)(end - p));
+                uint64_t le = q ? (uint64_t)(q - buf) : end;
+                uint64_t ls = p, lz = le;
+                while (ls < lz && is_space(buf[ls])) ++ls;
+                while (lz > ls && is_space(buf[lz - 1])) --lz;
+                memcpy(dst, buf + ls, lz - ls);
+                dst += lz - ls;
+                p = le + 1;
+            }
+        }
+    });
+    return true;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// reader
+
+struct dmx_reader {
+    std::unique_ptr<Source> src;
+    size_t batch_bytes = 256u << 20;
+    int threads = 1;
+    int format = 0;   // 1 FASTQ, 2 FASTA
+    std::vector<uint8_t> carry;
+    bool src_eof = false;
+
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Batch*> q;
+    bool done = false, stop = false;
+    std::string err;          // producer error (reported in order, after queued batches)
+    std::string api_err;
+
+    void produce();
+    bool next_batch(Batch** out, std::string& e);
+};
+
+bool dmx_reader::next_batch(Batch** out, std::string& e) {
+    *out = nullptr;
+    std::vector<uint8_t> buf;
+    buf.swap(carry);
+    size_t target = std::max<size_t>(batch_bytes, buf.size() + (1u << 20));
+    for (;;) {
+        // fill
+        while (!src_eof && buf.size() < target) {
+            const size_t old = buf.size();
+            const size_t want = std::min<size_t>(target - old, 8u << 20);
+            buf.resize(old + want);
+            const long n = src->read(buf.data() + old, want);
+            if (n < 0) {
+                e = src->err;
+                return false;
+            }
+            buf.resize(old + (size_t)n);
+            if (n == 0) src_eof = true;
+        }
+        if (!format) {
+            size_t p = 0;
+            while (p < buf.size() && (buf[p] == '\n' || buf[p] == '\r' || is_space(buf[p]))) ++p;
+            if (p == buf.size()) {
+                if (src_eof) return true;   // empty input
+                buf.clear();
+                continue;
+            }
+            if (buf[p] == '@') format = 1;
+            else if (buf[p] == '>') format = 2;
+            else {
+                e = "input is neither FASTQ ('@') nor FASTA ('>')";
+                return false;
+            }
+            if (p) buf.erase(buf.begin(), buf.begin() + p);
+        }
+        if (buf.empty()) return true;
+        std::vector<uint64_t> nl = newlines(buf.data(), buf.size(), threads);
+        if (src_eof && buf.back() != '\n') {   // last line without a newline
+            buf.push_back('\n');
+            nl.push_back(buf.size() - 1);
+        }
+        auto* b = new Batch();
+        b->fasta = format == 2;
+        uint64_t cut = 0;
+        if (format == 1) {
+            size_t nrec = nl.size() / 4;
+            if (src_eof && nl.size() % 4) {
+                // tolerate trailing blank lines only
+                const uint64_t s = nrec ? nl[4 * nrec - 1] + 1 : 0;
+                for (uint64_t p = s; p < buf.size(); ++p)
+                    if (!(buf[p] == '\n' || buf[p] == '\r' || is_space(buf[p]))) {
+                        delete b;
+                        e = "truncated FASTQ input (record with fewer than 4 lines)";
+                        return false;
+                    }
+            }
+            if (nrec == 0 && !src_eof) {
+                delete b;
+                target = buf.size() * 2;
+                continue;
+            }
+            cut = nrec ? nl[4 * nrec - 1] + 1 : buf.size();
+            if (src_eof && nl.size() % 4) cut = buf.size();
+            b->n_reads = nrec;
+            carry.assign(buf.begin() + (ptrdiff_t)cut, buf.end());
+            buf.resize(cut);
+            b->text_v.swap(buf);
+            if (!parse_fastq(b, nl, nrec, threads, e)) {
+                delete b;
+                return false;
+            }
+        } else {
+            // record starts: '>' at the start of the buffer or after a newline
+            std::vector<uint64_t> starts;
+            if (buf[0] == '>') starts.push_back(0);
+            for (uint64_t p : nl)
+                if (p + 1 < buf.size() && buf[p + 1] == '>') starts.push_back(p + 1);
+            if (starts.empty() || starts[0] != 0) {
+                delete b;
+                e = "FASTA sequence before the first '>'";
+                return false;
+            }
+            if (!src_eof && starts.size() < 2) {
+                delete b;
+                target = buf.size() * 2;
+                continue;
+            }
+            if (src_eof) {
+                cut = buf.size();
+            } else {
+                cut = starts.back();
+                starts.pop_back();
+            }
+            b->n_reads = starts.size();
+            carry.assign(buf.begin() + (ptrdiff_t)cut, buf.end());
+            buf.resize(cut);
+            b->text_v.swap(buf);
+            nl.erase(std::lower_bound(nl.begin(), nl.end(), cut), nl.end());
+            if (!parse_fasta(b, starts, nl, cut, threads, e)) {
+                delete b;
+                return false;
+            }
+        }
+        if (b->n_reads == 0 && src_eof && carry.empty()) {
+            delete b;
+            return true;
+        }
+        pack_batch(b, threads);
+        b->publish();
+        *out = b;
+        return true;
+    }
+}
+
+void dmx_reader::produce() {
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop || q.size() < 2; });
+            if (stop) return;
+        }
+        Batch* b = nullptr;
+        std::string e;
+        const bool ok = next_batch(&b, e);
+        std::lock_guard<std::mutex> lk(mu);
+        if (!ok) {
+            err = e.empty() ? "read error" : e;
+            done = true;
+        } else if (!b) {
+            done = true;
+        } else {
+            q.push_back(b);
+        }
+        cv.notify_all();
+        if (done) return;
+    }
+}
+
+extern "C" {
+
+int dmx_io_abi_version(void) { return DMX_IO_ABI_VERSION; }
+
+int dmx_reader_open(const char* path, size_t batch_bytes, int threads, dmx_reader** out) {
+    if (!path || !out) return -1;
+    *out = nullptr;
+    auto fd = std::make_unique<FdSource>();
+    if (!strcmp(path, "-")) {
+        fd->fd = 0;
+    } else {
+        fd->fd = ::open(path, O_RDONLY);
+        fd->own = true;
+        if (fd->fd < 0) return -2;
+    }
+    // sniff gzip magic
+    auto pre = std::make_unique<PrefixSource>();
+    pre->head.resize(2);
+    const long n = fd->read(pre->head.data(), 2);
+    if (n < 0) return -2;
+    pre->head.resize((size_t)n);
+    const bool gz = n == 2 && pre->head[0] == 0x1f && pre->head[1] == 0x8b;
+    pre->inner = std::move(fd);
+    auto* r = new dmx_reader();
+    if (gz) r->src = std::make_unique<GzSource>(std::move(pre));
+    else r->src = std::move(pre);
+    r->batch_bytes = std::max<size_t>(batch_bytes, 1u << 16);
+    r->threads = clamp_threads(threads);
+    r->th = std::thread([r] { r->produce(); });
+    *out = r;
+    return 0;
+}
+
+int dmx_reader_next(dmx_reader* r, dmx_batch** out) {
+    if (!r || !out) return -1;
+    *out = nullptr;
+    std::unique_lock<std::mutex> lk(r->mu);
+    r->cv.wait(lk, [&] { return !r->q.empty() || r->done; });
+    if (!r->q.empty()) {
+        *out = r->q.front();
+        r->q.pop_front();
+        r->cv.notify_all();
+        return 0;
+    }
+    if (!r->err.empty()) {
+        r->api_err = r->err;
+        return -3;
+    }
+    return 0;
+}
+
+const char* dmx_reader_error(dmx_reader* r) { return r ? r->api_err.c_str() : "null reader"; }
+
+void dmx_reader_close(dmx_reader* r) {
+    if (!r) return;
+    {
+        std::lock_guard<std::mutex> lk(r->mu);
+        r->stop = true;
+        r->cv.notify_all();
+    }
+    if (r->th.joinable()) r->th.join();
+    for (Batch* b : r->q) release(b);
+    delete r;
+}
+
+void dmx_batch_free(dmx_batch* b) { release(static_cast<Batch*>(b)); }
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// sink
+
+namespace {
+
+struct Comp {
+    uint8_t t[256];
+    Comp() {
+        for (int i = 0; i < 256; ++i) t[i] = (uint8_t)i;
+        const char* a = "ACGTUMRWSYKVHDBNacgtumrwsykvhdbn";
+        const char* b = "TGCAAKYWSRMBDHVNtgcaakywsrmbdhvn";
+        for (int i = 0; a[i]; ++i) t[(uint8_t)a[i]] = (uint8_t)b[i];
+    }
+};
+const Comp kComp;
+
+struct Out {
+    std::string path;
+    FILE* fp = nullptr;
+    bool gz = false;
+    bool any = false;
+    uint64_t n = 0, bp = 0;
+};
+
+struct Job {
+    Batch* b = nullptr;
+    std::vector<int32_t> idx, start, stop;
+    std::vector<uint8_t> rc, nrc;
+};
+
+bool gzip_member(const uint8_t* src, size_t n, int level, std::vector<uint8_t>& out) {
+    z_stream zs{};
+    if (deflateInit2(&zs, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+    out.resize(deflateBound(&zs, (uLong)n) + 64);
+    zs.next_in = const_cast<uint8_t*>(src);
+    zs.avail_in = (uInt)n;
+    zs.next_out = out.data();
+    zs.avail_out = (uInt)out.size();
+    const int ret = deflate(&zs, Z_FINISH);
+    out.resize(out.size() - zs.avail_out);
+    deflateEnd(&zs);
+    return ret == Z_STREAM_END;
+}
+
+}  // namespace
+
+struct dmx_sink {
+    std::vector<Out> outs;
+    bool fasta_out = false;
+    int level = 1;
+    int threads = 1;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::unique_ptr<Job> pending;
+    bool busy = false, stop = false, closed = false;
+    std::string err, api_err;
+
+    void worker();
+    bool process(Job& j, std::string& e);
+};
+
+bool dmx_sink::process(Job& j, std::string& e) {
+    Batch* b = j.b;
+    const size_t n = b->n_reads;
+    const int nout = (int)outs.size();
+    const int nth = (int)std::min<size_t>(threads, std::max<size_t>(1, n / 1024));
+    const bool fq = !fasta_out && !b->fasta;
+    // pass 1: bytes per (thread, output)
+    std::vector<std::vector<uint64_t>> sz(nth, std::vector<uint64_t>(nout, 0));
+    std::vector<std::vector<uint64_t>> cnt(nth, std::vector<uint64_t>(nout, 0));
+    std::vector<std::vector<uint64_t>> bps(nth, std::vector<uint64_t>(nout, 0));
+    std::atomic<bool> range_bad{false};
+    parallel(nth, [&](int t) {
+        const size_t lo = n * t / nth, hi = n * (t + 1) / nth;
+        for (size_t r = lo; r < hi; ++r) {
+            const int o = j.idx[r];
+            if (o < 0) continue;
+            if (o >= nout || j.start[r] < 0 || j.stop[r] < j.start[r] ||
+                (uint32_t)j.stop[r] > b->lens_v[r]) {
+                range_bad = true;
+                continue;
+            }
+            const uint64_t L = (uint64_t)(j.stop[r] - j.start[r]);
+            const uint64_t h = b->head_v[2 * r + 1] - b->head_v[2 * r] + 3ull * j.nrc[r];
+            sz[t][o] += 1 + h + 1 + L + 1 + (fq ? 2 + L + 1 : 0);
+            cnt[t][o] += 1;
+            bps[t][o] += L;
+        }
+    });
+    if (range_bad) {
+        e = "dmx_sink_write: output index or trim coordinates out of range";
+        return false;
+    }
+    std::vector<std::vector<std::vector<uint8_t>>> buf(nth, std::vector<std::vector<uint8_t>>(nout));
+    // pass 2: render
+    parallel(nth, [&](int t) {
+        std::vector<uint8_t*> w(nout, nullptr);
+        for (int o = 0; o < nout; ++o) {
+            buf[t][o].resize(sz[t][o]);
+            w[o] = buf[t][o].data();
+        }
+        const size_t lo = n * t / nth, hi = n * (t + 1) / nth;
+        const uint8_t* tx = b->text_v.data();
+        const uint8_t* st = b->fasta ? b->seqtext_v.data() : tx;
+        for (size_t r = lo; r < hi; ++r) {
+            const int o = j.idx[r];
+            if (o < 0) continue;
+            uint8_t* p = w[o];
+            *p++ = fq ? '@' : '>';
+            const uint64_t hs = b->head_v[2 * r], he = b->head_v[2 * r + 1];
+            memcpy(p, tx + hs, he - hs);
+            p += he - hs;
+            for (int k = 0; k < j.nrc[r]; ++k) {
+                memcpy(p, " rc", 3);
+                p += 3;
+            }
+            *p++ = '\n';
+            const uint32_t a = (uint32_t)j.start[r], z = (uint32_t)j.stop[r];
+            const uint8_t* s = st + b->seq_v[2 * r];
+            const uint32_t len = b->lens_v[r];
+            if (!j.rc[r]) {
+                memcpy(p, s + a, z - a);
+                p += z - a;
+            } else {   // orient = reverse complement: out[k] = comp(s[len-1-k])
+                for (uint32_t k = a; k < z; ++k) *p++ = kComp.t[s[len - 1 - k]];
+            }
+            *p++ = '\n';
+            if (fq) {
+                *p++ = '+';
+                *p++ = '\n';
+                const uint8_t* q = tx + b->qual_v[2 * r];
+                if (!j.rc[r]) {
+                    memcpy(p, q + a, z - a);
+                    p += z - a;
+                } else {
+                    for (uint32_t k = a; k < z; ++k) *p++ = q[len - 1 - k];
+                }
+                *p++ = '\n';
+            }
+            w[o] = p;
+        }
+    });
+    // pass 3: compress (independent gzip members), largest buffers first
+    std::vector<std::vector<std::vector<uint8_t>>> mem(nth, std::vector<std::vector<uint8_t>>(nout));
+    bool any_gz = false;
+    for (auto& o : outs) any_gz |= o.gz;
+    if (any_gz) {
+        std::vector<std::pair<int, int>> jobs;
+        for (int t = 0; t < nth; ++t)
+            for (int o = 0; o < nout; ++o)
+                if (outs[o].gz && !buf[t][o].empty()) jobs.emplace_back(t, o);
+        std::sort(jobs.begin(), jobs.end(), [&](auto& x, auto& y) {
+            return buf[x.first][x.second].size() > buf[y.first][y.second].size();
+        });
+        std::atomic<size_t> next{0};
+        std::atomic<bool> bad{false};
+        const int nc = (int)std::min<size_t>(threads, std::max<size_t>(1, jobs.size()));
+        parallel(nc, [&](int) {
+            for (size_t k; (k = next.fetch_add(1)) < jobs.size();) {
+                auto [t, o] = jobs[k];
+                if (!gzip_member(buf[t][o].data(), buf[t][o].size(), level, mem[t][o])) bad = true;
+                std::vector<uint8_t>().swap(buf[t][o]);
+            }
+        });
+        if (bad) {
+            e = "gzip compression failed";
+            return false;
+        }
+    }
+    // pass 4: write in input order
+    for (int o = 0; o < nout; ++o) {
+        Out& f = outs[o];
+        for (int t = 0; t < nth; ++t) {
+            const auto& v = f.gz ? mem[t][o] : buf[t][o];
+            if (!v.empty() && fwrite(v.data(), 1, v.size(), f.fp) != v.size()) {
+                e = "write failed: " + f.path + ": " + strerror(errno);
+                return false;
+            }
+            if (!v.empty()) f.any = true;
+            f.n += cnt[t][o];
+            f.bp += bps[t][o];
+        }
+    }
+    return true;
+}
+
+void dmx_sink::worker() {
+    for (;;) {
+        std::unique_ptr<Job> j;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop || pending; });
+            if (!pending) return;
+            j = std::move(pending);
+        }
+        std::string e;
+        const bool ok = err.empty() ? process(*j, e) : true;
+        release(j->b);
+        std::lock_guard<std::mutex> lk(mu);
+        if (!ok && err.empty()) err = e;
+        busy = false;
+        cv.notify_all();
+    }
+}
+
+extern "C" {
+
+int dmx_sink_open(const char* const* paths, int n_out, int fasta_out, int level, int threads,
+                  dmx_sink** out) {
+    if (!paths || n_out <= 0 || !out) return -1;
+    *out = nullptr;
+    auto* s = new dmx_sink();
+    s->fasta_out = fasta_out != 0;
+    s->level = std::max(0, std::min(9, level));
+    s->threads = clamp_threads(threads);
+    s->outs.resize(n_out);
+    for (int o = 0; o < n_out; ++o) {
+        Out& f = s->outs[o];
+        f.path = paths[o] ? paths[o] : "";
+        f.gz = f.path.size() > 3 && f.path.compare(f.path.size() - 3, 3, ".gz") == 0;
+        f.fp = f.path == "-" ? stdout : fopen(f.path.c_str(), "wb");
+        if (!f.fp) {
+            s->api_err = "cannot open " + f.path + ": " + strerror(errno);
+            for (int k = 0; k < o; ++k)
+                if (s->outs[k].fp && s->outs[k].fp != stdout) fclose(s->outs[k].fp);
+            for (auto& g : s->outs) g.fp = nullptr;
+            *out = s;   // caller reads the message, then frees
+            return -2;
+        }
+        setvbuf(f.fp, nullptr, _IOFBF, 1 << 20);
+    }
+    s->th = std::thread([s] { s->worker(); });
+    *out = s;
+    return 0;
+}
+
+int dmx_sink_write(dmx_sink* s, dmx_batch* bp, const int32_t* out_idx, const int32_t* start,
+                   const int32_t* stop, const uint8_t* rc, const uint8_t* n_rc) {
+    if (!s || !bp || s->closed || !s->th.joinable()) return -1;
+    Batch* b = static_cast<Batch*>(bp);
+    const size_t n = b->n_reads;
+    if (n && (!out_idx || !start || !stop || !rc || !n_rc)) return -1;
+    auto j = std::make_unique<Job>();
+    j->idx.assign(out_idx, out_idx + n);
+    j->start.assign(start, start + n);
+    j->stop.assign(stop, stop + n);
+    j->rc.assign(rc, rc + n);
+    j->nrc.assign(n_rc, n_rc + n);
+    std::unique_lock<std::mutex> lk(s->mu);
+    s->cv.wait(lk, [&] { return !s->busy; });
+    if (!s->err.empty()) {
+        s->api_err = s->err;
+        return -3;
+    }
+    b->refs.fetch_add(1);
+    j->b = b;
+    s->pending = std::move(j);
+    s->busy = true;
+    s->cv.notify_all();
+    return 0;
+}
+
+int dmx_sink_close(dmx_sink* s, uint64_t* n_written, uint64_t* bp_written) {
+    if (!s) return -1;
+    if (s->th.joinable()) {
+        {
+            std::unique_lock<std::mutex> lk(s->mu);
+            s->cv.wait(lk, [&] { return !s->busy; });
+            s->stop = true;
+            s->cv.notify_all();
+        }
+        s->th.join();
+    }
+    int rc = 0;
+    if (!s->err.empty()) {
+        s->api_err = s->err;
+        rc = -3;
+    }
+    for (size_t o = 0; o < s->outs.size(); ++o) {
+        Out& f = s->outs[o];
+        if (!f.fp) continue;
+        if (f.gz && !f.any) {   // empty output: still a valid gzip file
+            std::vector<uint8_t> m;
+            if (!gzip_member(nullptr, 0, s->level, m) || fwrite(m.data(), 1, m.size(), f.fp) != m.size()) {
+                s->api_err = "write failed: " + f.path;
+                rc = -3;
+            }
+        }
+        if (f.fp == stdout ? fflush(f.fp) != 0 : fclose(f.fp) != 0) {
+            s->api_err = "close failed: " + f.path + ": " + strerror(errno);
+            rc = -3;
+        }
+        f.fp = nullptr;
+        if (n_written) n_written[o] = f.n;
+        if (bp_written) bp_written[o] = f.bp;
+    }
+    s->closed = true;
+    return rc;
+}
+
+const char* dmx_sink_error(dmx_sink* s) { return s ? s->api_err.c_str() : "null sink"; }
+
+void dmx_sink_free(dmx_sink* s) {
+    if (!s) return;
+    if (!s->closed) dmx_sink_close(s, nullptr, nullptr);
+    delete s;
+}
+
+}  // extern "C"

@@ -22,7 +22,7 @@ import time
 import numpy as np
 
 from . import __version__
-from . import fastx, lib, panel
+from . import fastx, lib, nio, panel
 from .report import Stats
 
 
@@ -45,7 +45,7 @@ def build_parser():
     p.add_argument("-b", "--anywhere", dest="anywhere", action="append")
     p.add_argument("-e", "--error-rate", "--errors", dest="error_rate", type=float, default=0.1)
     p.add_argument("-O", "--overlap", type=int, default=3)
-    p.add_argument("-j", "--cores", type=int, default=1)
+    p.add_argument("-j", "--cores", type=int, default=1)   # host I/O threads (0 = all)
     p.add_argument("--rc", "--revcomp", dest="rc", action="store_true")
     p.add_argument("--action", default="trim")
     p.add_argument("-o", "--output")
@@ -61,7 +61,7 @@ def build_parser():
     p.add_argument("-N", "--no-match-adapter-wildcards", dest="no_adapter_wildcards",
                    action="store_true")
     p.add_argument("--match-read-wildcards", action="store_true")
-    p.add_argument("--device", type=int, default=int(os.environ.get("DMX_DEVICE", "0")))
+    p.add_argument("--device", type=int, default=None)
     p.add_argument("--batch-mb", type=int, default=256)
     p.add_argument("input")
     return p
@@ -94,130 +94,146 @@ def run(argv=None) -> int:
         _unsupported("mixing linked and single adapters in one call is not implemented")
     if linked and args.rc:
         _unsupported("--rc with linked adapters is not implemented")
-    level = 1 if args.zlevel1 else args.compression_level
 
-    ctx = lib.Context(args.device)
-    if linked:
-        ctx.set_panel(0, [a.front for a in ads], lib.DMX_FRONT, args.error_rate, args.overlap)
-        ctx.set_panel(1, [a.back for a in ads], lib.DMX_BACK, args.error_rate, args.overlap)
-        ctx.set_mode(lib.MODE_LINKED)
-    else:
-        wheres = [lib.DMX_FRONT if a.where == "front" else lib.DMX_BACK for a in ads]
-        if len(set(wheres)) == 1:
-            ctx.set_panel(0, [a.seq for a in ads], wheres[0] | (lib.DMX_RC if args.rc else 0),
-                          args.error_rate, args.overlap)
-        else:
-            ctx.set_panel_mixed(0, [a.seq for a in ads], wheres, args.rc, args.error_rate,
-                                args.overlap)
-        ctx.set_mode(lib.MODE_SINGLE)
+    devices = _devices(args)
+    ctxs = [lib.Context(d) for d in devices]
+    for ctx in ctxs:
+        _configure(ctx, ads, linked, args)
+    level = 1 if args.zlevel1 else args.compression_level
 
     demux = "{name}" in args.output
     fasta_out = fastx.is_fasta_path(args.output.replace("{name}", "x"))
-    writers: dict[str, fastx.Writer] = {}
-
-    def writer(key: str, path: str) -> fastx.Writer:
-        w = writers.get(key)
-        if w is None:
-            w = writers[key] = fastx.Writer(path, fasta_out, level)
-        return w
-
     names = [a.name for a in ads]
     if demux:   # cutadapt creates every demultiplexed output, also when it stays empty
-        for nm in names + ["unknown"]:
-            writer(nm, args.output.replace("{name}", nm))
+        paths = [args.output.replace("{name}", nm) for nm in names]
+        if not args.discard_untrimmed:
+            paths.append(args.output.replace("{name}", "unknown"))
+        unmatched_to = -1 if args.discard_untrimmed else len(names)
     else:
-        writer("__main__", args.output)
-        if args.untrimmed_output:
-            writer("__untrimmed__", args.untrimmed_output)
+        paths = [args.output] + ([args.untrimmed_output] if args.untrimmed_output else [])
+        unmatched_to = 1 if args.untrimmed_output else (-1 if args.discard_untrimmed else 0)
 
     stats = Stats(ads)
+    stats.rc_mode = bool(args.rc)
     t0 = time.perf_counter()
-    for batch in fastx.read_batches(args.input, args.batch_mb << 20):
-        n = len(batch)
-        if n == 0:
-            continue
-        blob, offs, lens = batch.seq_offsets()
-        res = ctx.run(lib.pack(blob, offs, lens))
-        _emit(batch, res, ads, linked, demux, args, writer, stats, fasta_out, lens)
-    for w in writers.values():
-        w.close()
+    sink = nio.Sink(paths, fasta_out, level, threads=args.cores)
+    try:
+        with nio.Reader(args.input, args.batch_mb << 20, threads=args.cores) as reader:
+            for batch in reader:
+                try:
+                    if len(batch):
+                        if len(ctxs) == 1:
+                            res = ctxs[0].run(batch.packed)
+                        else:
+                            res, _ = lib.run_multi(ctxs, batch.packed)
+                        plan = _plan(res, ads, linked, demux, unmatched_to, batch.lens, stats)
+                        sink.write(batch, *plan)
+                finally:
+                    batch.free()
+    finally:
+        sink.close()
+    stats.n_out = int(sink.n_written.sum())
+    stats.bp_out = int(sink.bp_written.sum())
     if args.json:
         stats.write_json(args.json, argv=argv, cores=args.cores, in_path=args.input,
                          error_rate=args.error_rate)
     if not args.quiet:
         print(f"This is dmx {__version__} (cutadapt 4.9-compatible demultiplexer on MI355X)")
         print(f"Command line parameters: {' '.join(argv)}")
-        print(f"Finished in {time.perf_counter() - t0:.3f} s\n")
+        print(f"Finished in {time.perf_counter() - t0:.3f} s on {len(ctxs)} GPU(s)\n")
         stats.summary()
-    ctx.close()
+    for ctx in ctxs:
+        ctx.close()
     return 0
 
 
-def _emit(batch, res, ads, linked, demux, args, writer, stats, fasta_out, lens):
-    n = len(batch)
+def _devices(args) -> list:
+    """GPUs for this call: DMX_GPUS ("all", a count, or a comma list) shards every batch over
+    several devices (-j is host I/O threads, the GPU count comes from the
+    environment).  An explicit --device / DMX_DEVICE pins one GPU; the default is every
+    visible GPU."""
+    spec = os.environ.get("DMX_GPUS", "").strip()
+    if not spec:
+        if args.device is not None:
+            return [args.device]
+        if os.environ.get("DMX_DEVICE", "").strip():
+            return [int(os.environ["DMX_DEVICE"])]
+        spec = "all"
+    if spec == "all":
+        n = lib.device_count()
+        if n <= 0:
+            raise lib.DmxError("DMX_GPUS=all but no HIP device is visible")
+        return list(range(n))
+    if "," in spec:
+        return [int(x) for x in spec.split(",") if x.strip()]
+    n = int(spec)
+    if n <= 0:
+        raise lib.DmxError("DMX_GPUS must be positive")
+    return list(range(n))
+
+
+def _configure(ctx, ads, linked, args):
+    if linked:
+        ctx.set_panel(0, [a.front for a in ads], lib.DMX_FRONT, args.error_rate, args.overlap)
+        ctx.set_panel(1, [a.back for a in ads], lib.DMX_BACK, args.error_rate, args.overlap)
+        ctx.set_mode(lib.MODE_LINKED)
+        return
+    wheres = [lib.DMX_FRONT if a.where == "front" else lib.DMX_BACK for a in ads]
+    if len(set(wheres)) == 1:
+        ctx.set_panel(0, [a.seq for a in ads], wheres[0] | (lib.DMX_RC if args.rc else 0),
+                      args.error_rate, args.overlap)
+    else:
+        ctx.set_panel_mixed(0, [a.seq for a in ads], wheres, args.rc, args.error_rate,
+                            args.overlap)
+    ctx.set_mode(lib.MODE_SINGLE)
+
+
+def _plan(res, ads, linked, demux, unmatched_to, lens, stats):
+    """Per-read output index, trim coordinates and orientation (vectorised), and statistics.
+
+    -g (FRONT): RemoveBeforeMatch keeps seq[rstop:]; -a (BACK): RemoveAfterMatch keeps
+    seq[:rstart]; linked: read[front.rstop:][:back.rstart]; coordinates of RC hits are on the
+    reverse complement, which the sink renders (with " rc" appended to the name)."""
+    n = len(res)
     lens = lens.astype(np.int64)
     bin1 = res["bin1"].astype(np.int64)
     matched = bin1 >= 0
+    m1_rstart = res["m1_rstart"].astype(np.int64)
+    m1_rstop = res["m1_rstop"].astype(np.int64)
     if linked:
-        # front part on the read, back part on read[front.rstop:] (LinkedAdapter.match_to)
-        start = np.where(matched, res["m1_rstop"], 0).astype(np.int64)
-        stop = np.where(matched, start + res["m2_rstart"], lens)
+        start = np.where(matched, m1_rstop, 0)
+        stop = np.where(matched, start + res["m2_rstart"].astype(np.int64), lens)
         rc = np.zeros(n, dtype=bool)
     else:
         is_front = np.array([a.where == "front" for a in ads] + [False])[bin1]
         rc = (res["rc1"] == 1) & matched
-        start = np.where(matched & is_front, res["m1_rstop"], 0).astype(np.int64)
-        stop = np.where(matched & ~is_front, res["m1_rstart"], lens).astype(np.int64)
+        start = np.where(matched & is_front, m1_rstop, 0)
+        stop = np.where(matched & ~is_front, m1_rstart, lens)
+    if demux:
+        out_idx = np.where(matched, bin1, unmatched_to)
+    else:
+        out_idx = np.where(matched, 0, unmatched_to)
+
     stats.n_in += n
     stats.bp_in += int(lens.sum())
     stats.n_with_adapter += int(matched.sum())
     stats.n_rc += int(rc.sum())
-    for a in np.unique(bin1[matched]):
-        sel = bin1 == a
-        stats.matches[int(a)] += int(sel.sum())
-        if args.rc:
-            stats.on_rc[int(a)] += int((sel & rc).sum())
-    for i in np.flatnonzero(matched):
-        a = int(bin1[i])
-        if linked:
-            stats.add_match(a, False, "front", int(res["m1_rstop"][i]), int(res["m1_errors"][i]))
-            blen = int(lens[i] - res["m1_rstop"][i])
-            stats.add_match(a, False, "back", blen - int(res["m2_rstart"][i]),
-                            int(res["m2_errors"][i]))
-        elif ads[a].where == "front":
-            stats.add_match(a, bool(rc[i]), "front", int(res["m1_rstop"][i]),
-                            int(res["m1_errors"][i]))
-        else:
-            stats.add_match(a, bool(rc[i]), "back", int(lens[i] - res["m1_rstart"][i]),
-                            int(res["m1_errors"][i]))
-
-    groups: dict[str, list] = {}
-    out_bp = 0
-    out_n = 0
-    for i in range(n):
-        if matched[i]:
-            key = ads[int(bin1[i])].name if demux else "__main__"
-            rec = fastx.render(batch, i, int(start[i]), int(stop[i]), bool(rc[i]),
-                               b" rc" if rc[i] else b"", fasta_out)
-            out_bp += int(stop[i] - start[i])
-        else:
-            if demux:
-                key = "unknown"
-            elif args.untrimmed_output:
-                key = "__untrimmed__"
-            elif args.discard_untrimmed:
-                stats.n_discard_untrimmed += 1
-                continue
-            else:
-                key = "__main__"
-            rec = fastx.render(batch, i, 0, int(lens[i]), False, b"", fasta_out)
-            out_bp += int(lens[i])
-        out_n += 1
-        groups.setdefault(key, []).append(rec)
-    stats.n_out += out_n
-    stats.bp_out += out_bp
-    for key, recs in groups.items():
-        writer(key, "").write_chunks(recs)
+    if not matched.all() and unmatched_to < 0:
+        stats.n_discard_untrimmed += int((~matched).sum())
+    bm = bin1[matched]
+    stats.add_counts(bm, rc[matched], len(ads))
+    e1 = res["m1_errors"].astype(np.int64)[matched]
+    if linked:
+        stats.add_matches(bm, "front", m1_rstop[matched], e1)
+        blen = (lens - m1_rstop)[matched]
+        stats.add_matches(bm, "back", blen - res["m2_rstart"].astype(np.int64)[matched],
+                          res["m2_errors"].astype(np.int64)[matched])
+    else:
+        fr = is_front[matched]
+        stats.add_matches(bm[fr], "front", m1_rstop[matched][fr], e1[fr])
+        stats.add_matches(bm[~fr], "back", (lens - m1_rstart)[matched][~fr], e1[~fr])
+    rc8 = rc.astype(np.uint8)
+    return out_idx.astype(np.int32), start.astype(np.int32), stop.astype(np.int32), rc8, rc8
 
 
 def main():

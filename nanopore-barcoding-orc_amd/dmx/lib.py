@@ -27,7 +27,8 @@ assert RESULT_DTYPE.itemsize == 40
 
 EXPORTS = ["dmx_abi_version", "dmx_open", "dmx_close", "dmx_last_error", "dmx_set_panel",
            "dmx_set_panel_mixed", "dmx_set_mode", "dmx_pack_words", "dmx_pack", "dmx_run", "dmx_load", "dmx_exec",
-           "dmx_sync", "dmx_fetch", "dmx_counts", "dmx_stats"]
+           "dmx_sync", "dmx_fetch", "dmx_counts", "dmx_stats", "dmx_device_count",
+           "dmx_run_multi"]
 
 
 class DmxError(RuntimeError):
@@ -70,7 +71,9 @@ def load() -> ctypes.CDLL:
     L.dmx_counts.argtypes = [P, c_u64p, c_size]
     L.dmx_stats.argtypes = [P, ctypes.POINTER(ctypes.c_float), c_int, c_u64p, c_int,
                             ctypes.POINTER(c_int)]
-    if L.dmx_abi_version() != 2:
+    L.dmx_device_count.restype = c_int
+    L.dmx_run_multi.argtypes = [ctypes.POINTER(P), c_int, P, P, c_u64p, P, c_size, c_size, P, c_u64p, c_size]
+    if L.dmx_abi_version() != 3:
         raise DmxError("libdmx ABI mismatch")
     _lib = L
     return L
@@ -212,3 +215,25 @@ class Context:
                 "windows": cl[2:4].tolist(), "resolved": cl[4:6].tolist(),
                 "traces": cl[6:8].tolist(), "windows_raw": cl[8:10].tolist(),
                 "flags": fl.value}
+
+
+def device_count() -> int:
+    """Visible HIP devices (0 without a GPU)."""
+    return int(load().dmx_device_count())
+
+
+def run_multi(ctxs, p: Packed):
+    """Shard one packed batch over several contexts (one per GPU); returns (results, counts)."""
+    L = load()
+    if not ctxs:
+        raise DmxError("run_multi needs at least one context")
+    out = np.zeros(p.n_reads, dtype=RESULT_DTYPE)
+    counts = np.zeros(ctxs[0].n_counts(), dtype=np.uint64)
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    rc = L.dmx_run_multi(arr, len(ctxs), p.seq2b.ctypes.data, p.nmask.ctypes.data,
+                         p.offsets.ctypes.data, p.lengths.ctypes.data, p.n_words, p.n_reads,
+                         out.ctypes.data, counts.ctypes.data, len(counts))
+    if rc < 0:
+        msg = L.dmx_last_error(ctxs[0]._h)
+        raise DmxError(f"dmx_run_multi failed ({rc}): {msg.decode() if msg else ''}")
+    return out, counts

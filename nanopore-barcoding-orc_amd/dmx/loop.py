@@ -1,0 +1,235 @@
+"""Fused replacement for scripts/02_cutadapt_loop.sh: both demultiplexing rounds in one pass.
+
+The reference runs cutadapt 13 times per sample (round 1 `-g file:SP5 --rc` at :64-72, then one
+`-a file:SP27rc --rc` call per SP5 bin at :91-103), re-reading and re-compressing every read,
+and then deletes the `unknown` and SP27_009..012 outputs (:107-119).  This driver reads the
+input once, runs DMX_MODE_TWO_ROUND on the GPU(s) (round 2 on the round-1-trimmed, oriented
+view of every read, no host round trip) and writes the files the script leaves behind:
+
+  demuxed/SP5/{SP5_i}_{dataset}.fastq.gz            round-1 output per SP5 bin (:70)
+  demuxed/SP5/cutadapt_SP5_{dataset}.json           round-1 report (:72)
+  demuxed/SP27/{SP27_j}_{SP5_i}_{dataset}.fastq.gz  round-2 output, j <= 8 (:100, :114-118)
+  demuxed/SP27/{SP5_i}_{dataset}.json               round-2 report per SP5 bin (:102)
+
+with the same record content and order as the 13 cutadapt calls (tests/test_cli_gpu.py checks
+it against the per-call CLI and the oracle).  `--no-cleanup` also writes the `unknown` and
+SP27_009..012 files the script deletes.  Options mirror the script's variables (e_rate,
+threads, adapter FASTAs); GPUs as in the CLI (DMX_GPUS / DMX_DEVICE, default all visible).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+from . import __version__, lib, nio, panel
+from .cli import _devices
+from .report import Stats
+
+INVALID_SP27 = ("SP27_009", "SP27_010", "SP27_011", "SP27_012")   # 02_cutadapt_loop.sh:114-118
+
+
+def dataset_name(infile: str) -> str:
+    """02_cutadapt_loop.sh:26-35."""
+    ds = os.path.basename(infile)
+    if ds.startswith("pychopped_"):
+        ds = ds[len("pychopped_"):]
+    for suf in (".fastq.gz", ".fastq", ".fq.gz", ".fq", ".gz", "_pass"):
+        if ds.endswith(suf):
+            ds = ds[:-len(suf)]
+    return ds
+
+
+def build_parser():
+    p = argparse.ArgumentParser(prog="dmx-demux-loop",
+                                description="fused scripts/02_cutadapt_loop.sh on MI355X")
+    p.add_argument("infile")
+    p.add_argument("-e", "--e-rate", type=float, default=0.1)
+    p.add_argument("-j", "--threads", type=int, default=24)
+    p.add_argument("--sp5", default=panel.SP5_FASTA, help="adapters_SP5 FASTA (:43)")
+    p.add_argument("--sp27", default=panel.SP27RC_FASTA, help="adapters_SP27 FASTA (:44)")
+    p.add_argument("--outdir", default=None, help="default: $(dirname $(dirname IN))/demuxed")
+    p.add_argument("--no-cleanup", action="store_true",
+                   help="keep the unknown and SP27_009..012 outputs (:107-119 delete them)")
+    p.add_argument("--compression-level", type=int, default=1)
+    p.add_argument("--batch-mb", type=int, default=256)
+    p.add_argument("--device", type=int, default=None)
+    return p
+
+
+def plan_rounds(res, lens):
+    """Composite trim coordinates of both rounds on the original read.
+
+    Round 1 (FRONT, --rc): T1 = orient(read, rc1)[s1:] with s1 = m1.rstop.  Round 2 (BACK, --rc)
+    on T1: keep orient(T1, rc2)[:r2] with r2 = m2.rstart.  With revcomp(orient(x, o)[a:b]) =
+    orient(x, !o)[n-b:n-a] the round-2 output is orient(read, rc1)[s1 : s1 + r2] if rc2 == 0
+    and orient(read, !rc1)[0 : r2] if rc2 == 1; its name carries one " rc" per RC'd round."""
+    lens = lens.astype(np.int64)
+    rc1 = res["rc1"].astype(np.uint8)
+    rc2 = res["rc2"].astype(np.uint8)
+    s1 = res["m1_rstop"].astype(np.int64)
+    r2 = res["m2_rstart"].astype(np.int64)
+    start2 = np.where(rc2 == 1, 0, s1)
+    stop2 = np.where(rc2 == 1, r2, s1 + r2)
+    orient2 = (rc1 ^ rc2).astype(np.uint8)
+    return (s1, lens, rc1), (start2, stop2, orient2, (rc1 + rc2).astype(np.uint8))
+
+
+def run(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = build_parser().parse_args(argv)
+    infile = args.infile
+    ds = dataset_name(infile)
+    outdir = args.outdir or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(infile))),
+                                         "demuxed")
+    print("=========================================")
+    print(f"Processing: {infile}")
+    print(f"Dataset name: {ds}")
+    print(f"Output directory: {outdir}")
+    print("=========================================")
+    for f in (infile, args.sp5, args.sp27):
+        if not os.path.isfile(f):
+            print(f"Error: Required file not found: {f}")
+            return 1
+    os.makedirs(os.path.join(outdir, "SP5"), exist_ok=True)
+    os.makedirs(os.path.join(outdir, "SP27"), exist_ok=True)
+    aset1, aset2 = panel.AdapterSet(), panel.AdapterSet()
+    aset1.add_spec(f"file:{args.sp5}", "front")
+    aset2.add_spec(f"file:{args.sp27}", "back")
+    ads1, ads2 = aset1.adapters, aset2.adapters
+    n1, n2 = [a.name for a in ads1], [a.name for a in ads2]
+
+    ctxs = [lib.Context(d) for d in _devices(args)]
+    for ctx in ctxs:
+        ctx.set_panel(0, [a.seq for a in ads1], lib.DMX_FRONT | lib.DMX_RC, args.e_rate, 3)
+        ctx.set_panel(1, [a.seq for a in ads2], lib.DMX_BACK | lib.DMX_RC, args.e_rate, 3)
+        ctx.set_mode(lib.MODE_TWO_ROUND)
+
+    # outputs: round 1 = one file per SP5 adapter (+ unknown); round 2 = per (SP5, SP27) pair
+    keep2 = [j for j, nm in enumerate(n2) if args.no_cleanup or nm not in INVALID_SP27]
+    p1 = [f"{outdir}/SP5/{nm}_{ds}.fastq.gz" for nm in n1]
+    if args.no_cleanup:
+        p1.append(f"{outdir}/SP5/unknown_{ds}.fastq.gz")
+    out2 = np.full((len(n1), len(n2) + 1), -1, dtype=np.int32)   # [bin1, bin2 + 1] -> output
+    p2 = []
+    for i, ident in enumerate(n1):
+        if args.no_cleanup:
+            out2[i, 0] = len(p2)
+            p2.append(f"{outdir}/SP27/unknown_{ident}_{ds}.fastq.gz")
+        for j in keep2:
+            out2[i, j + 1] = len(p2)
+            p2.append(f"{outdir}/SP27/{n2[j]}_{ident}_{ds}.fastq.gz")
+
+    st1 = Stats(ads1)
+    st1.rc_mode = True
+    st2 = []
+    for _ in n1:
+        s = Stats(ads2)
+        s.rc_mode = True
+        st2.append(s)
+    t0 = time.perf_counter()
+    print("Round 1: Demultiplexing with SP5 adapters...")
+    print("Round 2: Demultiplexing with SP27 adapters (fused with round 1)...")
+    sink1 = nio.Sink(p1, False, args.compression_level, threads=args.threads)
+    sink2 = nio.Sink(p2, False, args.compression_level, threads=args.threads)
+    bp2_out = np.zeros(len(n1), np.int64)
+    n2_out = np.zeros(len(n1), np.int64)
+    try:
+        with nio.Reader(infile, args.batch_mb << 20, threads=args.threads) as reader:
+            for batch in reader:
+                try:
+                    if not len(batch):
+                        continue
+                    if len(ctxs) == 1:
+                        res = ctxs[0].run(batch.packed)
+                    else:
+                        res, _ = lib.run_multi(ctxs, batch.packed)
+                    (s1, e1, o1), (s2, e2, o2, nrc2) = plan_rounds(res, batch.lens)
+                    b1 = res["bin1"].astype(np.int64)
+                    b2 = res["bin2"].astype(np.int64)
+                    m1 = b1 >= 0
+                    idx1 = np.where(m1, b1, len(n1) if args.no_cleanup else -1)
+                    # unmatched in round 1 is written untrimmed to unknown (--no-cleanup only)
+                    s1w = np.where(m1, s1, 0)
+                    o1w = np.where(m1, o1, 0).astype(np.uint8)
+                    sink1.write(batch, idx1, s1w, e1, o1w, o1w)
+                    idx2 = np.where(m1, out2[np.maximum(b1, 0), b2 + 1], -1)
+                    # round-2 unknown: the round-1 output record, untrimmed by round 2
+                    m2 = b2 >= 0
+                    s2w = np.where(m2, s2, s1)
+                    e2w = np.where(m2, e2, e1)
+                    o2w = np.where(m2, o2, o1).astype(np.uint8)
+                    n2w = np.where(m2, nrc2, o1).astype(np.uint8)
+                    sink2.write(batch, idx2, s2w, e2w, o2w, n2w)
+                    _round_stats(st1, st2, res, batch.lens, m1, m2, b1, b2, s1, s2w, e2w,
+                                 bp2_out, n2_out)
+                finally:
+                    batch.free()
+    finally:
+        sink1.close()
+        sink2.close()
+    st1.n_out = int(sink1.n_written.sum())
+    st1.bp_out = int(sink1.bp_written.sum())
+    for i, s in enumerate(st2):
+        s.n_out, s.bp_out = int(n2_out[i]), int(bp2_out[i])
+    st1.write_json(f"{outdir}/SP5/cutadapt_SP5_{ds}.json", argv=["dmx-demux-loop"] + argv,
+                   cores=args.threads, in_path=infile, error_rate=args.e_rate)
+    print(f"Found {len(n1)} identifiers from SP5 demultiplexing")
+    for i, ident in enumerate(n1):
+        st2[i].write_json(f"{outdir}/SP27/{ident}_{ds}.json",
+                          argv=["dmx-demux-loop"] + argv, cores=args.threads,
+                          in_path=f"{outdir}/SP5/{ident}_{ds}.fastq.gz", error_rate=args.e_rate)
+    for ctx in ctxs:
+        ctx.close()
+    print("Demultiplexing complete!")
+    print(f"Finished in {time.perf_counter() - t0:.3f} s on {len(ctxs)} GPU(s): "
+          f"{st1.n_in:,} reads, {st1.n_with_adapter:,} with an SP5 adapter")
+    print("Pipeline complete!")
+    print(f"Results in: {outdir}")
+    return 0
+
+
+def _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w, bp2_out, n2_out):
+    lens = lens.astype(np.int64)
+    n = len(res)
+    rc1 = (res["rc1"] == 1) & m1
+    st1.n_in += n
+    st1.bp_in += int(lens.sum())
+    st1.n_with_adapter += int(m1.sum())
+    st1.n_rc += int(rc1.sum())
+    st1.add_counts(b1[m1], rc1[m1], len(st1.adapters))
+    st1.add_matches(b1[m1], "front", s1[m1], res["m1_errors"].astype(np.int64)[m1])
+    # round 2, one report per SP5 bin: its input is that bin's round-1 output
+    len1 = lens - s1
+    rc2 = (res["rc2"] == 1) & m2
+    for i, s in enumerate(st2):
+        sel = m1 & (b1 == i)
+        if not sel.any():
+            continue
+        s.n_in += int(sel.sum())
+        s.bp_in += int(len1[sel].sum())
+        hit = sel & m2
+        s.n_with_adapter += int(hit.sum())
+        s.n_rc += int(rc2[sel].sum())
+        s.add_counts(b2[hit], rc2[hit], len(s.adapters))
+        s.add_matches(b2[hit], "back", len1[hit] - res["m2_rstart"].astype(np.int64)[hit],
+                      res["m2_errors"].astype(np.int64)[hit])
+        # reads the per-call cutadapt would write (all of them: unknown included), before the
+        # script's cleanup deletes files
+        n2_out[i] += int(sel.sum())
+        bp2_out[i] += int(np.where(m2, e2w - s2w, len1)[sel].sum())
+
+
+def main():
+    try:
+        sys.exit(run())
+    except lib.DmxError as e:
+        print(f"dmx-demux-loop: GPU error: {e}", file=sys.stderr)
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,207 @@
+"""ctypes binding of libdmx_io.so (include/dmx_io.h): native FASTQ/FASTA(.gz) ingest + packing
+and per-bin writers with parallel gzip.
+
+The CLI's record path: `Reader` yields `NativeBatch`es (record spans + the packed device layout,
+straight into `lib.Context.run`), `Sink` writes each read to its bin (or nowhere) with its trim
+coordinates and orientation.  Replaces dnaio/xopen around cutadapt's per-read loop
+(SURVEY.md §8f rank 1).  Like libdmx there is no Python fallback: a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .lib import DmxError, Packed
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+IO_PATH = os.path.join(HERE, "libdmx_io.so")
+IO_EXPORTS = ["dmx_io_abi_version", "dmx_reader_open", "dmx_reader_next", "dmx_reader_error",
+              "dmx_reader_close", "dmx_batch_free", "dmx_sink_open", "dmx_sink_write",
+              "dmx_sink_close", "dmx_sink_error", "dmx_sink_free"]
+
+
+class _CBatch(ctypes.Structure):
+    _fields_ = [("n_reads", ctypes.c_size_t), ("fasta", ctypes.c_int32), ("_pad", ctypes.c_int32),
+                ("text", ctypes.c_void_p), ("head", ctypes.c_void_p),
+                ("seqtext", ctypes.c_void_p), ("seq", ctypes.c_void_p),
+                ("qual", ctypes.c_void_p), ("lens", ctypes.c_void_p),
+                ("seq2b", ctypes.c_void_p), ("nmask", ctypes.c_void_p),
+                ("offsets", ctypes.c_void_p), ("n_words", ctypes.c_size_t),
+                ("total_nt", ctypes.c_uint64)]
+
+
+_io = None
+
+
+def load() -> ctypes.CDLL:
+    global _io
+    if _io is not None:
+        return _io
+    if not os.path.exists(IO_PATH):
+        raise DmxError(f"{IO_PATH} not built: run `make -C nanopore-barcoding-orc_amd`")
+    L = ctypes.CDLL(IO_PATH)
+    P, c_int, c_size = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    L.dmx_io_abi_version.restype = c_int
+    L.dmx_reader_open.argtypes = [ctypes.c_char_p, c_size, c_int, ctypes.POINTER(P)]
+    L.dmx_reader_next.argtypes = [P, ctypes.POINTER(ctypes.POINTER(_CBatch))]
+    L.dmx_reader_error.argtypes = [P]
+    L.dmx_reader_error.restype = ctypes.c_char_p
+    L.dmx_reader_close.argtypes = [P]
+    L.dmx_reader_close.restype = None
+    L.dmx_batch_free.argtypes = [ctypes.POINTER(_CBatch)]
+    L.dmx_batch_free.restype = None
+    L.dmx_sink_open.argtypes = [ctypes.POINTER(ctypes.c_char_p), c_int, c_int, c_int, c_int,
+                                ctypes.POINTER(P)]
+    L.dmx_sink_write.argtypes = [P, ctypes.POINTER(_CBatch), P, P, P, P, P]
+    L.dmx_sink_close.argtypes = [P, P, P]
+    L.dmx_sink_error.argtypes = [P]
+    L.dmx_sink_error.restype = ctypes.c_char_p
+    L.dmx_sink_free.argtypes = [P]
+    L.dmx_sink_free.restype = None
+    if L.dmx_io_abi_version() != 1:
+        raise DmxError("libdmx_io ABI mismatch")
+    _io = L
+    return L
+
+
+def _view(ptr, n, dtype):
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    ct = np.ctypeslib.as_ctypes_type(np.dtype(dtype))
+    return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), shape=(n,))
+
+
+class NativeBatch:
+    """One batch of records owned by libdmx_io (numpy views valid until `free`)."""
+
+    def __init__(self, ptr):
+        self._ptr = ptr
+        c = ptr.contents
+        n = int(c.n_reads)
+        self.n = n
+        self.fasta = bool(c.fasta)
+        self.lens = _view(c.lens, n, np.uint32)
+        self.head = _view(c.head, 2 * n, np.uint64).reshape(n, 2)
+        self.seq = _view(c.seq, 2 * n, np.uint64).reshape(n, 2)
+        self.qual = None if self.fasta else _view(c.qual, 2 * n, np.uint64).reshape(n, 2)
+        nw = int(c.n_words)
+        self.packed = Packed(_view(c.seq2b, nw, np.uint32), _view(c.nmask, nw, np.uint32),
+                             _view(c.offsets, n, np.uint64), self.lens)
+        self.total_nt = int(c.total_nt)
+        self._text, self._seqtext = c.text, c.seqtext
+
+    def __len__(self):
+        return self.n
+
+    # record access (tests / small consumers; the CLI never loops over records in Python)
+    def _bytes(self, base, a, b):
+        return ctypes.string_at(base + int(a), int(b - a)) if b > a else b""
+
+    def header(self, i) -> bytes:
+        return self._bytes(self._text, *self.head[i])
+
+    def sequence(self, i) -> bytes:
+        return self._bytes(self._seqtext, *self.seq[i])
+
+    def quality(self, i):
+        return None if self.qual is None else self._bytes(self._text, *self.qual[i])
+
+    def free(self):
+        if self._ptr is not None:
+            load().dmx_batch_free(self._ptr)
+            self._ptr = None
+            self.packed = None
+
+
+class Reader:
+    """Batches of a FASTQ/FASTA(.gz) file ("-" = stdin), parsed and packed natively."""
+
+    def __init__(self, path: str, batch_bytes: int = 256 << 20, threads: int = 0):
+        self._L = load()
+        h = ctypes.c_void_p()
+        rc = self._L.dmx_reader_open(path.encode(), int(batch_bytes), int(threads),
+                                     ctypes.byref(h))
+        if rc != 0:
+            raise OSError(f"cannot open {path}")
+        self._h = h
+        self.path = path
+
+    def __iter__(self):
+        while True:
+            b = self.next()
+            if b is None:
+                return
+            yield b
+
+    def next(self):
+        p = ctypes.POINTER(_CBatch)()
+        rc = self._L.dmx_reader_next(self._h, ctypes.byref(p))
+        if rc != 0:
+            msg = self._L.dmx_reader_error(self._h)
+            raise ValueError(f"{self.path}: {msg.decode() if msg else 'read error'}")
+        return NativeBatch(p) if p else None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.dmx_reader_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class Sink:
+    """Outputs (created now) receiving records in input order; '.gz' paths are gzip members."""
+
+    def __init__(self, paths, fasta_out: bool, level: int = 1, threads: int = 0):
+        self._L = load()
+        self.paths = list(paths)
+        arr = (ctypes.c_char_p * len(self.paths))(*[p.encode() for p in self.paths])
+        h = ctypes.c_void_p()
+        rc = self._L.dmx_sink_open(arr, len(self.paths), int(bool(fasta_out)), int(level),
+                                   int(threads), ctypes.byref(h))
+        self._h = h
+        if rc != 0:
+            msg = self._L.dmx_sink_error(h).decode() if h else "cannot open outputs"
+            self._L.dmx_sink_free(h)
+            self._h = None
+            raise OSError(msg)
+        self.n_written = self.bp_written = None
+
+    def write(self, batch: NativeBatch, out_idx, start, stop, rc, n_rc):
+        n = len(batch)
+        arrs = [np.ascontiguousarray(out_idx, np.int32), np.ascontiguousarray(start, np.int32),
+                np.ascontiguousarray(stop, np.int32), np.ascontiguousarray(rc, np.uint8),
+                np.ascontiguousarray(n_rc, np.uint8)]
+        for a in arrs:
+            if len(a) != n:
+                raise ValueError("per-read arrays must have one entry per read")
+        r = self._L.dmx_sink_write(self._h, batch._ptr, *[a.ctypes.data for a in arrs])
+        if r != 0:
+            raise OSError(self._L.dmx_sink_error(self._h).decode())
+
+    def close(self):
+        if self._h is None:
+            return
+        n = np.zeros(len(self.paths), np.uint64)
+        bp = np.zeros(len(self.paths), np.uint64)
+        r = self._L.dmx_sink_close(self._h, n.ctypes.data, bp.ctypes.data)
+        msg = self._L.dmx_sink_error(self._h).decode()
+        self._L.dmx_sink_free(self._h)
+        self._h = None
+        self.n_written, self.bp_written = n, bp
+        if r != 0:
+            raise OSError(msg)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.dmx_sink_free(self._h)
+            self._h = None

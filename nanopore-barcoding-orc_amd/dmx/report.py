@@ -11,7 +11,9 @@ from __future__ import annotations
 import json
 import platform
 import sys
-from collections import defaultdict
+from collections import Counter, defaultdict
+
+import numpy as np
 
 from . import __version__
 
@@ -24,13 +26,35 @@ class Stats:
         self.n_rc = 0
         self.n_with_adapter = 0
         self.n_discard_untrimmed = 0
+        self.rc_mode = False      # --rc given: on_reverse_complement is reported (else null)
         self.matches = defaultdict(int)
         self.on_rc = defaultdict(int)
-        # adapter index -> part ("front"/"back") -> removed length -> errors -> count
-        self.hist = defaultdict(lambda: defaultdict(lambda: defaultdict(lambda: defaultdict(int))))
+        # adapter index -> part ("front"/"back") -> Counter{(removed length, errors): count}
+        self.hist = defaultdict(lambda: defaultdict(Counter))
 
     def add_match(self, a: int, rc: bool, part: str, removed: int, errors: int):
-        self.hist[a][part][removed][errors] += 1
+        self.hist[a][part][(int(removed), int(errors))] += 1
+
+    def add_matches(self, a, part: str, removed, errors):
+        """Vectorised add_match for arrays of adapter index / removed length / errors."""
+        a = np.asarray(a, np.int64)
+        if not len(a):
+            return
+        key = (a << 40) | (np.asarray(removed, np.int64) << 8) | np.asarray(errors, np.int64)
+        u, c = np.unique(key, return_counts=True)
+        for k, n in zip(u.tolist(), c.tolist()):
+            self.hist[k >> 40][part][((k >> 8) & ((1 << 32) - 1), k & 255)] += n
+
+    def add_counts(self, bins, rc, n_adapters: int):
+        """Per-adapter totals from arrays of matched adapter index and RC flag."""
+        bins = np.asarray(bins, np.int64)
+        m = np.bincount(bins, minlength=n_adapters)
+        r = np.bincount(bins[np.asarray(rc, bool)], minlength=n_adapters)
+        for a in range(n_adapters):
+            if m[a]:
+                self.matches[a] += int(m[a])
+            if r[a]:
+                self.on_rc[a] += int(r[a])
 
     def to_json(self, argv, cores, in_path, error_rate):
         adapters = []
@@ -45,7 +69,9 @@ class Stats:
                     continue
                 else:
                     seq = ad.seq
-                h = self.hist[a][part]
+                h = defaultdict(dict)
+                for (L, e), cnt in self.hist[a][part].items():
+                    h[L][e] = cnt
                 ends[part] = {
                     "type": "regular", "sequence": seq, "error_rate": error_rate, "indels": True,
                     "error_lengths": None,   # UNVERIFIED layout; not produced
@@ -58,7 +84,7 @@ class Stats:
                 }
             adapters.append({
                 "name": ad.name, "total_matches": self.matches[a],
-                "on_reverse_complement": self.on_rc[a] if self.on_rc else None,
+                "on_reverse_complement": self.on_rc[a] if (self.rc_mode or self.on_rc) else None,
                 "linked": linked,
                 "five_prime_end": ends.get("front"), "three_prime_end": ends.get("back"),
             })

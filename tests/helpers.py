@@ -9,6 +9,7 @@ from dmx import fastx, panel
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLI = os.path.join(ROOT, "nanopore-barcoding-orc_amd", "bin", "cutadapt")
+LOOP = os.path.join(ROOT, "nanopore-barcoding-orc_amd", "bin", "dmx-demux-loop")
 
 
 def write_fastq(path, names, seqs, quals):

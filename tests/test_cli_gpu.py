@@ -1,6 +1,7 @@
 """The drop-in CLI replaying scripts/02_cutadapt_loop.sh's command sequence on the GPU; every
 output file is compared record-for-record with outputs rendered from the oracle."""
 import glob
+import json
 import os
 import subprocess
 
@@ -9,7 +10,7 @@ import pytest
 
 import oracle
 from dmx import panel, synth
-from helpers import (CLI, amplicon_reads, oracle_linked, oracle_round, random_quals, read_fastq,
+from helpers import (CLI, LOOP, amplicon_reads, oracle_linked, oracle_round, random_quals, read_fastq,
                      write_fastq)
 
 pytestmark = pytest.mark.gpu
@@ -64,12 +65,54 @@ def test_02_cutadapt_loop_dropin(tmp_path):
             assert got == [("@" + n, s, q) for n, s, q in exp2.get(b, [])], (ident, name27)
             total2 += len(got)
     assert total2 > 0.6 * len(seqs)
-    import json
     rep = json.load(open(f"{out}/SP5/cutadapt_SP5_{ds}.json"))
     assert rep["read_counts"]["input"] == len(seqs)
     assert rep["read_counts"]["read1_with_adapter"] == sum(len(v) for k, v in exp1.items()
                                                           if k >= 0)
     assert [a["name"] for a in rep["adapters_read1"]] == n5
+
+    # the fused driver (one pass, DMX_MODE_TWO_ROUND) writes the same files and reports
+    fused = tmp_path / "fused"
+    subprocess.run([LOOP, infile, "-j", "4", "--outdir", str(fused), "--no-cleanup"],
+                   check=True, stdout=subprocess.DEVNULL)
+    per_call = sorted(os.path.relpath(f, out) for f in glob.glob(f"{out}/*/*"))
+    assert sorted(os.path.relpath(f, fused) for f in glob.glob(f"{fused}/*/*")) == per_call
+    for rel in per_call:
+        if rel.endswith(".json"):
+            a, b = json.load(open(f"{out}/{rel}")), json.load(open(f"{fused}/{rel}"))
+            for key in ("read_counts", "basepair_counts", "adapters_read1"):
+                assert a[key] == b[key], (rel, key)
+        else:
+            assert read_fastq(f"{out}/{rel}") == read_fastq(f"{fused}/{rel}"), rel
+    # default: the files 02_cutadapt_loop.sh keeps after its cleanup (:107-119)
+    clean = tmp_path / "clean"
+    subprocess.run([LOOP, infile, "--outdir", str(clean)], check=True, stdout=subprocess.DEVNULL)
+    kept = sorted(os.path.relpath(f, clean) for f in glob.glob(f"{clean}/*/*"))
+    assert kept == sorted(r for r in per_call if "unknown" not in r and
+                          not any(f"SP27_0{k}" in r for k in ("09", "10", "11", "12")))
+
+
+def test_cli_multi_gpu_sharding_keeps_order(tmp_path):
+    """DMX_GPUS shards each batch over several contexts (here several contexts on one GPU);
+    outputs and report equal the single-context run."""
+    d = synth.generate("c2", n=4000, seed=21)
+    seqs = synth.to_strings(d)
+    rng = np.random.default_rng(4)
+    names = [f"r{i}" for i in range(len(seqs))]
+    write_fastq(str(tmp_path / "in.fastq"), names, seqs, random_quals(rng, map(len, seqs)))
+    outs = {}
+    for tag, gpus in (("one", "1"), ("three", "0,0,0")):
+        od = tmp_path / tag
+        od.mkdir()
+        env = dict(os.environ, DMX_GPUS=gpus)
+        subprocess.run([CLI, "-e", "0.1", "-j", "3", "--rc", "-g", f"file:{panel.SP5_FASTA}",
+                        "-o", f"{od}/{{name}}.fastq.gz", str(tmp_path / "in.fastq"),
+                        f"--json={od}/r.json", "--batch-mb", "1"], check=True, env=env,
+                       stdout=subprocess.DEVNULL)
+        outs[tag] = {os.path.basename(f): read_fastq(f) for f in glob.glob(f"{od}/*.fastq.gz")}
+        outs[tag]["json"] = json.load(open(f"{od}/r.json"))["adapters_read1"]
+    assert outs["one"] == outs["three"]
+    assert sum(len(v) for k, v in outs["one"].items() if k != "json") == len(seqs)
 
 
 def _read_fasta(path):

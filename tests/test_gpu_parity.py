@@ -203,3 +203,28 @@ def test_config5_linked_matches_oracle(ctx):
     ctx.set_panel(1, d["sp27"], lib.DMX_BACK)
     ctx.set_mode(lib.MODE_LINKED)
     _assert_same(ctx.run(lib.pack(d["blob"], d["offsets"], d["lengths"])), exp)
+
+
+def test_run_multi_shards_equal_single_context(ctx):
+    """dmx_run_multi: length-balanced contiguous shards over several contexts (here three on
+    one GPU, each with its own stream and host thread) give the single-context results in
+    input order, and the summed per-bin counts."""
+    d = synth.generate("c2", n=20000, seed=31)
+    exp = _gpu_two_round(ctx, d)
+    exp_counts = ctx.counts()
+    ctxs = [lib.Context(0) for _ in range(3)]
+    try:
+        for c in ctxs:
+            c.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC)
+            c.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC)
+            c.set_mode(lib.MODE_TWO_ROUND)
+        got, counts = lib.run_multi(ctxs, lib.pack(d["blob"], d["offsets"], d["lengths"]))
+        _assert_same(got, exp)
+        assert np.array_equal(counts, exp_counts)
+        # more shards than reads: empty shards are skipped
+        small = synth.generate("c2", n=2, seed=3)
+        g2, _ = lib.run_multi(ctxs, lib.pack(small["blob"], small["offsets"], small["lengths"]))
+        _assert_same(g2, _gpu_two_round(ctx, small))
+    finally:
+        for c in ctxs:
+            c.close()

@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
     exported = set(re.findall(r" T (dmx_\w+)", out))
     assert declared <= exported
     L = lib.load()
-    assert L.dmx_abi_version() == 2
+    assert L.dmx_abi_version() == 3
 
 
 def _unpack(p: lib.Packed, i: int) -> str:
@@ -113,3 +113,42 @@ def test_synth_config5_linked_shape():
     assert 300 < d["lengths"].mean() < 800
     e = synth.generate("c5", n=100, first=1900)
     assert (e["lengths"] == d["lengths"][1900:]).all()
+
+
+def test_loop_dataset_name_and_device_spec(monkeypatch):
+    """02_cutadapt_loop.sh:26-35 dataset naming; DMX_GPUS / DMX_DEVICE parsing (no GPU use)."""
+    from dmx import cli, loop
+    assert loop.dataset_name("/d/pychopped/pychopped_s1_pass.fastq.gz") == "s1"
+    assert loop.dataset_name("x/run7.fq") == "run7"
+    args = cli.build_parser().parse_args(["-g", "ACGT", "-o", "o.fq", "in.fq"])
+    monkeypatch.setenv("DMX_GPUS", "0,2,5")
+    assert cli._devices(args) == [0, 2, 5]
+    monkeypatch.setenv("DMX_GPUS", "3")
+    assert cli._devices(args) == [0, 1, 2]
+    monkeypatch.delenv("DMX_GPUS")
+    monkeypatch.setenv("DMX_DEVICE", "4")
+    assert cli._devices(args) == [4]
+    args.device = 1
+    assert cli._devices(args) == [1]
+
+
+def test_loop_composite_coordinates_match_two_calls():
+    """plan_rounds: the fused coordinates equal applying round 1 then round 2 as two separate
+    cutadapt calls would (orientation algebra checked on explicit strings)."""
+    from dmx import fastx, loop
+    rng = np.random.default_rng(9)
+    n = 400
+    seqs = ["".join(rng.choice(list("ACGT"), int(rng.integers(5, 60)))) for _ in range(n)]
+    lens = np.array([len(s) for s in seqs], np.uint32)
+    res = np.zeros(n, lib.RESULT_DTYPE)
+    res["rc1"] = rng.integers(0, 2, n)
+    res["rc2"] = rng.integers(0, 2, n)
+    res["m1_rstop"] = [int(rng.integers(0, L + 1)) for L in lens]
+    res["m2_rstart"] = [int(rng.integers(0, L - s + 1)) for L, s in zip(lens, res["m1_rstop"])]
+    _, (s2, e2, o2, nrc) = loop.plan_rounds(res, lens)
+    for i, s in enumerate(seqs):
+        t1 = (fastx.revcomp(s.encode()) if res["rc1"][i] else s.encode())[res["m1_rstop"][i]:]
+        t2 = (fastx.revcomp(t1) if res["rc2"][i] else t1)[:res["m2_rstart"][i]]
+        full = fastx.revcomp(s.encode()) if o2[i] else s.encode()
+        assert full[s2[i]:e2[i]] == t2
+        assert nrc[i] == res["rc1"][i] + res["rc2"][i]

@@ -1,0 +1,164 @@
+"""Native record I/O (libdmx_io, include/dmx_io.h) against the Python record layer (CPU only).
+
+The Python reader/renderer in dmx/fastx.py restates dnaio/xopen's conventions in a few lines and
+serves as the checker here; the CLI itself uses the native path."""
+import gzip
+import re
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+from dmx import fastx, lib, nio
+
+ROOT = __import__("os").path.dirname(__import__("os").path.dirname(__file__))
+
+
+def _records(n, seed=0, crlf=False):
+    rng = np.random.default_rng(seed)
+    recs = []
+    for i in range(n):
+        L = int(rng.integers(0, 400))
+        s = "".join(rng.choice(list("ACGTNacgtRY"), L))
+        q = "".join(chr(33 + int(x)) for x in rng.integers(0, 41, L))
+        recs.append((f"read{i} runid=x ch={i % 7}", s, q))
+    eol = "\r\n" if crlf else "\n"
+    text = "".join(f"@{h}{eol}{s}{eol}+{eol}{q}{eol}" for h, s, q in recs)
+    return recs, text
+
+
+def test_io_library_exports_every_declared_symbol():
+    hdr = open(f"{ROOT}/include/dmx_io.h").read()
+    declared = set(re.findall(r"^\s*(?:int|void|const char\*)\s+(dmx_\w+)\(", hdr, re.M))
+    assert declared == set(nio.IO_EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", nio.IO_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert declared <= set(re.findall(r" T (dmx_\w+)", out))
+    assert nio.load().dmx_io_abi_version() == 1
+
+
+@pytest.mark.parametrize("kind", ["plain", "gz", "gz_members", "crlf"])
+@pytest.mark.parametrize("batch_bytes", [1 << 16, 64 << 20])
+def test_reader_matches_python_and_packer(tmp_path, kind, batch_bytes):
+    recs, text = _records(3000, seed=1, crlf=(kind == "crlf"))
+    data = text.encode()
+    p = tmp_path / ("in.fastq.gz" if kind.startswith("gz") else "in.fastq")
+    if kind == "gz":
+        p.write_bytes(gzip.compress(data, 1))
+    elif kind == "gz_members":   # pigz/bgzip-like: several members back to back
+        cut = [0, len(data) // 3, len(data) // 2, len(data)]
+        p.write_bytes(b"".join(gzip.compress(data[a:b], 6) for a, b in zip(cut, cut[1:])))
+    else:
+        p.write_bytes(data)
+    got = []
+    with nio.Reader(str(p), batch_bytes=batch_bytes, threads=4) as r:
+        for b in r:
+            ref = lib.pack(np.frombuffer(b"".join(b.sequence(i) for i in range(len(b))) or b"\0",
+                                         np.uint8),
+                           np.concatenate([[0], np.cumsum(b.lens[:-1], dtype=np.uint64)])
+                           .astype(np.uint64) if len(b) else np.zeros(0, np.uint64), b.lens)
+            assert np.array_equal(b.packed.offsets, ref.offsets)
+            assert np.array_equal(b.packed.seq2b, ref.seq2b)
+            assert np.array_equal(b.packed.nmask, ref.nmask)
+            for i in range(len(b)):
+                got.append((b.header(i).decode(), b.sequence(i).decode(), b.quality(i).decode()))
+            b.free()
+    assert got == recs
+
+
+def test_reader_fasta_multiline_and_edge_cases(tmp_path):
+    p = tmp_path / "c.fasta"
+    p.write_text("\n>a x\nACGT \nAC\n\n>b\nGG\n>empty\n>last\r\nTT")
+    with nio.Reader(str(p), batch_bytes=1 << 16) as r:
+        bs = list(r)
+    assert sum(len(b) for b in bs) == 4
+    b = bs[0]
+    assert [b.header(i) for i in range(4)] == [b"a x", b"b", b"empty", b"last"]
+    assert [b.sequence(i) for i in range(4)] == [b"ACGTAC", b"GG", b"", b"TT"]
+    assert b.quality(0) is None and b.fasta
+    # big FASTA through several batches
+    rng = np.random.default_rng(3)
+    seqs = ["".join(rng.choice(list("ACGT"), int(rng.integers(1, 3000)))) for _ in range(500)]
+    txt = "".join(f">s{i}\n" + "\n".join(s[k:k + 60] for k in range(0, len(s), 60)) + "\n"
+                  for i, s in enumerate(seqs))
+    (tmp_path / "m.fa.gz").write_bytes(gzip.compress(txt.encode()))
+    out = []
+    with nio.Reader(str(tmp_path / "m.fa.gz"), batch_bytes=1 << 16, threads=3) as r:
+        for b in r:
+            out += [b.sequence(i).decode() for i in range(len(b))]
+    assert out == seqs
+
+
+def test_reader_empty_and_errors(tmp_path):
+    (tmp_path / "e.fq").write_bytes(b"")
+    with nio.Reader(str(tmp_path / "e.fq")) as r:
+        assert list(r) == []
+    (tmp_path / "e.fq.gz").write_bytes(gzip.compress(b""))
+    with nio.Reader(str(tmp_path / "e.fq.gz")) as r:
+        assert list(r) == []
+    for bad, msg in [(b"@a\nAC\n-\nII\n", "third line"), (b"@a\nAC\n+\nI\n", "lengths"),
+                     (b"@a\nAC\n+\n", "truncated"), (b"xyz\n", "neither")]:
+        (tmp_path / "b.fq").write_bytes(bad)
+        with pytest.raises(ValueError, match=msg):
+            with nio.Reader(str(tmp_path / "b.fq")) as r:
+                list(r)
+    (tmp_path / "t.fq.gz").write_bytes(gzip.compress(b"@a\nAC\n+\nII\n" * 1000)[:-20])
+    with pytest.raises(ValueError, match="truncated gzip"):
+        with nio.Reader(str(tmp_path / "t.fq.gz")) as r:
+            list(r)
+    with pytest.raises(OSError):
+        nio.Reader(str(tmp_path / "missing.fq"))
+
+
+@pytest.mark.parametrize("fasta_out", [False, True])
+def test_sink_matches_python_render(tmp_path, fasta_out):
+    recs, text = _records(2500, seed=2)
+    (tmp_path / "in.fq").write_text(text)
+    rng = np.random.default_rng(5)
+    n_out = 5
+    ext = ".fasta" if fasta_out else ".fastq"
+    paths = [str(tmp_path / f"o{k}{ext}.gz") if k % 2 == 0 else str(tmp_path / f"o{k}{ext}")
+             for k in range(n_out)]
+    expect = [[] for _ in range(n_out)]
+    sink = nio.Sink(paths, fasta_out, level=1, threads=4)
+    pyb = list(fastx.read_batches(str(tmp_path / "in.fq"), batch_bytes=1 << 28))
+    assert len(pyb) == 1
+    pb = pyb[0]
+    base = 0
+    with nio.Reader(str(tmp_path / "in.fq"), batch_bytes=1 << 16) as r:
+        for b in r:
+            n = len(b)
+            lens = b.lens.astype(np.int64)
+            idx = rng.integers(-1, n_out - 1, n).astype(np.int32)   # last output stays empty
+            a = (rng.random(n) * (lens + 1)).astype(np.int64)
+            z = a + (rng.random(n) * (lens - a + 1)).astype(np.int64)
+            rc = rng.integers(0, 2, n).astype(np.uint8)
+            nrc = (rc + rng.integers(0, 2, n) * 2).astype(np.uint8)
+            for i in range(n):
+                if idx[i] >= 0:
+                    expect[idx[i]].append(fastx.render(pb, base + i, int(a[i]), int(z[i]),
+                                                       bool(rc[i]), b" rc" * int(nrc[i]),
+                                                       fasta_out))
+            sink.write(b, idx, a, z, rc, nrc)
+            b.free()   # the sink keeps its own reference until the batch is written
+            base += n
+    sink.close()
+    for k in range(n_out):
+        raw = open(paths[k], "rb").read()
+        if paths[k].endswith(".gz"):
+            raw = gzip.decompress(raw)
+        assert raw == b"".join(expect[k]), k
+        assert int(sink.n_written[k]) == len(expect[k])
+    assert len(expect[-1]) == 0 and gzip.decompress(open(paths[-1], "rb").read()) == b""
+
+
+def test_sink_rejects_bad_coordinates(tmp_path):
+    (tmp_path / "in.fq").write_text("@a\nACGT\n+\nIIII\n")
+    sink = nio.Sink([str(tmp_path / "o.fq")], False)
+    with nio.Reader(str(tmp_path / "in.fq")) as r:
+        b = r.next()
+        sink.write(b, [0], [1], [9], [0], [0])
+        b.free()
+    with pytest.raises(OSError, match="out of range"):
+        sink.close()
