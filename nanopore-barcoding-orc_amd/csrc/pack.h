@@ -33,8 +33,9 @@ inline const PackTables& pack_tables() {
 }
 
 // Pack one read of n nt from src into the word arrays at nt offset g0 (a multiple of 32).
-// The words of the read's last partial 32-nt group are written whole (zero tail), so the
-// caller only needs to zero the padding between reads if the buffer is reused.
+// Every word of the read's ceil(n/32) groups is written (zero tail), and reads are laid out
+// back to back on 32-nt boundaries, so only the DMX_PACK_PAD head and the tail after the last
+// read need zeroing by the caller.
 inline void pack_one(const uint8_t* src, uint32_t n, uint64_t g0, uint32_t* seq, uint32_t* nmask) {
     const PackTables& T = pack_tables();
     uint32_t* sw = seq + g0 / 16;
@@ -50,7 +51,7 @@ inline void pack_one(const uint8_t* src, uint32_t n, uint64_t g0, uint32_t* seq,
             nb |= (uint32_t)T.nflag[ch] << y;
         }
         sw[x / 16] = w0;
-        if (cnt > 16) sw[x / 16 + 1] = w1;
+        sw[x / 16 + 1] = w1;   // whole 32-nt groups: no word of a read's span is left unwritten
         nw[x / 32] = nb;
     }
 }

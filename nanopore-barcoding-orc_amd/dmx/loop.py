@@ -136,17 +136,26 @@ def run(argv=None) -> int:
     sink1 = nio.Sink(p1, False, args.compression_level, threads=args.threads)
     sink2 = nio.Sink(p2, False, args.compression_level, threads=args.threads)
     bp2_out = np.zeros(len(n1), np.int64)
+    prof = dict(read_wait=0.0, gpu=0.0, plan_write=0.0, drain=0.0)
     n2_out = np.zeros(len(n1), np.int64)
     try:
         with nio.Reader(infile, args.batch_mb << 20, threads=args.threads) as reader:
-            for batch in reader:
+            while True:
+                tw = time.perf_counter()
+                batch = reader.next()
+                prof["read_wait"] += time.perf_counter() - tw
+                if batch is None:
+                    break
                 try:
                     if not len(batch):
                         continue
+                    tw = time.perf_counter()
                     if len(ctxs) == 1:
                         res = ctxs[0].run(batch.packed)
                     else:
                         res, _ = lib.run_multi(ctxs, batch.packed)
+                    prof["gpu"] += time.perf_counter() - tw
+                    tw = time.perf_counter()
                     (s1, e1, o1), (s2, e2, o2, nrc2) = plan_rounds(res, batch.lens)
                     b1 = res["bin1"].astype(np.int64)
                     b2 = res["bin2"].astype(np.int64)
@@ -166,11 +175,17 @@ def run(argv=None) -> int:
                     sink2.write(batch, idx2, s2w, e2w, o2w, n2w)
                     _round_stats(st1, st2, res, batch.lens, m1, m2, b1, b2, s1, s2w, e2w,
                                  bp2_out, n2_out)
+                    prof["plan_write"] += time.perf_counter() - tw
                 finally:
                     batch.free()
     finally:
+        tw = time.perf_counter()
         sink1.close()
         sink2.close()
+        prof["drain"] += time.perf_counter() - tw
+    if os.environ.get("DMX_PROFILE_IO"):
+        print("io profile (s): " + ", ".join(f"{k} {v:.3f}" for k, v in prof.items()),
+              file=sys.stderr)
     st1.n_out = int(sink1.n_written.sum())
     st1.bp_out = int(sink1.bp_written.sum())
     for i, s in enumerate(st2):

@@ -162,3 +162,63 @@ def test_sink_rejects_bad_coordinates(tmp_path):
         b.free()
     with pytest.raises(OSError, match="out of range"):
         sink.close()
+
+
+def _bgzf(data: bytes, block: int = 60000) -> bytes:
+    """BGZF (bgzip/htslib) blocks: gzip members with a 'BC' extra subfield = block size - 1."""
+    import struct
+    out = []
+    for k in range(0, max(len(data), 1), block):
+        chunk = data[k:k + block]
+        c = zlib.compressobj(6, zlib.DEFLATED, -15)
+        raw = c.compress(chunk) + c.flush()
+        hdr = b"\x1f\x8b\x08\x04" + b"\0" * 4 + b"\0\xff" + struct.pack("<H", 6) + b"BC" + \
+            struct.pack("<HH", 2, 18 + len(raw) + 8 - 1)
+        out.append(hdr + raw + struct.pack("<II", zlib.crc32(chunk), len(chunk)))
+    return b"".join(out) + bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def _read_all(path, batch_bytes=1 << 20, threads=4):
+    got = []
+    with nio.Reader(str(path), batch_bytes=batch_bytes, threads=threads) as r:
+        for b in r:
+            got += [(b.header(i).decode(), b.sequence(i).decode(), b.quality(i).decode())
+                    for i in range(len(b))]
+            b.free()
+    return got
+
+
+@pytest.mark.parametrize("batch_bytes", [1 << 16, 1 << 20, 64 << 20])
+def test_sized_members_parallel_inflate(tmp_path, batch_bytes):
+    """Our writer's DX members (several per output: <= 4 MiB each), BGZF blocks, and a DX file
+    followed by an ordinary member all read back exactly; the files are plain gzip to others."""
+    recs, text = _records(30000, seed=4)
+    (tmp_path / "in.fq").write_text(text)
+    sink = nio.Sink([str(tmp_path / "dx.fq.gz")], False, level=1, threads=4)
+    with nio.Reader(str(tmp_path / "in.fq"), batch_bytes=2 << 20) as r:
+        for b in r:
+            n = len(b)
+            z = np.zeros(n, np.uint8)
+            sink.write(b, np.zeros(n, np.int32), np.zeros(n, np.int32), b.lens.astype(np.int32),
+                       z, z)
+            b.free()
+    sink.close()
+    dx = (tmp_path / "dx.fq.gz").read_bytes()
+    assert dx[12:14] == b"DX" and dx.count(b"\x1f\x8b\x08\x04") > 4
+    assert gzip.decompress(dx) == text.encode()
+    assert _read_all(tmp_path / "dx.fq.gz", batch_bytes) == recs
+    (tmp_path / "b.fq.gz").write_bytes(_bgzf(text.encode()))
+    assert gzip.decompress((tmp_path / "b.fq.gz").read_bytes()) == text.encode()
+    assert _read_all(tmp_path / "b.fq.gz", batch_bytes) == recs
+    extra, etext = _records(500, seed=6)
+    (tmp_path / "mix.fq.gz").write_bytes(dx + gzip.compress(etext.encode()))
+    assert _read_all(tmp_path / "mix.fq.gz", batch_bytes) == recs + extra
+
+
+def test_sized_member_crc_mismatch_is_an_error(tmp_path):
+    recs, text = _records(200, seed=7)
+    blob = bytearray(_bgzf(text.encode(), block=10000))
+    blob[200] ^= 0x40   # flip a bit inside the first block's deflate data
+    (tmp_path / "bad.fq.gz").write_bytes(bytes(blob))
+    with pytest.raises(ValueError):
+        _read_all(tmp_path / "bad.fq.gz")

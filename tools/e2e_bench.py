@@ -1,0 +1,154 @@
+"""End-to-end wall time of the demultiplexing step on a synthetic FASTQ(.gz) (not the bench line).
+
+SURVEY.md §8d asks for kernel time on resident reads (bench.py) and, separately, the
+end-to-end wall time including gzip and parse.  This tool generates `--reads` reads of a
+workload (default c2: 12x12 panel, lognormal ~1.2 kb) with random qualities, writes them as
+FASTQ.gz (level 1, parallel members, via libdmx_io), then times
+  fused : bin/dmx-demux-loop IN       (one pass, both rounds; what 02_cutadapt_loop.sh leaves)
+          on plain FASTQ (01_pychopper.sh:57 writes *_pass.fastq uncompressed), on our
+          multi-member .gz (parallel inflate) and on a single-member .gz (sequential inflate)
+  calls : the 13 bin/cutadapt calls of 02_cutadapt_loop.sh:64-103 (per-call drop-in)
+and prints one JSON line with reads/s for each.  Usage:
+  python tools/e2e_bench.py --reads 1000000 [--workload c2] [--threads 16] [--skip-calls]
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+import zlib
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "nanopore-barcoding-orc_amd")
+sys.path.insert(0, PKG)
+
+from dmx import nio, panel, synth  # noqa: E402
+
+
+def write_fastq(path_plain: str, d: dict, seed: int, chunk: int = 100_000) -> int:
+    """FASTQ text assembled with numpy (names r<i>, Phred 5..40), chunk by chunk."""
+    rng = np.random.default_rng(seed)
+    blob, offs, lens = d["blob"], d["offsets"].astype(np.int64), d["lengths"].astype(np.int64)
+    n = len(lens)
+    with open(path_plain, "wb") as fh:
+        for lo in range(0, n, chunk):
+            hi = min(n, lo + chunk)
+            names = [f"@r{i} ch={i % 512}\n".encode() for i in range(lo, hi)]
+            nl = np.array([len(x) for x in names], np.int64)
+            L = lens[lo:hi]
+            size = nl + L + 3 + L + 1
+            rec = np.zeros(hi - lo + 1, np.int64)
+            rec[1:] = np.cumsum(size)
+            out = np.empty(int(rec[-1]), np.uint8)
+            name_blob = np.frombuffer(b"".join(names), np.uint8)
+            nstart = np.concatenate([[0], np.cumsum(nl)[:-1]])
+            idx = np.repeat(rec[:-1] - nstart, nl) + np.arange(len(name_blob))
+            out[idx] = name_blob
+            s0 = rec[:-1] + nl
+            tot = int(L.sum())
+            rel = np.arange(tot) - np.repeat(np.cumsum(L) - L, L)
+            sidx = np.repeat(s0, L) + rel
+            out[sidx] = blob[np.repeat(offs[lo:hi], L) + rel]
+            out[s0 + L] = 10
+            out[s0 + L + 1] = 43
+            out[s0 + L + 2] = 10
+            out[sidx + np.repeat(L + 3, L)] = rng.integers(38, 74, tot, dtype=np.uint8)
+            out[rec[1:] - 1] = 10
+            fh.write(out.tobytes())
+    return n
+
+
+def gzip_native(src: str, dst: str, threads: int):
+    sink = nio.Sink([dst], False, 1, threads=threads)
+    with nio.Reader(src, 256 << 20, threads=threads) as r:
+        for b in r:
+            n = len(b)
+            z = np.zeros(n, np.uint8)
+            sink.write(b, np.zeros(n, np.int32), np.zeros(n, np.int32), b.lens.astype(np.int32),
+                       z, z)
+            b.free()
+    sink.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=1_000_000)
+    ap.add_argument("--workload", default="c2")
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--skip-calls", action="store_true")
+    ap.add_argument("--workdir", default=None)
+    a = ap.parse_args()
+    wd = a.workdir or tempfile.mkdtemp(prefix="dmx_e2e_")
+    pych = os.path.join(wd, "pychopped")
+    os.makedirs(pych, exist_ok=True)
+    t = time.perf_counter()
+    d = synth.generate(a.workload, n=a.reads, seed=77)
+    plain = os.path.join(pych, "pychopped_e2e.fastq")
+    gz = plain + ".gz"
+    write_fastq(plain, d, seed=5)
+    gzip_native(plain, gz, a.threads)
+    # a single-member gzip (Python gzip / pigz-like): only sequential inflate is possible
+    gz1 = os.path.join(wd, "single", "pychopped_e2e.fastq.gz")
+    os.makedirs(os.path.dirname(gz1), exist_ok=True)
+    with open(plain, "rb") as fi, open(gz1, "wb") as fo:
+        c = zlib.compressobj(1, zlib.DEFLATED, 31, 8, zlib.Z_HUFFMAN_ONLY)
+        while True:
+            chunk = fi.read(64 << 20)
+            if not chunk:
+                break
+            fo.write(c.compress(chunk))
+        fo.write(c.flush())
+    gen_s = time.perf_counter() - t
+    raw_bytes, gz_bytes = os.path.getsize(plain), os.path.getsize(gz)
+    env = dict(os.environ)
+    res = {"workload": a.workload, "reads": a.reads, "threads": a.threads,
+           "input_fastq_bytes": raw_bytes, "input_gz_bytes": gz_bytes, "gen_s": round(gen_s, 1)}
+
+    for tag, path in (("fused_plain", plain), ("fused_gz_members", gz),
+                      ("fused_gz_single", gz1)):
+        t = time.perf_counter()
+        p = subprocess.run([os.path.join(PKG, "bin", "dmx-demux-loop"), path, "-j",
+                            str(a.threads), "--outdir", os.path.join(wd, tag)], check=True,
+                           env=dict(env, DMX_PROFILE_IO="1"), stdout=subprocess.DEVNULL,
+                           stderr=subprocess.PIPE, text=True)
+        fs = time.perf_counter() - t
+        res[f"{tag}_s"] = round(fs, 3)
+        res[f"{tag}_reads_per_s"] = round(a.reads / fs, 1)
+        res[f"{tag}_profile"] = p.stderr.strip().splitlines()[-1] if p.stderr.strip() else ""
+    os.remove(plain)
+
+    if not a.skip_calls:
+        out = os.path.join(wd, "calls")
+        os.makedirs(f"{out}/SP5", exist_ok=True)
+        os.makedirs(f"{out}/SP27", exist_ok=True)
+        cli = os.path.join(PKG, "bin", "cutadapt")
+        j = str(a.threads)
+        t = time.perf_counter()
+        subprocess.run([cli, "--action=trim", "-e", "0.1", "-j", j, "--rc",
+                        "-g", f"file:{panel.SP5_FASTA}", "-o", f"{out}/SP5/{{name}}_e2e.fastq.gz",
+                        gz, f"--json={out}/SP5/cutadapt_SP5_e2e.json"], check=True, env=env,
+                       stdout=subprocess.DEVNULL)
+        ids = sorted(os.path.basename(f)[:-len("_e2e.fastq.gz")]
+                     for f in glob.glob(f"{out}/SP5/*_e2e.fastq.gz") if "unknown" not in f)
+        for ident in ids:
+            subprocess.run([cli, "--action=trim", "-e", "0.1", "-j", j, "--rc",
+                            "-a", f"file:{panel.SP27RC_FASTA}",
+                            "-o", f"{out}/SP27/{{name}}_{ident}_e2e.fastq.gz",
+                            f"{out}/SP5/{ident}_e2e.fastq.gz",
+                            f"--json={out}/SP27/{ident}_e2e.json"], check=True, env=env,
+                           stdout=subprocess.DEVNULL)
+        cs = time.perf_counter() - t
+        res["calls_s"] = round(cs, 3)
+        res["calls_reads_per_s"] = round(a.reads / cs, 1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
