@@ -138,6 +138,29 @@ int dmx_counts(dmx_ctx* ctx, uint64_t* out_counts, size_t n_out);
 int dmx_stats(dmx_ctx* ctx, float* stage_ms, int n_stage, uint64_t* counts, int n_counts,
               int* flags);
 
+/* ---- Residual-primer failsafe: exact degenerate-motif location (`seqkit locate -d`) ---------
+ * Replaces: `seqkit locate -d --pattern-file PRIMERS ENDS` in the failsafe of
+ * scripts/04_cleaning_primers.sh:397-460 (`:422`; seqkit v2, not vendored).  Every occurrence
+ * (overlapping ones included) of every IUPAC pattern (1..64 nt, at most 128 patterns) in every
+ * record, on the positive strand and — unless DMX_LOC_ONLY_POSITIVE — on the negative strand
+ * (the pattern matched against the reverse complement; reported in positive-strand
+ * coordinates).  Case-sensitive unless DMX_LOC_IGNORE_CASE (seqkit -i).  Pattern codes admit
+ * A/C/G/T(U) as IUPAC says (N = any of them); any other record byte matches nothing.
+ * Records are ASCII (caller-owned blob + offsets/lengths).  Writes min(total, cap) hits in
+ * unspecified order, *n_hits = total (call again with a larger buffer if total > cap). */
+#define DMX_LOC_IGNORE_CASE 0x1
+#define DMX_LOC_ONLY_POSITIVE 0x2
+typedef struct dmx_hit {
+    uint64_t seq;      /* record index                                    */
+    int32_t pattern;   /* pattern index                                   */
+    int32_t strand;    /* 0 = '+', 1 = '-'                                */
+    int32_t start;     /* 1-based first position on the positive strand   */
+    int32_t end;       /* 1-based last position (inclusive)               */
+} dmx_hit;
+int dmx_locate(dmx_ctx* ctx, const char* const* patterns, const int* plens, int n_patterns,
+               int flags, const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens,
+               size_t n_seqs, dmx_hit* out, size_t cap, uint64_t* n_hits);
+
 #ifdef __cplusplus
 }
 #endif

@@ -161,7 +161,6 @@ int grow_clusters(Ctx* c) {
 
 }  // namespace
 
-struct dmx_ctx : Ctx {};
 
 extern "C" {
 
@@ -427,7 +426,8 @@ size_t dmx_pack_words(uint64_t total_nt, size_t n_reads) {
 
 int dmx_pack(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens, size_t n_reads,
              uint32_t* out_seq2b, uint32_t* out_nmask, uint64_t* out_offsets) {
-    if ((!ascii && n_reads) || !out_seq2b || !out_nmask || !out_offsets) return DMX_E_INVALID;
+    if ((n_reads && (!offsets || !lens)) || !out_seq2b || !out_nmask || !out_offsets)
+        return DMX_E_INVALID;
     uint64_t g = DMX_PACK_PAD;
     uint64_t total = 0;
     for (size_t r = 0; r < n_reads; ++r) {
@@ -435,6 +435,7 @@ int dmx_pack(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens
         g += ((uint64_t)lens[r] + kPackAlign - 1) / kPackAlign * kPackAlign;
         total += lens[r];
     }
+    if (!ascii && total) return DMX_E_INVALID;   // a batch of empty reads needs no text
     const size_t words = dmx_pack_words(total, n_reads);
     memset(out_seq2b, 0, words * sizeof(uint32_t));
     memset(out_nmask, 0, words * sizeof(uint32_t));

@@ -77,3 +77,6 @@ int launch_round(Ctx* c, int round, hipStream_t st);
 int launch_finalize(Ctx* c, int round, hipStream_t st);
 
 }  // namespace dmx
+
+// The public opaque handle (include/dmx.h) is the host context.
+struct dmx_ctx : dmx::Ctx {};

@@ -133,10 +133,21 @@ __device__ __forceinline__ Cluster make_cluster(uint32_t item, int sub, uint32_t
     return c;
 }
 
-// Lower-bound key: the slot's best accepted score is >= lb, and a cell scoring exactly lb has a
-// cost <= cost (so an equal-score cell of higher cost can never win).  Max over tasks.
-__device__ __forceinline__ int lb_key(int lb, int cost) {
-    return lb > 0 ? (lb << 8) | (255 - cost) : 0;
+// Lower-bound key: the slot has an accepted cell of orientation o, cost `cost` and score >= lb,
+// so the slot's winning key is <= (lb, o, cost) in make_key's order (score desc, forward before
+// RC, cost asc).  Max over tasks: higher score, then forward, then lower cost.  A cell of equal
+// score bound loses to it only if it is RC against a forward bound, or of the same orientation
+// with a higher cost — a forward cell beats an RC cell of equal score whatever the costs
+// (ReverseComplementer takes the RC read only on a strictly greater score).
+__device__ __forceinline__ int lb_key(int lb, int o, int cost) {
+    return lb > 0 ? (lb << 9) | ((1 - o) << 8) | (255 - cost) : 0;
+}
+__device__ __forceinline__ int lb_score(int lbk) { return lbk ? (lbk >> 9) : -1000; }
+// can a cell of orientation o and cost `cost` whose score is at most ub beat the bound?
+__device__ __forceinline__ bool beats_lb(int lbk, int ub, int o, int cost) {
+    if (!lbk) return true;
+    const int lbs = lbk >> 9, lbo = 1 - ((lbk >> 8) & 1), lbc = 255 - (lbk & 255);
+    return ub > lbs || (ub == lbs && (o < lbo || (o == lbo && cost <= lbc)));
 }
 
 // One task's Myers scan over view columns (js, jhi]; last-row candidates are reported for
@@ -158,7 +169,7 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
     int d = (front && real) ? 0 : m;
     bool have = false;
     uint32_t cj1 = 0, cj2 = 0;
-    int cub = -128, lbk = 0;   // lbk = (lower bound << 8) | (255 - its cost), 0 = none
+    int cub = -128, lbk = 0;   // lbk = lb_key of the best certainly-accepted cell, 0 = none
 
 #define DMX_SCAN_STEP(q)                                                                  \
     {                                                                                     \
@@ -171,7 +182,7 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
                 const int ubc = lr - 2 * d;                                               \
                 {   /* certainly accepted: aligned length >= L0 and acc is monotone */       \
                     const int L0 = min(m, (int)j - d);                                    \
-                    if (L0 >= 0 && d <= (int)acc[L0]) lbk = max(lbk, lb_key(L0 - 3 * d, d)); \
+                    if (L0 >= 0 && d <= (int)acc[L0]) lbk = max(lbk, lb_key(L0 - 3 * d, tv.o, d)); \
                 }                                                                         \
                 if (have && j - cj2 <= gap) {                                             \
                     cj2 = j;                                                              \
@@ -213,7 +224,7 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
             dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
             if (dd <= (int)acc[i]) {              // accepted for sure (aligned length is i)
                 ubl = max(ubl, i - 2 * dd);
-                lbk = max(lbk, lb_key(i - 3 * dd, dd));
+                lbk = max(lbk, lb_key(i - 3 * dd, tv.o, dd));
             }
         }
         if (ubl > -128) {
@@ -303,12 +314,10 @@ __device__ __forceinline__ Cand make_cand(const TaskView& tv, uint32_t item, int
     return c;
 }
 
-// can a cell of cost `cost` whose aligned adapter length is <= lr beat the lower-bound key?
-__device__ __forceinline__ bool viable_lb(int lbk, int lr, int cost) {
-    if (!lbk) return true;
-    const int lbs = lbk >> 8, lbc = 255 - (lbk & 255);
-    const int ub = lr - 2 * cost;
-    return ub > lbs || (ub == lbs && cost <= lbc);
+// can a cell of orientation o and cost `cost` whose aligned adapter length is <= lr beat the
+// lower-bound key?
+__device__ __forceinline__ bool viable_lb(int lbk, int lr, int o, int cost) {
+    return beats_lb(lbk, lr - 2 * cost, o, cost);
 }
 
 // 16 view positions from view position p (may be negative or past the view: guard words).
@@ -337,7 +346,7 @@ __device__ __forceinline__ void flush_cands(const Sink& sink, const TaskView& tv
         const int cost = (int)((c0 >> bit) & 1ull) | ((int)((c1 >> bit) & 1ull) << 1) |
                          ((int)((c2 >> bit) & 1ull) << 2);
         const uint32_t j = seg + (uint32_t)bit;
-        if (!viable_lb(lbk, min(m, (int)j + cost), cost)) continue;
+        if (!viable_lb(lbk, min(m, (int)j + cost), tv.o, cost)) continue;
         const Cand cd = make_cand(tv, item, sub, m, cost, j);
         if (cost <= 3) sink.st[0].push(cd);
         else sink.st[1].push(cd);
@@ -378,7 +387,7 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
             if (ok) {                                                                     \
                 /* certainly accepted: aligned length >= L0 and acc is monotone (far from \
                    column 0, L0 = m and acc[m] = k >= d) */                               \
-                if (L0 >= 0) lbk = max(lbk, lb_key(L0 - 3 * d, d));                       \
+                if (L0 >= 0) lbk = max(lbk, lb_key(L0 - 3 * d, tv.o, d));                       \
                 if (!segset) {                                                            \
                     segset = true;                                                        \
                     seg = j;                                                              \
@@ -436,7 +445,7 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
             dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
             if (dd <= (int)acc[i]) {              // accepted for sure (aligned length is i)
                 rows |= 1ull << i;
-                lbk = max(lbk, lb_key(i - 3 * dd, dd));
+                lbk = max(lbk, lb_key(i - 3 * dd, tv.o, dd));
             }
         }
     }
@@ -445,7 +454,7 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
         const int i = __ffsll((unsigned long long)rows) - 1;
         rows &= rows - 1;
         const int cost = col_cost(pv, mv, i);
-        if (!viable_lb(lbk, i, cost)) continue;
+        if (!viable_lb(lbk, i, tv.o, cost)) continue;
         const Cand cd = make_cand(tv, item, sub, i, cost, len);
         if (cost <= 3) sink.st[0].push(cd);
         else sink.st[1].push(cd);
@@ -1474,8 +1483,7 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
         const Cluster c = R.cl[ci];
         const uint32_t slot = slot_of(R, c.item, c.sub);
         const int lbk = R.lb[slot];
-        const int lbs = lbk ? (lbk >> 8) : -1000;    // slot's best score is >= lbs ...
-        const int lbc = 255 - (lbk & 255);            // ... reached with cost <= lbc
+        const int lbs = lb_score(lbk);                // slot's best score is >= lbs
         Outcome out;
         out.key = ~0ull;
         out.origin = 0;
@@ -1511,8 +1519,7 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
 
         // can a cell of cost `cost` whose aligned adapter length is <= lr still win the slot?
         auto viable = [&](int lr, int cost) {
-            const int ub = lr - 2 * cost;   // score <= aligned length - 2 cost
-            return ub > lbs || (ub == lbs && cost <= lbc);
+            return beats_lb(lbk, lr - 2 * cost, tv.o, cost);   // score <= lr - 2 cost
         };
         auto consider = [&](int iend, int j, int s, int cost, uint64_t t) {
             const int ub = min(iend, j + cost) - 2 * cost;
@@ -1728,7 +1735,7 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
             out.pad = 0;
             const int lrmax = min(iend, j + cost);
             const int ub = lrmax - 2 * cost;
-            if (viable_lb(R.lb[slot], lrmax, cost) &&
+            if (viable_lb(R.lb[slot], lrmax, c.o, cost) &&
                 make_key(ub, c.o, cost, c.a, t) <= R.winner[slot]) {
                 if (cost == 0) {              // exact: the pointer chain is the pure diagonal
                     const int origin = j - iend;

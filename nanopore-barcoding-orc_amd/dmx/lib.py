@@ -28,7 +28,12 @@ assert RESULT_DTYPE.itemsize == 40
 EXPORTS = ["dmx_abi_version", "dmx_open", "dmx_close", "dmx_last_error", "dmx_set_panel",
            "dmx_set_panel_mixed", "dmx_set_mode", "dmx_pack_words", "dmx_pack", "dmx_run", "dmx_load", "dmx_exec",
            "dmx_sync", "dmx_fetch", "dmx_counts", "dmx_stats", "dmx_device_count",
-           "dmx_run_multi"]
+           "dmx_run_multi", "dmx_locate"]
+
+LOC_IGNORE_CASE, LOC_ONLY_POSITIVE = 0x1, 0x2
+HIT_DTYPE = np.dtype([("seq", "<u8"), ("pattern", "<i4"), ("strand", "<i4"), ("start", "<i4"),
+                      ("end", "<i4")])
+assert HIT_DTYPE.itemsize == 24
 
 
 class DmxError(RuntimeError):
@@ -73,6 +78,9 @@ def load() -> ctypes.CDLL:
                             ctypes.POINTER(c_int)]
     L.dmx_device_count.restype = c_int
     L.dmx_run_multi.argtypes = [ctypes.POINTER(P), c_int, P, P, c_u64p, P, c_size, c_size, P, c_u64p, c_size]
+    L.dmx_locate.argtypes = [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int), c_int,
+                             c_int, P, c_u64p, P, c_size, P, c_size,
+                             ctypes.POINTER(ctypes.c_uint64)]
     if L.dmx_abi_version() != 3:
         raise DmxError("libdmx ABI mismatch")
     _lib = L
@@ -193,6 +201,38 @@ class Context:
         out = np.zeros(self._n_loaded, dtype=RESULT_DTYPE)
         self._check(self._L.dmx_fetch(self._h, out.ctypes.data), "dmx_fetch")
         return out
+
+    def locate(self, patterns, ascii_blob: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
+               ignore_case: bool = False, only_positive: bool = False) -> np.ndarray:
+        """Every exact IUPAC occurrence of every pattern (both strands unless only_positive):
+        HIT_DTYPE records sorted as `seqkit locate` prints them — by record, then pattern, '+'
+        hits by start, then '-' hits in the order a scan of the reverse complement meets them
+        (descending positive-strand end)."""
+        pats = [p.encode("ascii") if isinstance(p, str) else bytes(p) for p in patterns]
+        arr = (ctypes.c_char_p * max(len(pats), 1))(*pats)
+        pl = (ctypes.c_int * max(len(pats), 1))(*[len(p) for p in pats])
+        blob = np.ascontiguousarray(ascii_blob, dtype=np.uint8)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lengths, dtype=np.uint32)
+        flags = (LOC_IGNORE_CASE if ignore_case else 0) | (LOC_ONLY_POSITIVE if only_positive
+                                                           else 0)
+        cap = max(1024, len(lens))
+        while True:
+            hits = np.zeros(cap, dtype=HIT_DTYPE)
+            nh = ctypes.c_uint64()
+            self._check(self._L.dmx_locate(self._h, arr, pl, len(pats), flags,
+                                           blob.ctypes.data if len(blob) else None,
+                                           offs.ctypes.data, lens.ctypes.data, len(lens),
+                                           hits.ctypes.data, cap, ctypes.byref(nh)),
+                        "dmx_locate")
+            if nh.value <= cap:
+                hits = hits[:nh.value]
+                break
+            cap = int(nh.value)
+        key2 = np.where(hits["strand"] == 0, hits["start"].astype(np.int64),
+                        -hits["end"].astype(np.int64))
+        order = np.lexsort((key2, hits["strand"], hits["pattern"], hits["seq"]))
+        return hits[order]
 
     def n_counts(self) -> int:
         a1 = 0 if self.mode == MODE_SINGLE else self.panel_sizes[1]

@@ -1,0 +1,169 @@
+"""Residual-primer failsafe (scripts/04_cleaning_primers.sh:397-460): the drop-in `seqkit`
+(subseq -r / locate -d / grep -f) with `locate` on the GPU (libdmx `dmx_locate`), checked against
+the CPU restatement of `seqkit locate -d` (oracle/seqkit_locate.py; parity unpinned: seqkit is
+not installed and the reference ships no seqkit output)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import seqkit_locate as skl
+from dmx import panel
+from dmx.seqkit import region_slice
+from helpers import instantiate
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "nanopore-barcoding-orc_amd", "bin")
+SEQKIT = os.path.join(BIN, "seqkit")
+DATA = os.path.dirname(panel.SP5_FASTA)
+
+
+def _primers():
+    out = []
+    for f in ("COI_primers.fa", "RNA_primers.fa"):
+        for h, s in panel.read_fasta(os.path.join(DATA, f)):
+            s = "".join(s.split())
+            if s:
+                out.append((h.split()[0], s))
+    return out
+
+
+def _write_fasta(path, recs, width=0):
+    with open(path, "w") as fh:
+        for h, s in recs:
+            fh.write(f">{h}\n")
+            if width:
+                for i in range(0, len(s), width):
+                    fh.write(s[i:i + width] + "\n")
+            else:
+                fh.write(s + "\n")
+
+
+def _consensuses(rng, prims, n):
+    prims = [(h, p) for h, p in prims if set(p) <= set("ACGTRYSWKMBDHVN")]
+    """Trimmed consensuses: mostly clean; some keep a (perfect or 1-error) primer copy at an
+    end, on either strand, some carry one deeper than 100 nt (must not be flagged), a few are
+    shorter than 100 nt or lower-case."""
+    recs = []
+    for i in range(n):
+        L = int(rng.integers(20, 900))
+        s = "".join(rng.choice(list("ACGT"), size=L))
+        u = rng.random()
+        p = prims[int(rng.integers(len(prims)))][1]
+        inst = instantiate(rng, p, err=0.0 if rng.random() < 0.7 else 0.04)
+        if rng.random() < 0.5:
+            inst = skl.revcomp(inst)
+        if u < 0.08:
+            s = inst + s
+        elif u < 0.16:
+            s = s + inst
+        elif u < 0.20 and L > 300:
+            s = s[:150] + inst + s[150:]
+        elif u < 0.22:
+            s = s.lower()
+        recs.append((f"cons{i};size={int(rng.integers(1, 500))} extra words", s))
+    return recs
+
+
+# ------------------------------------------------------------------------- CPU -------------
+
+def test_region_slice_semantics():
+    assert region_slice(300, 1, 100) == (0, 100)
+    assert region_slice(300, -100, -1) == (200, 300)
+    assert region_slice(50, 1, 100) == (0, 50)
+    assert region_slice(50, -100, -1) == (0, 50)
+    assert region_slice(10, 13, -1) == (10, 10)
+    assert region_slice(0, 1, 100) == (0, 0)
+
+
+def test_oracle_locate_kats():
+    rows = skl.locate([("s", "AAGCTTAGCT")], [("p", "AGCT")])
+    # '+' at 2-5 and 7-10; AGCT is its own reverse complement, so '-' finds the same places,
+    # reported in the order a scan of the reverse complement meets them
+    assert [(r[3], r[4], r[5]) for r in rows] == [("+", 2, 5), ("+", 7, 10), ("-", 7, 10),
+                                                   ("-", 2, 5)]
+    assert skl.locate([("s", "AAAA")], [("p", "AA")], only_positive=True)[-1][4:6] == (3, 4)
+    assert skl.locate([("s", "ACGU")], [("p", "ACGT")])[0][6] == "ACGU"
+    assert skl.locate([("s", "acgt")], [("p", "ACGT")]) == []
+    assert len(skl.locate([("s", "acgt")], [("p", "ACGT")], ignore_case=True)) == 2
+    assert skl.locate([("s", "ANGT")], [("p", "ANGT")]) == []          # N in a record: no base
+    rows = skl.locate([("s", "AATGCC")], [("p", "RYK")])   # '-': ATT on the rc GGCATT
+    assert [(r[3], r[4], r[5], r[6]) for r in rows] == [("+", 2, 4, "ATG"), ("-", 1, 3, "ATT")]
+
+
+def test_seqkit_cli_host_subcommands(tmp_path):
+    recs = [("a x", "ACGT" * 40), ("b", "AC"), ("c", "")]
+    fa = str(tmp_path / "in.fa")
+    _write_fasta(fa, recs)
+    out = subprocess.run([SEQKIT, "subseq", "-r", "-100:-1", fa], check=True,
+                         capture_output=True).stdout.decode()
+    s = ("ACGT" * 40)[-100:]
+    assert out == f">a x\n{s[:60]}\n{s[60:]}\n>b\nAC\n>c\n"
+    ids = tmp_path / "ids"
+    ids.write_text("seqID\nb\n")
+    out = subprocess.run([SEQKIT, "grep", "-v", "-f", str(ids), fa], check=True,
+                         capture_output=True).stdout.decode()
+    assert out.startswith(">a x\n") and ">b" not in out and ">c\n" in out
+    r = subprocess.run([SEQKIT, "stats", fa], capture_output=True, env={
+        "PATH": BIN + os.pathsep + "/usr/bin:/bin"})
+    assert r.returncode == 2 and b"no other seqkit" in r.stderr
+
+
+# ------------------------------------------------------------------------- GPU -------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("icase,posonly", [(False, False), (True, False), (False, True)])
+def test_gpu_locate_matches_oracle(ctx, icase, posonly):
+    rng = np.random.default_rng(5 + icase + 2 * posonly)
+    prims = _primers() + [("short", "ACG"), ("lc", "acgtn"), ("deg64", "N" * 3 + "ACGTRYKM" * 7
+                                                                + "GAC"), ("u", "ACGU")]
+    recs = _consensuses(rng, prims, 1500) + [("empty", ""), ("one", "A"), ("u", "ACGUACGU"),
+                                             ("allN", "N" * 80), ("mixed", "acgtACGTacgt")]
+    exp = skl.locate(recs, prims, ignore_case=icase, only_positive=posonly)
+    from dmx import lib
+    seqs = [s for _, s in recs]
+    lens = np.array([len(s) for s in seqs], dtype=np.uint32)
+    offs = np.zeros(len(seqs), dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    blob = np.frombuffer("".join(seqs).encode(), dtype=np.uint8)
+    hits = ctx.locate([p for _, p in prims], blob, offs, lens, ignore_case=icase,
+                      only_positive=posonly)
+    got = [(recs[int(h["seq"])][0], prims[int(h["pattern"])][0], "-" if h["strand"] else "+",
+            int(h["start"]), int(h["end"])) for h in hits]
+    assert got == [(r[0], r[1], r[3], r[4], r[5]) for r in exp]
+    assert len(got) > 100
+
+
+@pytest.mark.gpu
+def test_04_failsafe_dropin(tmp_path):
+    """The failsafe's four seqkit calls (04_cleaning_primers.sh:414-436) with our bin first on
+    PATH; the locations TSV and the cleaned FASTA equal what the restated seqkit predicts."""
+    rng = np.random.default_rng(17)
+    prims = _primers()
+    recs = _consensuses(rng, prims, 1200)
+    trimmed = str(tmp_path / "S1_primerless_round1.fasta")
+    _write_fasta(trimmed, recs)
+    primers = str(tmp_path / "primers.fa")
+    _write_fasta(primers, prims)
+    ends, loc = str(tmp_path / "ends.fasta"), str(tmp_path / "loc.tsv")
+    ids, clean = str(tmp_path / "ids.txt"), str(tmp_path / "cleanest.fasta")
+    script = (f"set -euo pipefail\n"
+              f"seqkit subseq -r 1:100 {trimmed} > {ends}\n"
+              f"seqkit subseq -r -100:-1 {trimmed} >> {ends}\n"
+              f"seqkit locate -d --pattern-file {primers} {ends} > {loc}\n"
+              f"cut -f1 {loc} | sort -u > {ids}\n"
+              f"seqkit grep -v -f {ids} {trimmed} > {clean}\n")
+    env = dict(os.environ, PATH=BIN + os.pathsep + os.environ.get("PATH", ""))
+    subprocess.run(["bash", "-c", script], check=True, env=env)
+    end_recs = [(h, s[slice(*region_slice(len(s), 1, 100))]) for h, s in recs] + \
+               [(h, s[slice(*region_slice(len(s), -100, -1))]) for h, s in recs]
+    rows = skl.locate([(h.split()[0], s) for h, s in end_recs], prims)
+    exp_tsv = "seqID\tpatternName\tpattern\tstrand\tstart\tend\tmatched\n" + "".join(
+        "\t".join(str(x) for x in r) + "\n" for r in rows)
+    assert open(loc).read() == exp_tsv
+    flagged = {r[0] for r in rows} | {"seqID"}
+    assert 50 < len(flagged) < 400
+    exp_clean = "".join(f">{h}\n" + "".join(s[i:i + 60] + "\n" for i in range(0, len(s), 60))
+                        for h, s in recs if h.split()[0] not in flagged)
+    assert open(clean).read() == exp_clean

@@ -228,3 +228,25 @@ def test_run_multi_shards_equal_single_context(ctx):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize("where", ["front", "back", "mixed"])
+@pytest.mark.parametrize("e", [0.1, 0.25])
+def test_tie_stress_short_adapters(ctx, where, e):
+    """Short adapters (3..14 nt, some IUPAC) against short reads give many equal-score matches
+    on both strands and across adapters: every cutadapt tie rule (forward over RC on equal
+    score whatever the errors, fewer errors, earlier adapter, earlier cell) is exercised."""
+    rng = np.random.default_rng({"front": 41, "back": 42, "mixed": 43}[where] + int(e * 100))
+    panel = _random_panel(rng, 12, 3, 14, 0.1)
+    seqs = _reads_with(rng, panel, 4000, L=(0, 60), err=0.1)
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    if where == "mixed":
+        wh = [oracle.FRONT if rng.random() < 0.5 else oracle.BACK for _ in panel]
+    else:
+        wh = [oracle.FRONT if where == "front" else oracle.BACK] * len(panel)
+    exp = oracle.run_batch(oracle.Panel(panel, wh, max_errors=e), None, blob, offs, lens,
+                           mode=0, use_rc=True, threads=8)
+    ctx.set_panel_mixed(0, panel, [lib.DMX_FRONT if w == oracle.FRONT else lib.DMX_BACK
+                                   for w in wh], True, e)
+    ctx.set_mode(lib.MODE_SINGLE)
+    _assert_same(ctx.run(lib.pack(blob, offs, lens)), exp)
