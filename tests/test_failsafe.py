@@ -41,10 +41,10 @@ def _write_fasta(path, recs, width=0):
 
 
 def _consensuses(rng, prims, n):
-    prims = [(h, p) for h, p in prims if set(p) <= set("ACGTRYSWKMBDHVN")]
     """Trimmed consensuses: mostly clean; some keep a (perfect or 1-error) primer copy at an
     end, on either strand, some carry one deeper than 100 nt (must not be flagged), a few are
-    shorter than 100 nt or lower-case."""
+    shorter than 100 nt or lower-case.  Primer copies come from the upper-case IUPAC patterns."""
+    prims = [(h, p) for h, p in prims if set(p) <= set("ACGTRYSWKMBDHVN")]
     recs = []
     for i in range(n):
         L = int(rng.integers(20, 900))
