@@ -250,3 +250,59 @@ def test_tie_stress_short_adapters(ctx, where, e):
                                    for w in wh], True, e)
     ctx.set_mode(lib.MODE_SINGLE)
     _assert_same(ctx.run(lib.pack(blob, offs, lens)), exp)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_windowed_path_orientation_ties(ctx, seed):
+    """The shared-suffix window path (real SP5 / SP27rc panels) on reads built to tie across
+    orientations and adapters: one adapter copy on the forward strand and another on the
+    reverse strand (full, partial at a read end, or internal), with 0-8 % edits each."""
+    rng = np.random.default_rng(900 + seed)
+    _, sp5 = panel.load_panel(panel.SP5_FASTA)
+    _, sp27 = panel.load_panel(panel.SP27RC_FASTA)
+    seqs = []
+    for _ in range(6000):
+        body = "".join(rng.choice(list("ACGT"), size=int(rng.integers(60, 400))))
+        pan = sp5 if rng.random() < 0.6 else sp27
+        a = _mutate(rng, pan[int(rng.integers(len(pan)))], float(rng.choice([0, 0.03, 0.08])))
+        b = _mutate(rng, pan[int(rng.integers(len(pan)))], float(rng.choice([0, 0.03, 0.08])))
+        if rng.random() < 0.4:
+            a = a[int(rng.integers(0, len(a) - 3)):]
+        if rng.random() < 0.4:
+            b = b[:int(rng.integers(3, len(b)))]
+        u = rng.random()
+        if u < 0.4:
+            s = a + body + oracle_rc(b)
+        elif u < 0.7:
+            s = oracle_rc(b) + body + a
+        else:
+            s = body[:30] + a + body[30:] + oracle_rc(b)
+        seqs.append(s)
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    for p1, w in ((sp5, oracle.FRONT), (sp27, oracle.BACK)):
+        exp = oracle.run_batch(oracle.Panel(p1, w), None, blob, offs, lens, mode=0, use_rc=True,
+                               threads=8)
+        ctx.set_panel(0, p1, (lib.DMX_FRONT if w == oracle.FRONT else lib.DMX_BACK) | lib.DMX_RC)
+        ctx.set_mode(lib.MODE_SINGLE)
+        _assert_same(ctx.run(lib.pack(blob, offs, lens)), exp)
+    exp = oracle.run_batch(oracle.Panel(sp5, oracle.FRONT), oracle.Panel(sp27, oracle.BACK), blob,
+                           offs, lens, mode=1, use_rc=True, threads=8)
+    ctx.set_panel(0, sp5, lib.DMX_FRONT | lib.DMX_RC)
+    ctx.set_panel(1, sp27, lib.DMX_BACK | lib.DMX_RC)
+    ctx.set_mode(lib.MODE_TWO_ROUND)
+    _assert_same(ctx.run(lib.pack(blob, offs, lens)), exp)
+
+
+def _mutate(rng, a, err):
+    out = []
+    for c in a:
+        r = rng.random()
+        if r < err * 0.6:
+            out.append("ACGT"[int(rng.integers(4))])
+        elif r < err * 0.8:
+            pass
+        elif r < err:
+            out += [c, "ACGT"[int(rng.integers(4))]]
+        else:
+            out.append(c)
+    return "".join(out)
