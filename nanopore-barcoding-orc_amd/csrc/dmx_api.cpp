@@ -71,8 +71,10 @@ int ensure_pipeline(Ctx* c) {
     const bool linked = c->mode == DMX_MODE_LINKED;
     const size_t slots0 = linked ? n * (size_t)std::max(1, c->panel[0].n) : n;
     const size_t items = linked ? slots0 : n;
-    if (c->slot_cap < std::max(slots0, items) || !c->d_res || c->cap_reads < n) {
-        const size_t s = std::max(slots0, items);
+    // non-linked rounds may need one winner slot per (item, orientation): see orient_slot
+    const size_t need = std::max(slots0, items) * (linked ? 1 : 2);
+    if (c->slot_cap < need || !c->d_res || c->cap_reads < n) {
+        const size_t s = need;
         int rc;
         if ((rc = dev_alloc(c, &c->d_res, n))) return rc;
         for (int r = 0; r < 2; ++r) {
@@ -319,6 +321,9 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
             kk = std::max(kk, allow);
             ad.pacc[L] = (int8_t)kk;
         }
+        // score = aligned adapter length - 2 cost - (adapter chars facing a gap) >= L - 3 cost
+        for (int L = 1; L < 72; ++L)
+            if (ad.acc[L] >= 0 && L - 3 * (int)ad.acc[L] <= 0) hp.nonpos = true;
         ad.m = (uint8_t)m;
         ad.k = (uint8_t)k;
         ad.kk = (int8_t)std::min(kk, k);
@@ -517,13 +522,20 @@ int dmx_exec(dmx_ctx* c) {
     CK(hipEventRecord(c->ev[8], st));
     CK(hipMemsetAsync(c->d_counters, 0, 32 * sizeof(uint32_t), st));
     CK(hipMemsetAsync(c->d_counts, 0, c->n_counts * sizeof(unsigned long long), st));
+    // A panel whose accepted matches can score <= 0 keeps one winner per orientation:
+    // ReverseComplementer compares the two orientations' best scores with "no match" = 0, so
+    // a read whose only forward match scores -1 is taken reverse-complemented (and unmatched).
+    for (int r = 0; r < 2; ++r)
+        c->orient_slot[r] = c->mode != DMX_MODE_LINKED && c->panel[r].n_orient == 2 &&
+                            c->panel[r].nonpos;
     const size_t slots0 = c->mode == DMX_MODE_LINKED ? c->n_reads * (size_t)c->panel[0].n
-                                                     : c->n_reads;
+                                                     : c->n_reads * (c->orient_slot[0] ? 2 : 1);
     CK(hipMemsetAsync(c->d_winner[0], 0xFF, slots0 * sizeof(unsigned long long), st));
     if ((rc = launch_round(c, 0, st))) return rc;
     if ((rc = launch_finalize(c, 0, st))) return rc;
     if (c->mode != DMX_MODE_SINGLE) {
-        CK(hipMemsetAsync(c->d_winner[1], 0xFF, c->item_cap * sizeof(unsigned long long), st));
+        CK(hipMemsetAsync(c->d_winner[1], 0xFF, c->item_cap * (c->orient_slot[1] ? 2 : 1) *
+                                                     sizeof(unsigned long long), st));
         if ((rc = launch_round(c, 1, st))) return rc;
         if ((rc = launch_finalize(c, 1, st))) return rc;
     }

@@ -182,15 +182,18 @@ struct Outcome {      // best cell found by the resolve lane of a cluster
 // 64-bit ordering key, smaller = better, matching cutadapt's selection order:
 //   score desc (Aligner.locate / best_match / ReverseComplementer), forward before RC on equal
 //   score, fewer errors, earlier adapter (file order), earlier cell in locate's scan order.
+// Fields (high to low): 127 - score (8 bits: accepted matches may score <= 0 with high error
+// allowances, down to -128), orientation (1), cost (7), adapter (8), scan position (40).
 __host__ __device__ inline uint64_t make_key(int score, int o, int cost, int a, uint64_t t) {
-    return ((uint64_t)(127 - score) << 57) | ((uint64_t)o << 56) | ((uint64_t)cost << 49) |
-           ((uint64_t)a << 41) | (t & ((1ull << 41) - 1));
+    const int s = score < -128 ? -128 : score;
+    return ((uint64_t)(127 - s) << 56) | ((uint64_t)o << 55) | ((uint64_t)cost << 48) |
+           ((uint64_t)a << 40) | (t & ((1ull << 40) - 1));
 }
-__host__ __device__ inline int key_score(uint64_t k) { return 127 - (int)(k >> 57); }
-__host__ __device__ inline int key_orient(uint64_t k) { return (int)((k >> 56) & 1); }
-__host__ __device__ inline int key_cost(uint64_t k) { return (int)((k >> 49) & 127); }
-__host__ __device__ inline int key_adapter(uint64_t k) { return (int)((k >> 41) & 255); }
-__host__ __device__ inline uint64_t key_t(uint64_t k) { return k & ((1ull << 41) - 1); }
+__host__ __device__ inline int key_score(uint64_t k) { return 127 - (int)(k >> 56); }
+__host__ __device__ inline int key_orient(uint64_t k) { return (int)((k >> 55) & 1); }
+__host__ __device__ inline int key_cost(uint64_t k) { return (int)((k >> 48) & 127); }
+__host__ __device__ inline int key_adapter(uint64_t k) { return (int)((k >> 40) & 255); }
+__host__ __device__ inline uint64_t key_t(uint64_t k) { return k & ((1ull << 40) - 1); }
 
 // ---------------------------------------------------------------------------------------------
 // Packed read streams.  seq: 2 bits per nt (16 nt / u32, nt x at bits 2(x%16)); nmask: 1 bit per

@@ -18,6 +18,7 @@ struct HostPanel {
     bool ring_small = true;
     bool filter = false;
     bool verify = false;
+    bool nonpos = false;      // an accepted match may score <= 0 (needs per-orientation winners)
     DevAdapter ad[kMaxAdapters];
 };
 
@@ -47,7 +48,8 @@ struct Ctx {
     int32_t* d_origin[2] = {nullptr, nullptr};
     int32_t* d_lb[2] = {nullptr, nullptr};
     bool ring_small[2] = {true, true};
-    bool band_ok[2] = {true, true};   // every adapter has kk <= 7: banded resolve
+    bool band_ok[2] = {true, true};
+    bool orient_slot[2] = {false, false};   // per round: one winner slot per (item, orientation)   // every adapter has kk <= 7: banded resolve
     bool force_ring = false;          // DMX_RESOLVE=ring (A/B testing)
     size_t slot_cap = 0;
     Cluster* d_cl[2] = {nullptr, nullptr};

@@ -25,6 +25,7 @@ struct RoundArgs {
     uint32_t n_items;            // host count / upper bound
     int32_t T;                   // tasks per item
     int32_t per_task_slot;       // linked round 0: one winner slot per (read, pair)
+    int32_t slot_div;            // > 0: one slot per (item, orientation), sub / slot_div = o
     Cluster* cl;
     Outcome* outc;
     uint32_t* cl_count;
@@ -93,7 +94,8 @@ __device__ __forceinline__ bool task_view(const RoundArgs& R, uint32_t item, int
 }
 
 __device__ __forceinline__ uint32_t slot_of(const RoundArgs& R, uint32_t item, int sub) {
-    return R.per_task_slot ? item * (uint32_t)R.T + (uint32_t)sub : item;
+    if (R.per_task_slot) return item * (uint32_t)R.T + (uint32_t)sub;
+    return R.slot_div ? 2u * item + (uint32_t)(sub >= R.slot_div) : item;
 }
 
 __device__ __forceinline__ void load_panel_lds(const DevPanel* P, uint64_t* s_peq, int8_t* s_acc,
@@ -217,7 +219,7 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
     // 3' adapters: cutadapt also scans the last column (cells (i, n), i < m: adapter prefix
     // aligned at the read end).  Flag it if any such cell would be accepted.
     const uint32_t len = tv.len;
-    if (lastcol && !front && len > 0) {
+    if (lastcol && !front) {   // an empty view too: cells (i, 0) cost i (rate >= 1 accepts)
         int dd = 0;
         int ubl = -128;
         for (int i = 1; i < m; ++i) {
@@ -439,7 +441,7 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
     // 3' adapters: last-column cells (adapter prefix aligned at the read end)
     uint64_t rows = 0;
     const uint32_t len = tv.len;
-    if (lastcol && !front && len > 0) {
+    if (lastcol && !front) {   // an empty view too: cells (i, 0) cost i (rate >= 1 accepts)
         int dd = 0;
         for (int i = 1; i < m; ++i) {
             dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
@@ -804,7 +806,8 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             const uint32_t v = vbeg + vl;
             TaskView tv;
             task_view(R, v / (uint32_t)no, (int)(v % (uint32_t)no) * A, A, tv);
-            cnt[e] = (tv.len + SEG - 1) / SEG;
+            // an empty view of a 3' panel still gets its last-column window (one segment)
+            cnt[e] = tv.len ? (tv.len + SEG - 1) / SEG : (P->where == kFront ? 0u : 1u);
             grp[e] = (int)tv.strand;
         }
         if (grp[e]) sum1 += cnt[e];
@@ -878,7 +881,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             filter_segment(R, tv, P0, P1, S, s_fpeq, s_thr, hbit, kf, kf_far, gap, seg0, st, item,
                            o);
             const uint32_t len = tv.len;
-            if (!front && P1 == len && len > 0) {
+            if (!front && P1 == len) {
                 // 3' panels: the last column (adapter prefix off the read end) is always checked
                 if (S.have && len - S.w2 <= gap) {
                     st.push(make_window(item, o, tv, S.w1, len, 1, S.wb));
@@ -1881,6 +1884,7 @@ struct FinalArgs {
     uint32_t n_reads;
     int32_t mode;
     int32_t A0, A1;             // adapters per panel
+    int32_t oslot;              // this round keeps one winner slot per (item, orientation)
     unsigned long long* counts; // (A0+1)*(A1+1) + 2
     // linked mode
     const unsigned long long* winner0;   // per (read, pair) front winners
@@ -1980,6 +1984,25 @@ __global__ __launch_bounds__(256) void finalize2_linked_kernel(FinalArgs F) {
         if (s_hist[x]) atomicAdd(&F.counts[x * (F.A0 + 1) + x], (unsigned long long)s_hist[x]);
 }
 
+// The winning key of slot base `i` and its orientation.  With one slot per orientation,
+// ReverseComplementer's rule: the reverse complement is used iff its best score is strictly
+// greater than the forward one, an orientation without a match counting 0 — so the chosen
+// orientation may have no match (o = 1, key = none: the read is written reverse-complemented
+// and unmatched).  Returns the index of the chosen slot.
+__device__ __forceinline__ uint32_t pick_winner(const FinalArgs& F, uint32_t i, uint64_t& key,
+                                                int& o) {
+    if (!F.oslot) {
+        key = F.winner[i];
+        o = key != ~0ull ? key_orient(key) : 0;
+        return i;
+    }
+    const uint64_t kf = F.winner[2 * i], kr = F.winner[2 * i + 1];
+    const int sf = kf != ~0ull ? key_score(kf) : 0, sr = kr != ~0ull ? key_score(kr) : 0;
+    o = sr > sf ? 1 : 0;
+    key = o ? kr : kf;
+    return 2 * i + (uint32_t)o;
+}
+
 // Round 0 epilogue (one thread per read): write m1/bin1, build the round-1 view (the
 // round-0-trimmed sequence: FRONT -> view[rstop:], BACK -> view[:rstart]) and queue it.
 __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
@@ -2001,11 +2024,14 @@ __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
         out._pad = 0;
         out.m1 = dmx_match{0, 0, 0, 0, 0, 0};
         out.m2 = out.m1;
-        const uint64_t key = F.winner[r];
+        uint64_t key;
+        int o;
+        const uint32_t ws = pick_winner(F, r, key, o);
+        out.rc1 = (uint8_t)o;
         if (key != ~0ull) {
-            int a, o;
+            int a;
             const uint32_t n = F.lens[r];
-            decode_match(key, F.origin[r], n, F.p0, out.m1, a, o);
+            decode_match(key, F.origin[ws], n, F.p0, out.m1, a, o);
             out.bin1 = (int16_t)a;
             out.rc1 = (uint8_t)o;
             if (F.mode == DMX_MODE_TWO_ROUND) {
@@ -2024,10 +2050,10 @@ __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
             } else {
                 atomicAdd(&s_hist[a + 1], 1u);
             }
-            if (o) atomicAdd(&s_hist[nh], 1u);
         } else {
             atomicAdd(&s_hist[0], 1u);
         }
+        if (o) atomicAdd(&s_hist[nh], 1u);
         F.res[r] = out;
     }
     __syncthreads();
@@ -2054,16 +2080,18 @@ __global__ __launch_bounds__(256) void finalize1_kernel(FinalArgs F) {
     if (i < *F.n_items) {
         const ItemView v = F.items[i];
         dmx_result& out = F.res[v.read];
-        const uint64_t key = F.winner[i];
+        uint64_t key;
+        int o;
+        const uint32_t ws = pick_winner(F, i, key, o);
         int b = -1;
+        out.rc2 = (uint8_t)o;
         if (key != ~0ull) {
-            int a, o;
-            decode_match(key, F.origin[i], v.len, F.p1, out.m2, a, o);
+            int a;
+            decode_match(key, F.origin[ws], v.len, F.p1, out.m2, a, o);
             out.bin2 = (int16_t)a;
-            out.rc2 = (uint8_t)o;
             b = a;
-            if (o) atomicAdd(&s_hist2[nbins], 1u);
         }
+        if (o) atomicAdd(&s_hist2[nbins], 1u);
         atomicAdd(&s_hist2[(out.bin1 + 1) * (F.A1 + 1) + (b + 1)], 1u);
     }
     __syncthreads();
@@ -2091,6 +2119,7 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     const HostPanel& hp = c->panel[round];
     const bool linked = c->mode == DMX_MODE_LINKED;
     R.per_task_slot = (linked && round == 0) ? 1 : 0;
+    R.slot_div = c->orient_slot[round] ? hp.n : 0;
     if (round == 0) {
         R.items = nullptr;
         R.n_items_dev = nullptr;
@@ -2111,7 +2140,9 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     R.origin = c->d_origin[round];
     R.lb = c->d_lb[round];
     if (R.T > kScanBlock) return DMX_E_UNSUPPORTED;
-    hipMemsetAsync(R.lb, 0, sizeof(int32_t) * (round == 0 ? c->slot_cap : c->item_cap), st);
+    hipMemsetAsync(R.lb, 0, sizeof(int32_t) * (round == 0 ? c->slot_cap
+                                                         : c->item_cap * (R.slot_div ? 2 : 1)),
+                   st);
 
     const uint32_t rpb = kScanBlock / R.T;
     const uint32_t grid = (uint32_t)((R.n_items + rpb - 1) / rpb);
@@ -2194,6 +2225,7 @@ int launch_finalize(Ctx* c, int round, hipStream_t st) {
     F.mode = c->mode;
     F.A0 = c->panel[0].n;
     F.A1 = c->mode == DMX_MODE_SINGLE ? 0 : c->panel[1].n;
+    F.oslot = c->orient_slot[round] ? 1 : 0;
     F.counts = c->d_counts;
     F.winner0 = c->d_winner[0];
     F.origin0 = c->d_origin[0];

@@ -206,7 +206,9 @@ def _plan(res, ads, linked, demux, unmatched_to, lens, stats):
         rc = np.zeros(n, dtype=bool)
     else:
         is_front = np.array([a.where == "front" for a in ads] + [False])[bin1]
-        rc = (res["rc1"] == 1) & matched
+        # ReverseComplementer may pick the reverse complement of a read that matches nothing
+        # there (its forward best scored < 0): the unmatched record is then written reversed
+        rc = res["rc1"] == 1
         start = np.where(matched & is_front, m1_rstop, 0)
         stop = np.where(matched & ~is_front, m1_rstart, lens)
     if demux:

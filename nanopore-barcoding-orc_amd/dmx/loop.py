@@ -163,15 +163,18 @@ def run(argv=None) -> int:
                     idx1 = np.where(m1, b1, len(n1) if args.no_cleanup else -1)
                     # unmatched in round 1 is written untrimmed to unknown (--no-cleanup only)
                     s1w = np.where(m1, s1, 0)
-                    o1w = np.where(m1, o1, 0).astype(np.uint8)
+                    o1w = o1.astype(np.uint8)   # an unmatched read may still be taken RC'd
                     sink1.write(batch, idx1, s1w, e1, o1w, o1w)
                     idx2 = np.where(m1, out2[np.maximum(b1, 0), b2 + 1], -1)
                     # round-2 unknown: the round-1 output record, untrimmed by round 2
                     m2 = b2 >= 0
-                    s2w = np.where(m2, s2, s1)
-                    e2w = np.where(m2, e2, e1)
-                    o2w = np.where(m2, o2, o1).astype(np.uint8)
-                    n2w = np.where(m2, nrc2, o1).astype(np.uint8)
+                    # unmatched in round 2 but taken reverse-complemented: RC of the round-1
+                    # record T1 = orient(read, rc1)[s1:n], i.e. orient(read, !rc1)[0 : n - s1]
+                    u2rc = ~m2 & (res["rc2"] == 1)
+                    s2w = np.where(m2, s2, np.where(u2rc, 0, s1))
+                    e2w = np.where(m2, e2, np.where(u2rc, e1 - s1, e1))
+                    o2w = np.where(m2, o2, np.where(u2rc, 1 - o1, o1)).astype(np.uint8)
+                    n2w = np.where(m2, nrc2, o1 + u2rc).astype(np.uint8)
                     sink2.write(batch, idx2, s2w, e2w, o2w, n2w)
                     _round_stats(st1, st2, res, batch.lens, m1, m2, b1, b2, s1, s2w, e2w,
                                  bp2_out, n2_out)
@@ -210,7 +213,7 @@ def run(argv=None) -> int:
 def _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w, bp2_out, n2_out):
     lens = lens.astype(np.int64)
     n = len(res)
-    rc1 = (res["rc1"] == 1) & m1
+    rc1 = res["rc1"] == 1
     st1.n_in += n
     st1.bp_in += int(lens.sum())
     st1.n_with_adapter += int(m1.sum())
@@ -219,7 +222,7 @@ def _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w, bp2_out, n2_
     st1.add_matches(b1[m1], "front", s1[m1], res["m1_errors"].astype(np.int64)[m1])
     # round 2, one report per SP5 bin: its input is that bin's round-1 output
     len1 = lens - s1
-    rc2 = (res["rc2"] == 1) & m2
+    rc2 = (res["rc2"] == 1) & m1
     for i, s in enumerate(st2):
         sel = m1 & (b1 == i)
         if not sel.any():

@@ -110,21 +110,21 @@ def best_match(adapters, where, seq, e=0.1, min_overlap=3):
     return best, bm
 
 
-def demux_round(adapters, where, seq, use_rc=True, e=0.1):
+def demux_round(adapters, where, seq, use_rc=True, e=0.1, min_overlap=3):
     """ReverseComplementer: returns (index, is_rc, match, trimmed_seq)."""
-    af, mf = best_match(adapters, where, seq, e)
+    af, mf = best_match(adapters, where, seq, e, min_overlap)
     ar, mr = (-1, None)
     rc = revcomp(seq)
     if use_rc:
-        ar, mr = best_match(adapters, where, rc, e)
+        ar, mr = best_match(adapters, where, rc, e, min_overlap)
     fs = mf[4] if mf else 0
     rs = mr[4] if mr else 0
     if use_rc and rs > fs:
         a, mt, src, is_rc = ar, mr, rc, True
     else:
         a, mt, src, is_rc = af, mf, seq, False
-    if a < 0:
-        return -1, False, None, seq
+    if a < 0:   # nothing matched in the chosen orientation (may still be the RC read)
+        return -1, is_rc, None, src
     trimmed = src[mt[3]:] if where[a] == FRONT else src[:mt[2]]
     return a, is_rc, mt, trimmed
 

@@ -35,14 +35,14 @@ def oracle_round(records, seqs_panel, where, rc):
     out = {}
     for (name, seq, qual), r in zip(records, res):
         b = int(r["bin1"])
+        if r["rc1"]:   # also for an unmatched read taken reverse-complemented
+            seq = fastx.revcomp(seq.encode()).decode()
+            qual = qual[::-1]
+            name = name + " rc"
         if b < 0:
             out.setdefault(-1, []).append((name[1:] if name.startswith("@") else name, seq,
                                            qual))
             continue
-        if r["rc1"]:
-            seq = fastx.revcomp(seq.encode()).decode()
-            qual = qual[::-1]
-            name = name + " rc"
         if where == oracle.FRONT:
             s0, s1 = int(r["m1_rstop"]), len(seq)
         else:

@@ -231,11 +231,13 @@ def test_run_multi_shards_equal_single_context(ctx):
 
 
 @pytest.mark.parametrize("where", ["front", "back", "mixed"])
-@pytest.mark.parametrize("e", [0.1, 0.25])
-def test_tie_stress_short_adapters(ctx, where, e):
+@pytest.mark.parametrize("e,mo", [(0.1, 3), (0.25, 3), (3, 1), (4, 2)])
+def test_tie_stress_short_adapters(ctx, where, e, mo):
     """Short adapters (3..14 nt, some IUPAC) against short reads give many equal-score matches
     on both strands and across adapters: every cutadapt tie rule (forward over RC on equal
-    score whatever the errors, fewer errors, earlier adapter, earlier cell) is exercised."""
+    score whatever the errors, fewer errors, earlier adapter, earlier cell) is exercised.  With
+    absolute error counts (-e 3 / 4) and short -O, accepted matches can score <= 0, and
+    ReverseComplementer may take an orientation that matches nothing (its "no match" = 0)."""
     rng = np.random.default_rng({"front": 41, "back": 42, "mixed": 43}[where] + int(e * 100))
     panel = _random_panel(rng, 12, 3, 14, 0.1)
     seqs = _reads_with(rng, panel, 4000, L=(0, 60), err=0.1)
@@ -244,10 +246,10 @@ def test_tie_stress_short_adapters(ctx, where, e):
         wh = [oracle.FRONT if rng.random() < 0.5 else oracle.BACK for _ in panel]
     else:
         wh = [oracle.FRONT if where == "front" else oracle.BACK] * len(panel)
-    exp = oracle.run_batch(oracle.Panel(panel, wh, max_errors=e), None, blob, offs, lens,
-                           mode=0, use_rc=True, threads=8)
+    exp = oracle.run_batch(oracle.Panel(panel, wh, max_errors=e, min_overlap=mo), None, blob,
+                           offs, lens, mode=0, use_rc=True, threads=8)
     ctx.set_panel_mixed(0, panel, [lib.DMX_FRONT if w == oracle.FRONT else lib.DMX_BACK
-                                   for w in wh], True, e)
+                                   for w in wh], True, e, mo)
     ctx.set_mode(lib.MODE_SINGLE)
     _assert_same(ctx.run(lib.pack(blob, offs, lens)), exp)
 
@@ -306,3 +308,21 @@ def _mutate(rng, a, err):
         else:
             out.append(c)
     return "".join(out)
+
+
+def test_two_round_nonpositive_scores(ctx):
+    """Both rounds with per-orientation winners (-e 3 on the real panels' 17-nt index parts
+    would not do: short random panels, -O 2): an unmatched read may be taken RC'd in either
+    round, and round 2 runs on whatever round 1 chose."""
+    rng = np.random.default_rng(77)
+    p1, p2 = _random_panel(rng, 6, 4, 9), _random_panel(rng, 6, 4, 9)
+    seqs = _reads_with(rng, p1 + p2, 5000, L=(0, 50), err=0.1)
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    exp = oracle.run_batch(oracle.Panel(p1, oracle.FRONT, max_errors=3, min_overlap=2),
+                           oracle.Panel(p2, oracle.BACK, max_errors=3, min_overlap=2), blob, offs,
+                           lens, mode=1, use_rc=True, threads=8)
+    assert ((exp["bin1"] >= 0) & (exp["bin2"] < 0) & (exp["rc2"] == 1)).any()
+    ctx.set_panel(0, p1, lib.DMX_FRONT | lib.DMX_RC, 3, 2)
+    ctx.set_panel(1, p2, lib.DMX_BACK | lib.DMX_RC, 3, 2)
+    ctx.set_mode(lib.MODE_TWO_ROUND)
+    _assert_same(ctx.run(lib.pack(blob, offs, lens)), exp)
