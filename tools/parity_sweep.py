@@ -124,6 +124,40 @@ def case_random(rng, ctx):
     return len(seqs), compare(got, exp), params, seqs
 
 
+def case_random_pair(rng, ctx):
+    """Two random panels as two rounds (FRONT then BACK) or as linked -g F...R pairs."""
+    linked = bool(rng.random() < 0.4)
+    p1 = random_panel(rng)
+    p2 = random_panel(rng)
+    if linked:
+        k = min(len(p1), len(p2))
+        p1, p2 = p1[:k], p2[:k]
+    e = float(rng.choice([0.05, 0.1, 0.15, 0.2])) if rng.random() < 0.85 else \
+        float(rng.integers(1, 4))
+    mo = int(rng.choice([1, 3, 3, 5]))
+    use_rc = (not linked) and bool(rng.random() < 0.8)
+    seqs = []
+    for s in reads_for(rng, p1 + p2, int(rng.integers(200, 2500))):
+        if linked and rng.random() < 0.6:
+            a = int(rng.integers(len(p1)))
+            s = (rand_seq(rng, int(rng.integers(0, 20))) + mutate(rng, p1[a], 0.05) +
+                 rand_seq(rng, int(rng.integers(0, 200))) + mutate(rng, p2[a], 0.05) +
+                 rand_seq(rng, int(rng.integers(0, 20))))
+        seqs.append(s)
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    exp = oracle.run_batch(oracle.Panel(p1, oracle.FRONT, max_errors=e, min_overlap=mo),
+                           oracle.Panel(p2, oracle.BACK, max_errors=e, min_overlap=mo), blob,
+                           offs, lens, mode=2 if linked else 1, use_rc=use_rc, threads=16)
+    f = lib.DMX_RC if use_rc else 0
+    ctx.set_panel(0, p1, lib.DMX_FRONT | f, e, mo)
+    ctx.set_panel(1, p2, lib.DMX_BACK | f, e, mo)
+    ctx.set_mode(lib.MODE_LINKED if linked else lib.MODE_TWO_ROUND)
+    got = ctx.run(lib.pack(blob, offs, lens))
+    params = dict(kind="pair", linked=linked, panel1=p1, panel2=p2, e=e, min_overlap=mo,
+                  rc=use_rc)
+    return len(seqs), compare(got, exp), params, seqs
+
+
 def case_synth(rng, ctx):
     cfg = str(rng.choice(["c1", "c2", "c2x24", "c4", "c5"]))
     seed = int(rng.integers(1000, 10 ** 6))
@@ -155,7 +189,8 @@ def main():
     bad = []
     with lib.Context(0) as ctx:
         while time.time() - t0 < a.seconds:
-            fn = case_random if rng.random() < 0.75 else case_synth
+            u = rng.random()
+            fn = case_random if u < 0.5 else (case_random_pair if u < 0.8 else case_synth)
             n, idx, params, seqs = fn(rng, ctx)
             cases += 1
             reads += n
