@@ -849,11 +849,29 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     const int kf_far = min(kf, (int)s_pf[71]);
     const uint32_t gap = (uint32_t)P->max_mk;
 
-    for (uint32_t tb = 0; tb < T0 + T1; tb += kScanBlock) {
-        const uint32_t t = tb + threadIdx.x;
-        if (t < T0 + T1) {
-            const int g = t < T0 ? 0 : 1;
-            const uint32_t tt = g ? t - T0 : t;
+    // With both orientations of every item (--rc) the two strand groups have equal segment
+    // counts; then the block's two halves walk them in step (half 0: strand-0 segment tt, half
+    // 1: strand-1 segment tt), so both strands of the same reads are loaded together and the
+    // second load of each byte hits in L2 (strand-major order re-read it from the fabric:
+    // 1.8x the algorithmic bytes).  The strand branch stays wave-uniform.
+    const bool paired = T1 == T0 && T0 > 0;
+    const uint32_t step = paired ? (uint32_t)kScanBlock / 2 : (uint32_t)kScanBlock;
+    const uint32_t total = paired ? T0 : T0 + T1;
+    for (uint32_t tb = 0; tb < total; tb += step) {
+        int g;
+        uint32_t tt;
+        bool valid;
+        if (paired) {
+            g = threadIdx.x >= (uint32_t)kScanBlock / 2 ? 1 : 0;
+            tt = tb + (threadIdx.x & ((uint32_t)kScanBlock / 2 - 1));
+            valid = tt < T0;
+        } else {
+            const uint32_t t = tb + threadIdx.x;
+            valid = t < T0 + T1;
+            g = t < T0 ? 0 : 1;
+            tt = g ? t - T0 : t;
+        }
+        if (valid) {
             // the last view whose segment prefix is <= tt (views of the other strand add 0)
             uint32_t lo = 0, hi = nv;                  // answer in [lo, hi)
             while (hi - lo > 1) {
