@@ -185,12 +185,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    dev = local_rank
+    # DMX_DIST_BACKEND=gloo: rehearse the N-rank path with several ranks sharing the GPUs of a
+    # smaller box (RCCL refuses two ranks on one device); the default is RCCL over xGMI.
+    backend = os.environ.get("DMX_DIST_BACKEND", "nccl")
     if world > 1:
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")   # RCCL over xGMI
+        dev = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        tdist.init_process_group(backend)
         dist = tdist
+    on_gpu = backend == "nccl"
 
     from dmx import lib, synth
     gen_threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
@@ -203,7 +209,7 @@ def main():
     gen_s = time.perf_counter() - t0
 
     linked = args.workload == "c5"
-    ctx = lib.Context(local_rank if world > 1 else 0)
+    ctx = lib.Context(dev)
     if linked:   # 04_cleaning_primers.sh:377: -g F...R per pair, no --rc
         ctx.set_panel(0, d["sp5"], lib.DMX_FRONT, 0.1)
         ctx.set_panel(1, d["sp27"], lib.DMX_BACK, 0.1)
@@ -219,7 +225,8 @@ def main():
         c = ctx.counts()
         if dist is not None:
             import torch
-            t = torch.from_numpy(c.astype(np.int64)).cuda()
+            t = torch.from_numpy(c.astype(np.int64))
+            t = t.cuda() if on_gpu else t
             dist.all_reduce(t)
             c = t.cpu().numpy()
         return c
@@ -267,7 +274,7 @@ def main():
         raise SystemExit(f"pipeline flags {flags}: cluster overflow or window violation")
     if dist is not None:
         import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
