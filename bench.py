@@ -84,6 +84,63 @@ def cpu_baseline(workload: str, threads: int, target_s: float = 12.0):
                       "not installed)"}
 
 
+def chop_cpu_baseline(threads: int, cutoff: float, target_s: float = 12.0):
+    """Oracle primer-hit search (oracle/chop_oracle.c, plain O(mn) DP on pthreads) on a bounded
+    sample of the chop workload.  rank 0, N=1 only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import chopper  # test infrastructure: timed CPU baseline only
+    from dmx import chop, synth
+    primers = chop.load_primers(chop.PRIMERS_FASTA)
+    pilot = synth.generate("c2", n=40 * threads, seed=99)
+    t = time.perf_counter()
+    chopper.batch_hit_counts(primers, cutoff, pilot["blob"], pilot["offsets"], pilot["lengths"],
+                             threads)
+    rate = len(pilot["lengths"]) / (time.perf_counter() - t)
+    n = int(max(500, min(2_000_000, rate * target_s)))
+    d = synth.generate("c2", n=n, seed=98)
+    t = time.perf_counter()
+    chopper.batch_hit_counts(primers, cutoff, d["blob"], d["offsets"], d["lengths"], threads)
+    dt = time.perf_counter() - t
+    return {"value": n / dt / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "port",
+            "sample": f"{n} reads of config 2 (seed 98): hits of SP5, SP27 and their reverse "
+                      f"complements at cutoff {cutoff}, {dt:.1f} s wall on {threads} host threads "
+                      "(oracle/chop_oracle.c, a plain-DP restatement; pychopper / edlib are not "
+                      "installed)"}
+
+
+def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutoff, gen_s):
+    """pychopper-style reorientation (01_pychopper.sh).  Dominant kernel: dmx::chop_kernel."""
+    L = lengths.astype(np.float64)
+    alg_bytes = (float(np.sum(np.ceil(L / 4) + np.ceil(L / 8) + 12.0)) + 8.0 * len(L)
+                 + 16.0 * (n_hits + n_segs))
+    kern_ms = ms["chop"] / K
+    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+    cols = float(np.sum(L + np.maximum(np.ceil(L / 512) - 1, 0) * 116)) * 4   # + warm-up, 4 labels
+    return {
+        "metric": "Mreads/s pychopper-style reorientation (01_pychopper.sh: -m edlib -p, "
+                  "M13 SP5/SP27 primers)",
+        "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
+        "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic",
+        "config": {"workload": f"chop: {args.reads} synthetic ONT reads per GPU (config 2 "
+                               "generator, both orientations), primers "
+                               "M13_seqs_for_pychopper.fa, layout +:SP5,-SP27|-:SP27,-SP5, "
+                               "-p, inputs resident in HBM",
+                   "cutoff": cutoff, "reads_per_gpu": args.reads, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "algorithmic_bytes_per_launch": round(alg_bytes),
+                     "kernel": "dmx::chop_kernel", "avg_launch_ms": round(kern_ms, 3),
+                     "note": "VALU-bound bit-vector scan (DESIGN.md §8d)"},
+        "valu": {"columns_per_s": cols / (kern_ms / 1e3)},
+        "stage_ms_per_step": {k: round(v / K, 3) for k, v in ms.items()},
+        "hits_per_read": round(n_hits / max(1, len(L)), 4),
+        "segments_per_read": round(n_segs / max(1, len(L)), 4),
+        "gen_s": round(gen_s, 1),
+    }
+
+
 def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s,
                    clusters, windows, windows_raw, resolved, traces):
     # roofline of the dominant kernel: the shared-suffix filter (reads every base of every
@@ -174,8 +231,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="c2x24", choices=["c2x24", "c2", "c4", "c1", "c5"],
-                    help="c5 = config 5, linked COI primers (-g F...R) on consensus FASTA")
+    ap.add_argument("--workload", default="c2x24",
+                    choices=["c2x24", "c2", "c4", "c1", "c5", "chop"],
+                    help="c5 = config 5, linked COI primers (-g F...R) on consensus FASTA; "
+                         "chop = pychopper-style reorientation (01_pychopper.sh) of config 2's "
+                         "reads")
     ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -201,15 +261,22 @@ def main():
     from dmx import lib, synth
     gen_threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
     t0 = time.perf_counter()
-    d = synth.generate(args.workload, n=args.reads, first=rank * args.reads,
-                       threads=gen_threads)
+    chop_mode = args.workload == "chop"
+    d = synth.generate("c2" if chop_mode else args.workload, n=args.reads,
+                       first=rank * args.reads, threads=gen_threads)
     packed = lib.pack(d["blob"], d["offsets"], d["lengths"])
+    tune = None
+    if chop_mode:   # the CLI's autotune sample: the first 10000 reads
+        nt = min(10000, len(d["lengths"]))
+        tune = lib.pack(d["blob"], d["offsets"][:nt], d["lengths"][:nt])
     lengths = d["lengths"].copy()
     del d["blob"]
     gen_s = time.perf_counter() - t0
 
     linked = args.workload == "c5"
     ctx = lib.Context(dev)
+    if chop_mode:
+        return chop_main(args, ctx, packed, tune, lengths, gen_s, world, rank, dist, on_gpu)
     if linked:   # 04_cleaning_primers.sh:377: -g F...R per pair, no --rc
         ctx.set_panel(0, d["sp5"], lib.DMX_FRONT, 0.1)
         ctx.set_panel(1, d["sp27"], lib.DMX_BACK, 0.1)
@@ -288,6 +355,57 @@ def main():
                              clusters, windows, windows_raw, resolved, traces)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def chop_main(args, ctx, packed, tune, lengths, gen_s, world, rank, dist, on_gpu):
+    """--workload chop: one step = dmx_chop_exec (primer hits, segments, read-order compaction)
+    over the resident batch; the cutoff is tuned once beforehand the way bin/pychopper does."""
+    from dmx import chop
+    primers = chop.load_primers(chop.PRIMERS_FASTA)
+    with open(chop.CONFIG_FILE) as fh:
+        rules = chop.parse_config(fh.read(), [p[0] for p in primers])
+    ch = chop.Chopper(ctx, primers, rules, True)
+    ctx.load(tune)
+    cutoff = ch.autotune(np.arange(tune.n_reads))
+    ch.set_cutoff(cutoff)
+    ctx.load(packed)
+    del packed
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        ctx.chop_exec()
+    ms = {"chop": 0.0, "order": 0.0}
+    barrier_sync()
+    t = time.perf_counter()
+    tot = (0, 0)
+    for _ in range(args.steps):
+        tot = ctx.chop_exec()
+        st = ctx.chop_stats()
+        ms["chop"] += st["chop"]
+        ms["order"] += st["order"]
+    barrier_sync()
+    elapsed = time.perf_counter() - t
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    K = args.steps
+    value = args.reads * world * K / elapsed / 1e6
+    out = chop_line(args, world, K, value, elapsed, ms, lengths, tot[0], tot[1], cutoff, gen_s)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = chop_cpu_baseline(args.cpu_threads, cutoff)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -161,6 +161,49 @@ int dmx_locate(dmx_ctx* ctx, const char* const* patterns, const int* plens, int 
                int flags, const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens,
                size_t n_seqs, dmx_hit* out, size_t cap, uint64_t* n_hits);
 
+/* ---- Read reorientation, pychopper style (the producer of the demultiplexer's input) ---------
+ * Replaces: the primer search and read segmentation of
+ *   `pychopper -b M13_seqs_for_pychopper.fa -c M13_config_for_pychopper.txt -p -m edlib`
+ * (scripts/01_pychopper.sh:45-57; pychopper 2.7.10 / edlib are not vendored — the semantics are
+ * restated in DESIGN.md §8d, parity unpinned).  Runs on the batch made resident by dmx_load.
+ * Labels: primer p (file order) is label 2p, its reverse complement label 2p+1 (pychopper's
+ * "-NAME").  IUPAC codes in primers (N = any base); a read N matches anything.
+ * Hits: per label, each maximal run of read columns whose least infix edit distance is
+ * <= k = (int)(cutoff * m) gives one hit: the run's first column of least distance (stop) and
+ * the start of the shortest optimal alignment ending there.
+ * Segments: a read's hits sorted by (start, stop, label) are paired greedily left to right;
+ * consecutive hits (a, b) with a rule (rule_left[r], rule_right[r]) form a segment on strand
+ * rule_strand[r] (0 '+', 1 '-'; the first rule of a pair wins) spanning [a.start, b.stop) with
+ * keep_primers (pychopper -p), else [a.stop, b.start) (empty if the hits overlap). */
+#define DMX_CHOP_MAX_PRIMERS 8
+#define DMX_CHOP_MAX_RULES 32
+typedef struct dmx_chop_hit {
+    uint32_t read;
+    int16_t label;
+    int16_t dist;          /* edit distance                                        */
+    int32_t start, stop;   /* [start, stop) on the read as given                   */
+} dmx_chop_hit;
+typedef struct dmx_chop_seg {
+    uint32_t read;
+    int32_t start, stop;   /* [start, stop) on the read as given, stop >= start     */
+    int16_t strand;        /* 0 = '+', 1 = '-' (the segment is written reverse-complemented) */
+    int16_t rule;
+} dmx_chop_seg;
+/* primers: uppercase IUPAC (U -> T), 1..64 nt each; cutoff in [0, 1). */
+int dmx_chop_set(dmx_ctx* ctx, const char* const* primers, const int* plens, int n_primers,
+                 const int* rule_left, const int* rule_right, const int* rule_strand, int n_rules,
+                 double cutoff, int keep_primers);
+/* Hits and segments of every resident read (synchronous); totals in *n_hits / *n_segs. */
+int dmx_chop_exec(dmx_ctx* ctx, uint64_t* n_hits, uint64_t* n_segs);
+/* Results of the last dmx_chop_exec (any pointer may be NULL): per-read segment and hit counts
+ * (n_reads entries each) and the first seg_cap / hit_cap records in read order (within a read:
+ * segments left to right, hits by (start, stop, label)). */
+int dmx_chop_fetch(dmx_ctx* ctx, uint32_t* n_seg, uint32_t* n_hit, dmx_chop_seg* segs,
+                   size_t seg_cap, dmx_chop_hit* hits, size_t hit_cap);
+/* Device time (ms) of the last dmx_chop_exec: [0] chop_kernel (its final launch), [1] the
+ * read-order compaction.  Returns the reads per block the final launch used. */
+int dmx_chop_stats(dmx_ctx* ctx, float* ms, int n_ms);
+
 #ifdef __cplusplus
 }
 #endif

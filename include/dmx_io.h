@@ -73,8 +73,22 @@ int dmx_sink_write(dmx_sink* s, dmx_batch* b, const int32_t* out_idx, const int3
                    const int32_t* stop, const uint8_t* rc, const uint8_t* n_rc);
 /* Wait for pending writes, close every output; n_written / bp_written (n_out entries each,
  * may be NULL) receive the records and bases written per output. */
+/* Row form (pychopper-style outputs, several records per read): row r writes read[r] to output
+ * out_idx[r] (-1 = nothing) as sequence = read[start[r]:stop[r]] (positions on the read as
+ * given), reverse-complemented (qualities reversed) if rc[r]; name = the read's name line when
+ * name_mode[r] == 0, or "{start}:{stop}|{id} strand=+|-{comment}" when name_mode[r] == 1 (id = the
+ * name up to the first blank, comment = the rest of the line).  Rows of one output keep their
+ * order.  Asynchronous like dmx_sink_write. */
+int dmx_sink_write_rows(dmx_sink* s, dmx_batch* b, size_t n_rows, const uint32_t* read,
+                        const int32_t* out_idx, const int32_t* start, const int32_t* stop,
+                        const uint8_t* rc, const uint8_t* name_mode);
 int dmx_sink_close(dmx_sink* s, uint64_t* n_written, uint64_t* bp_written);
 const char* dmx_sink_error(dmx_sink* s);
+
+/* Mean read quality of a FASTQ batch (pychopper -Q): out[i] = -10 log10 of the mean Phred+33
+ * error probability of read i, summed in read order in IEEE double (0 for an empty read).
+ * Returns -2 for a FASTA batch. */
+int dmx_batch_mean_qual(const dmx_batch* b, double* out);
 /* Free a sink after dmx_sink_close (or to abandon it). */
 void dmx_sink_free(dmx_sink* s);
 

@@ -200,6 +200,7 @@ void dmx_close(dmx_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
+    chop_release(c);
     void* bufs[] = {c->d_seq_alloc, c->d_nmask_alloc,     c->d_offs,     c->d_lens,      c->d_res,
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
                     c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_pairs, c->d_counters,

@@ -10,6 +10,8 @@
 
 namespace dmx {
 
+struct ChopState;   // read reorientation (dmx_chop.hip)
+
 struct HostPanel {
     bool sieve = false;       // index screen usable (filter + verify, index blocks <= 32)
     int n = 0;
@@ -73,8 +75,10 @@ struct Ctx {
     hipEvent_t ev[13] = {};   // [3r..3r+2] round r stages, [6+r] finalize, [8] start,
                               // [9+2r] after filter, [10+2r] after verify
     bool executed = false;
+    ChopState* chop = nullptr;   // dmx_chop_* state, created by dmx_chop_set
 };
 
+void chop_release(Ctx* c);
 int launch_round(Ctx* c, int round, hipStream_t st);
 int launch_finalize(Ctx* c, int round, hipStream_t st);
 

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdlib>
 #include <atomic>
 #include <condition_variable>
@@ -917,7 +918,33 @@ struct Job {
     Batch* b = nullptr;
     std::vector<int32_t> idx, start, stop;
     std::vector<uint8_t> rc, nrc;
+    // row mode (dmx_sink_write_rows): row r renders read rread[r]; start/stop are positions on
+    // the read as given (reverse-complemented after cutting when rc); mode 1 names the record
+    // "{start}:{stop}|{id} strand=+|-{comment}"
+    bool rows = false;
+    std::vector<uint32_t> rread;
+    std::vector<uint8_t> mode;
 };
+
+inline uint32_t ndigits(uint32_t v) {
+    uint32_t d = 1;
+    while (v >= 10) {
+        v /= 10;
+        ++d;
+    }
+    return d;
+}
+
+inline uint8_t* put_u32(uint8_t* p, uint32_t v) {
+    uint8_t tmp[10];
+    int n = 0;
+    do {
+        tmp[n++] = (uint8_t)('0' + v % 10);
+        v /= 10;
+    } while (v);
+    while (n) *p++ = tmp[--n];
+    return p;
+}
 
 constexpr size_t kMemberMax = 4u << 20;   // uncompressed bytes per gzip member
 
@@ -985,7 +1012,7 @@ struct dmx_sink {
 
 bool dmx_sink::process(Job& j, std::string& e) {
     Batch* b = j.b;
-    const size_t n = b->n_reads;
+    const size_t n = j.rows ? j.rread.size() : b->n_reads;
     const int nout = (int)outs.size();
     const int nth = (int)std::min<size_t>(threads, std::max<size_t>(1, n / 1024));
     const bool fq = !fasta_out && !b->fasta;
@@ -999,13 +1026,18 @@ bool dmx_sink::process(Job& j, std::string& e) {
         for (size_t r = lo; r < hi; ++r) {
             const int o = j.idx[r];
             if (o < 0) continue;
-            if (o >= nout || j.start[r] < 0 || j.stop[r] < j.start[r] ||
-                (uint32_t)j.stop[r] > b->lens_v[r]) {
+            const size_t ri = j.rows ? j.rread[r] : r;
+            if (o >= nout || ri >= b->n_reads || j.start[r] < 0 || j.stop[r] < j.start[r] ||
+                (uint32_t)j.stop[r] > b->lens_v[ri]) {
                 range_bad = true;
                 continue;
             }
             const uint64_t L = (uint64_t)(j.stop[r] - j.start[r]);
-            const uint64_t h = b->head_v[2 * r + 1] - b->head_v[2 * r] + 3ull * j.nrc[r];
+            const uint64_t hl = b->head_v[2 * ri + 1] - b->head_v[2 * ri];
+            const uint64_t h = (j.rows && j.mode[r] == 1)
+                                   ? hl + ndigits((uint32_t)j.start[r]) +
+                                         ndigits((uint32_t)j.stop[r]) + 2 + 9
+                                   : hl + 3ull * j.nrc[r];
             sz[t][o] += 1 + h + 1 + L + 1 + (fq ? 2 + L + 1 : 0);
             cnt[t][o] += 1;
             bps[t][o] += L;
@@ -1029,19 +1061,39 @@ bool dmx_sink::process(Job& j, std::string& e) {
         for (size_t r = lo; r < hi; ++r) {
             const int o = j.idx[r];
             if (o < 0) continue;
+            const size_t ri = j.rows ? j.rread[r] : r;
             uint8_t* p = w[o];
             *p++ = fq ? '@' : '>';
-            const uint64_t hs = b->head_v[2 * r], he = b->head_v[2 * r + 1];
-            memcpy(p, tx + hs, he - hs);
-            p += he - hs;
-            for (int k = 0; k < j.nrc[r]; ++k) {
-                memcpy(p, " rc", 3);
-                p += 3;
+            const uint64_t hs = b->head_v[2 * ri], he = b->head_v[2 * ri + 1];
+            if (j.rows && j.mode[r] == 1) {   // segment of a read: "start:stop|id strand=+ ..."
+                p = put_u32(p, (uint32_t)j.start[r]);
+                *p++ = ':';
+                p = put_u32(p, (uint32_t)j.stop[r]);
+                *p++ = '|';
+                uint64_t cut = hs;
+                while (cut < he && tx[cut] != ' ' && tx[cut] != '\t') ++cut;
+                memcpy(p, tx + hs, cut - hs);
+                p += cut - hs;
+                memcpy(p, j.rc[r] ? " strand=-" : " strand=+", 9);
+                p += 9;
+                memcpy(p, tx + cut, he - cut);
+                p += he - cut;
+            } else {
+                memcpy(p, tx + hs, he - hs);
+                p += he - hs;
+                for (int k = 0; k < j.nrc[r]; ++k) {
+                    memcpy(p, " rc", 3);
+                    p += 3;
+                }
             }
             *p++ = '\n';
-            const uint32_t a = (uint32_t)j.start[r], z = (uint32_t)j.stop[r];
-            const uint8_t* s = st + b->seq_v[2 * r];
-            const uint32_t len = b->lens_v[r];
+            const uint32_t len = b->lens_v[ri];
+            uint32_t a = (uint32_t)j.start[r], z = (uint32_t)j.stop[r];
+            if (j.rows && j.rc[r]) {   // row coordinates are on the read as given
+                a = len - (uint32_t)j.stop[r];
+                z = len - (uint32_t)j.start[r];
+            }
+            const uint8_t* s = st + b->seq_v[2 * ri];
             if (!j.rc[r]) {
                 memcpy(p, s + a, z - a);
                 p += z - a;
@@ -1052,7 +1104,7 @@ bool dmx_sink::process(Job& j, std::string& e) {
             if (fq) {
                 *p++ = '+';
                 *p++ = '\n';
-                const uint8_t* q = tx + b->qual_v[2 * r];
+                const uint8_t* q = tx + b->qual_v[2 * ri];
                 if (!j.rc[r]) {
                     memcpy(p, q + a, z - a);
                     p += z - a;
@@ -1178,6 +1230,36 @@ int dmx_sink_open(const char* const* paths, int n_out, int fasta_out, int level,
     return 0;
 }
 
+}  // extern "C"
+
+namespace {
+
+int sink_enqueue(dmx_sink* s, Batch* b, std::unique_ptr<Job> j) {
+    std::unique_lock<std::mutex> lk(s->mu);
+    s->cv.wait(lk, [&] { return !s->busy; });
+    if (!s->err.empty()) {
+        s->api_err = s->err;
+        return -3;
+    }
+    b->refs.fetch_add(1);
+    j->b = b;
+    s->pending = std::move(j);
+    s->busy = true;
+    s->cv.notify_all();
+    return 0;
+}
+
+struct QualTable {
+    double p[256];
+    QualTable() {
+        for (int i = 0; i < 256; ++i) p[i] = std::pow(10.0, -((double)i - 33.0) / 10.0);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
 int dmx_sink_write(dmx_sink* s, dmx_batch* bp, const int32_t* out_idx, const int32_t* start,
                    const int32_t* stop, const uint8_t* rc, const uint8_t* n_rc) {
     if (!s || !bp || s->closed || !s->th.joinable()) return -1;
@@ -1190,17 +1272,50 @@ int dmx_sink_write(dmx_sink* s, dmx_batch* bp, const int32_t* out_idx, const int
     j->stop.assign(stop, stop + n);
     j->rc.assign(rc, rc + n);
     j->nrc.assign(n_rc, n_rc + n);
-    std::unique_lock<std::mutex> lk(s->mu);
-    s->cv.wait(lk, [&] { return !s->busy; });
-    if (!s->err.empty()) {
-        s->api_err = s->err;
-        return -3;
-    }
-    b->refs.fetch_add(1);
-    j->b = b;
-    s->pending = std::move(j);
-    s->busy = true;
-    s->cv.notify_all();
+    return sink_enqueue(s, b, std::move(j));
+}
+
+int dmx_sink_write_rows(dmx_sink* s, dmx_batch* bp, size_t n_rows, const uint32_t* read,
+                        const int32_t* out_idx, const int32_t* start, const int32_t* stop,
+                        const uint8_t* rc, const uint8_t* name_mode) {
+    if (!s || !bp || s->closed || !s->th.joinable()) return -1;
+    if (n_rows && (!read || !out_idx || !start || !stop || !rc || !name_mode)) return -1;
+    Batch* b = static_cast<Batch*>(bp);
+    auto j = std::make_unique<Job>();
+    j->rows = true;
+    j->rread.assign(read, read + n_rows);
+    j->idx.assign(out_idx, out_idx + n_rows);
+    j->start.assign(start, start + n_rows);
+    j->stop.assign(stop, stop + n_rows);
+    j->rc.assign(rc, rc + n_rows);
+    j->mode.assign(name_mode, name_mode + n_rows);
+    j->nrc.assign(n_rows, 0);
+    return sink_enqueue(s, b, std::move(j));
+}
+
+int dmx_batch_mean_qual(const dmx_batch* bp, double* out) {
+    if (!bp) return -1;
+    const Batch* b = static_cast<const Batch*>(bp);
+    if (b->fasta) return -2;
+    const size_t n = b->n_reads;
+    if (n && !out) return -1;
+    static const QualTable qt;
+    const int nth = (int)std::min<size_t>(std::min(clamp_threads(0), 16),
+                                          std::max<size_t>(1, n / 4096));
+    parallel(nth, [&](int t) {
+        const size_t lo = n * t / nth, hi = n * (t + 1) / nth;
+        for (size_t r = lo; r < hi; ++r) {
+            const uint32_t len = b->lens_v[r];
+            if (!len) {
+                out[r] = 0.0;
+                continue;
+            }
+            const uint8_t* q = b->text_v.data() + b->qual_v[2 * r];
+            double sum = 0.0;
+            for (uint32_t k = 0; k < len; ++k) sum += qt.p[q[k]];
+            out[r] = -10.0 * std::log10(sum / (double)len);
+        }
+    });
     return 0;
 }
 

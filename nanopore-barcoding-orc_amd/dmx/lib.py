@@ -29,12 +29,20 @@ assert RESULT_DTYPE.itemsize == 40
 EXPORTS = ["dmx_abi_version", "dmx_open", "dmx_close", "dmx_last_error", "dmx_set_panel",
            "dmx_set_panel_mixed", "dmx_set_mode", "dmx_pack_words", "dmx_pack", "dmx_run", "dmx_load", "dmx_exec",
            "dmx_sync", "dmx_fetch", "dmx_counts", "dmx_stats", "dmx_device_count",
-           "dmx_run_multi", "dmx_locate"]
+           "dmx_run_multi", "dmx_locate", "dmx_chop_set", "dmx_chop_exec", "dmx_chop_fetch",
+           "dmx_chop_stats"]
 
 LOC_IGNORE_CASE, LOC_ONLY_POSITIVE = 0x1, 0x2
 HIT_DTYPE = np.dtype([("seq", "<u8"), ("pattern", "<i4"), ("strand", "<i4"), ("start", "<i4"),
                       ("end", "<i4")])
 assert HIT_DTYPE.itemsize == 24
+
+# include/dmx.h dmx_chop_hit / dmx_chop_seg (pychopper-style reorientation)
+CHOP_HIT_DTYPE = np.dtype([("read", "<u4"), ("label", "<i2"), ("dist", "<i2"), ("start", "<i4"),
+                           ("stop", "<i4")])
+CHOP_SEG_DTYPE = np.dtype([("read", "<u4"), ("start", "<i4"), ("stop", "<i4"),
+                           ("strand", "<i2"), ("rule", "<i2")])
+assert CHOP_HIT_DTYPE.itemsize == 16 and CHOP_SEG_DTYPE.itemsize == 16
 
 
 class DmxError(RuntimeError):
@@ -82,6 +90,12 @@ def load() -> ctypes.CDLL:
     L.dmx_locate.argtypes = [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int), c_int,
                              c_int, P, c_u64p, P, c_size, P, c_size,
                              ctypes.POINTER(ctypes.c_uint64)]
+    L.dmx_chop_set.argtypes = [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int), c_int,
+                               ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                               ctypes.POINTER(c_int), c_int, ctypes.c_double, c_int]
+    L.dmx_chop_exec.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    L.dmx_chop_fetch.argtypes = [P, P, P, P, c_size, P, c_size]
+    L.dmx_chop_stats.argtypes = [P, ctypes.POINTER(ctypes.c_float), c_int]
     if L.dmx_abi_version() != 3:
         raise DmxError("libdmx ABI mismatch")
     _lib = L
@@ -184,6 +198,7 @@ class Context:
         self._check(self._L.dmx_run(self._h, p.seq2b.ctypes.data, p.nmask.ctypes.data,
                                     p.offsets.ctypes.data, p.lengths.ctypes.data, p.n_words,
                                     p.n_reads, out.ctypes.data), "dmx_run")
+        self._n_loaded = p.n_reads
         return out
 
     def load(self, p: Packed):
@@ -234,6 +249,50 @@ class Context:
                         -hits["end"].astype(np.int64))
         order = np.lexsort((key2, hits["strand"], hits["pattern"], hits["seq"]))
         return hits[order]
+
+    # ---- pychopper-style reorientation (include/dmx.h dmx_chop_*) --------------
+    def chop_set(self, primers, rules, cutoff: float, keep_primers: bool = True):
+        """primers: IUPAC strings (label 2p = primer p, 2p+1 = its reverse complement);
+        rules: [(left label, right label, strand 0 '+' / 1 '-')]; cutoff: maximum edit distance
+        as a fraction of the primer length; keep_primers: pychopper -p."""
+        seqs = [s.encode("ascii") for s in primers]
+        arr = (ctypes.c_char_p * max(len(seqs), 1))(*seqs)
+        lens = (ctypes.c_int * max(len(seqs), 1))(*[len(s) for s in seqs])
+        nr = len(rules)
+        rl = (ctypes.c_int * max(nr, 1))(*[int(r[0]) for r in rules])
+        rr = (ctypes.c_int * max(nr, 1))(*[int(r[1]) for r in rules])
+        rs = (ctypes.c_int * max(nr, 1))(*[int(r[2]) for r in rules])
+        self._check(self._L.dmx_chop_set(self._h, arr, lens, len(seqs), rl, rr, rs, nr,
+                                         float(cutoff), int(bool(keep_primers))), "dmx_chop_set")
+
+    def chop_exec(self):
+        """Hits and segments of the resident batch (after load); returns (n_hits, n_segs)."""
+        nh, ns = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self._L.dmx_chop_exec(self._h, ctypes.byref(nh), ctypes.byref(ns)),
+                    "dmx_chop_exec")
+        self._chop_tot = (int(nh.value), int(ns.value))
+        return self._chop_tot
+
+    def chop_fetch(self, segs: bool = True, hits: bool = False):
+        """(segments per read, hits per read, CHOP_SEG_DTYPE records, CHOP_HIT_DTYPE records),
+        records in read order."""
+        nh, ns = self._chop_tot
+        n = getattr(self, "_n_loaded", 0)
+        nseg = np.zeros(n, dtype=np.uint32)
+        nhit = np.zeros(n, dtype=np.uint32)
+        sg = np.zeros(ns if segs else 0, dtype=CHOP_SEG_DTYPE)
+        ht = np.zeros(nh if hits else 0, dtype=CHOP_HIT_DTYPE)
+        self._check(self._L.dmx_chop_fetch(self._h, nseg.ctypes.data if n else None,
+                                           nhit.ctypes.data if n else None,
+                                           sg.ctypes.data if len(sg) else None, len(sg),
+                                           ht.ctypes.data if len(ht) else None, len(ht)),
+                    "dmx_chop_fetch")
+        return nseg, nhit, sg, ht
+
+    def chop_stats(self):
+        ms = (ctypes.c_float * 2)()
+        rpb = self._check(self._L.dmx_chop_stats(self._h, ms, 2), "dmx_chop_stats")
+        return {"chop": float(ms[0]), "order": float(ms[1]), "reads_per_block": int(rpb)}
 
     def n_counts(self) -> int:
         a1 = 0 if self.mode == MODE_SINGLE else self.panel_sizes[1]

@@ -19,7 +19,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 IO_PATH = os.path.join(HERE, "libdmx_io.so")
 IO_EXPORTS = ["dmx_io_abi_version", "dmx_reader_open", "dmx_reader_next", "dmx_reader_error",
               "dmx_reader_close", "dmx_batch_free", "dmx_sink_open", "dmx_sink_write",
-              "dmx_sink_close", "dmx_sink_error", "dmx_sink_free"]
+              "dmx_sink_close", "dmx_sink_error", "dmx_sink_free", "dmx_sink_write_rows",
+              "dmx_batch_mean_qual"]
 
 
 class _CBatch(ctypes.Structure):
@@ -55,6 +56,8 @@ def load() -> ctypes.CDLL:
     L.dmx_sink_open.argtypes = [ctypes.POINTER(ctypes.c_char_p), c_int, c_int, c_int, c_int,
                                 ctypes.POINTER(P)]
     L.dmx_sink_write.argtypes = [P, ctypes.POINTER(_CBatch), P, P, P, P, P]
+    L.dmx_sink_write_rows.argtypes = [P, ctypes.POINTER(_CBatch), c_size, P, P, P, P, P, P]
+    L.dmx_batch_mean_qual.argtypes = [ctypes.POINTER(_CBatch), P]
     L.dmx_sink_close.argtypes = [P, P, P]
     L.dmx_sink_error.argtypes = [P]
     L.dmx_sink_error.restype = ctypes.c_char_p
@@ -107,6 +110,14 @@ class NativeBatch:
 
     def quality(self, i):
         return None if self.qual is None else self._bytes(self._text, *self.qual[i])
+
+    def mean_qual(self) -> np.ndarray:
+        """Per-read mean quality (pychopper -Q): -10 log10 of the mean error probability."""
+        out = np.zeros(self.n, dtype=np.float64)
+        rc = load().dmx_batch_mean_qual(self._ptr, out.ctypes.data if self.n else None)
+        if rc != 0:
+            raise ValueError("mean quality needs FASTQ input")
+        return out
 
     def free(self):
         if self._ptr is not None:
@@ -185,6 +196,20 @@ class Sink:
             if len(a) != n:
                 raise ValueError("per-read arrays must have one entry per read")
         r = self._L.dmx_sink_write(self._h, batch._ptr, *[a.ctypes.data for a in arrs])
+        if r != 0:
+            raise OSError(self._L.dmx_sink_error(self._h).decode())
+
+    def write_rows(self, batch: NativeBatch, read, out_idx, start, stop, rc, name_mode):
+        """Several records per read (include/dmx_io.h dmx_sink_write_rows): row r writes
+        read[r][start[r]:stop[r]] (positions on the read as given; reverse-complemented if
+        rc[r]) to output out_idx[r]; name_mode 1 names it "start:stop|id strand=+|- ..."."""
+        arrs = [np.ascontiguousarray(read, np.uint32), np.ascontiguousarray(out_idx, np.int32),
+                np.ascontiguousarray(start, np.int32), np.ascontiguousarray(stop, np.int32),
+                np.ascontiguousarray(rc, np.uint8), np.ascontiguousarray(name_mode, np.uint8)]
+        n = len(arrs[0])
+        if any(len(a) != n for a in arrs):
+            raise ValueError("row arrays must have equal lengths")
+        r = self._L.dmx_sink_write_rows(self._h, batch._ptr, n, *[a.ctypes.data for a in arrs])
         if r != 0:
             raise OSError(self._L.dmx_sink_error(self._h).decode())
 

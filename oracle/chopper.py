@@ -1,0 +1,251 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.  CPU restatement of the pychopper-style read
+reorientation of scripts/01_pychopper.sh:45-57:
+
+    pychopper -b M13_seqs_for_pychopper.fa -c M13_config_for_pychopper.txt -k LSK114 -Q 10
+              -w RESCUED -u UNCLASS -l SHORT -S STATS -p -t 24 -m edlib IN > PASS
+
+pychopper 2.7.10 and edlib are not vendored in /root/reference and not installed here, and the
+reference holds no pychopper output: PARITY UNPINNED.  The semantics are the build's definition
+(DESIGN.md §8d), restated from edlib's HW ("infix") alignment mode and pychopper's documented
+options:
+
+  labels    primer p of the -b FASTA (file order; name = first header word) is label 2p
+            ("NAME"), its reverse complement label 2p+1 ("-NAME", the config's notation)
+  hits      per label: every maximal run of read columns j with D(j) <= int(cutoff * m), D(j)
+            = least edit distance of the label ending at column j (IUPAC codes; a read N
+            matches anything); hit = the run's first column of least D (stop) and the start of
+            the shortest optimal alignment ending there — oracle/chop_oracle.c (plain O(mn) DP)
+            or `hits_py` (pure Python, tiny cases)
+  segments  a read's hits sorted by (start, stop, label) are paired greedily left to right by
+            the config rules (M13_config_for_pychopper.txt:1 "+:SP5,-SP27|-:SP27,-SP5"); span
+            [a.start, b.stop) with -p (keep primers), else [a.stop, b.start) (empty if they
+            overlap)
+  classes   FASTQ mean quality (-10 log10 of the mean error probability) < -Q -> qcfail;
+            0 segments -> unclassified (record unchanged); 1 -> pass (short if < -z);
+            >= 2 -> every segment rescued (short if < -z); '-' segments reverse-complemented;
+            segment records named "{start}:{stop}|{id} strand=+|-" + the original comment
+  autotune  without -q: the cutoff of 0.05, 0.10, ..., 0.40 giving the most reads with a
+            segment among the first -Y QC-passing reads (ties -> the smaller)
+
+Only tests/ (and bench.py's cpu_baseline leg, through `batch_hit_counts`) use this module, as
+the checker of libdmx's `dmx_chop_*` (HIP) path and of the `bin/pychopper` drop-in.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+
+import oracle as _orc
+
+AUTOTUNE_CUTOFFS = (0.05, 0.1, 0.15, 0.2, 0.25, 0.3, 0.35, 0.4)
+
+_COMP = str.maketrans("ACGTUMRWSYKVHDBNacgtumrwsykvhdbn", "TGCAAKYWSRMBDHVNtgcaakywsrmbdhvn")
+_IUPAC = {"A": "A", "C": "C", "G": "G", "T": "T", "U": "T", "R": "AG", "Y": "CT", "S": "CG",
+          "W": "AT", "K": "GT", "M": "AC", "B": "CGT", "D": "AGT", "H": "ACT", "V": "ACG",
+          "N": "ACGT"}
+_ready = False
+
+
+def revcomp(s: str) -> str:
+    return s.translate(_COMP)[::-1]
+
+
+def labels(primers):
+    """[(name, seq)] -> [(label name, seq)]: NAME, -NAME per primer, in file order."""
+    out = []
+    for name, seq in primers:
+        s = seq.upper().replace("U", "T")
+        out += [(name, s), ("-" + name, revcomp(s))]
+    return out
+
+
+def parse_config(text: str, names):
+    """"+:SP5,-SP27|-:SP27,-SP5" -> [(left label, right label, strand 0 '+' / 1 '-')]."""
+    idx = {}
+    for p, nm in enumerate(names):
+        idx[nm] = 2 * p
+        idx["-" + nm] = 2 * p + 1
+    rules = []
+    for part in text.strip().split("|"):
+        strand, pair = part.split(":", 1)
+        a, b = (x.strip() for x in pair.split(","))
+        rules.append((idx[a], idx[b], 0 if strand.strip() == "+" else 1))
+    return rules
+
+
+def _lib():
+    global _ready
+    L = _orc.lib()
+    if not _ready:
+        L.orc_chop_hits.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_double,
+                                    ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        L.orc_chop_batch.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int),
+                                     ctypes.c_int, ctypes.c_double, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_int, ctypes.c_void_p]
+        _ready = True
+    return L
+
+
+def hits_c(pat: str, read: str, cutoff: float):
+    """[(start, stop, dist)] of one label in one read, in stop order (oracle/chop_oracle.c)."""
+    L = _lib()
+    cap = 64
+    while True:
+        buf = np.zeros(3 * cap, dtype=np.int32)
+        nh = L.orc_chop_hits(pat.encode(), len(pat), float(cutoff), read.encode(), len(read),
+                             buf.ctypes.data, cap)
+        if nh < 0:
+            raise ValueError(f"bad primer {pat!r}")
+        if nh <= cap:
+            break
+        cap = nh
+    return [(int(buf[3 * i + 1]), int(buf[3 * i]), int(buf[3 * i + 2])) for i in range(nh)]
+
+
+def _eq(p: str, r: str) -> bool:
+    return r not in "ACGT" or r in _IUPAC[p]
+
+
+def _global(pat: str, txt: str) -> int:
+    prev = list(range(len(pat) + 1))
+    for t, ch in enumerate(txt, 1):
+        cur = [t]
+        for i in range(1, len(pat) + 1):
+            cur.append(min(prev[i - 1] + (0 if _eq(pat[i - 1], ch) else 1), cur[i - 1] + 1,
+                           prev[i] + 1))
+        prev = cur
+    return prev[-1]
+
+
+def hits_py(pat: str, read: str, cutoff: float):
+    """Pure-Python full-matrix version of hits_c (tiny cases only)."""
+    m, n = len(pat), len(read)
+    k = int(cutoff * m)
+    R = read.upper()
+    col = list(range(m + 1))
+    D = [m]
+    for j in range(1, n + 1):
+        cur = [0]
+        for i in range(1, m + 1):
+            cur.append(min(col[i - 1] + (0 if _eq(pat[i - 1], R[j - 1]) else 1), cur[i - 1] + 1,
+                           col[i] + 1))
+        col = cur
+        D.append(col[m])
+    out, j = [], 1
+    while j <= n:
+        if D[j] > k:
+            j += 1
+            continue
+        e = j
+        while e < n and D[e + 1] <= k:
+            e += 1
+        best = min(D[j:e + 1])
+        stop = D.index(best, j, e + 1)
+        start = next(s for s in range(stop, -1, -1) if _global(pat, R[s:stop]) == best)
+        out.append((start, stop, best))
+        j = e + 1
+    return out
+
+
+def read_hits(labs, read: str, cutoff: float, impl=None):
+    """All hits of one read: [(start, stop, label, dist)] sorted by (start, stop, label)."""
+    impl = impl or hits_c
+    out = []
+    for li, (_, pat) in enumerate(labs):
+        out += [(s, e, li, d) for s, e, d in impl(pat, read, cutoff)]
+    out.sort()
+    return out
+
+
+def segments(hits, rules, keep: bool):
+    """Greedy left-to-right pairing: [(start, stop, strand, rule)]."""
+    table = {}
+    for r, (a, b, st) in enumerate(rules):
+        table.setdefault((a, b), (r, st))
+    segs, i = [], 0
+    while i + 1 < len(hits):
+        h1, h2 = hits[i], hits[i + 1]
+        rs = table.get((h1[2], h2[2]))
+        if rs is None:
+            i += 1
+            continue
+        a = h1[0] if keep else h1[1]
+        b = h2[1] if keep else h2[0]
+        segs.append((a, max(a, b), rs[1], rs[0]))
+        i += 2
+    return segs
+
+
+def mean_qual(qual: str) -> float:
+    """-10 log10 of the mean Phred+33 error probability, summed in read order."""
+    if not qual:
+        return 0.0
+    s = 0.0
+    for c in qual:
+        s += 10.0 ** (-(ord(c) - 33) / 10.0)
+    return -10.0 * math.log10(s / len(qual))
+
+
+def seg_name(head: str, a: int, b: int, strand: int) -> str:
+    cut = len(head)
+    for i, ch in enumerate(head):
+        if ch in " \t":
+            cut = i
+            break
+    return f"{a}:{b}|{head[:cut]} strand={'-' if strand else '+'}{head[cut:]}"
+
+
+def chop_records(records, primers, config: str, cutoff: float, keep: bool = True,
+                 min_qual: float = 7.0, min_len: int = 50, fasta: bool = False):
+    """records [(header, seq, qual-or-None)] -> {pass, rescued, unclass, short, qcfail}:
+    lists of (header, seq, qual) in input order."""
+    labs = labels(primers)
+    rules = parse_config(config, [p[0] for p in primers])
+    out = {k: [] for k in ("pass", "rescued", "unclass", "short", "qcfail")}
+    for head, seq, qual in records:
+        if not fasta and mean_qual(qual) < min_qual:
+            out["qcfail"].append((head, seq, qual))
+            continue
+        segs = segments(read_hits(labs, seq, cutoff), rules, keep)
+        if not segs:
+            out["unclass"].append((head, seq, qual))
+            continue
+        dest = "pass" if len(segs) == 1 else "rescued"
+        for a, b, st, _ in segs:
+            s = seq[a:b]
+            q = qual[a:b] if qual is not None else None
+            if st:
+                s = revcomp(s)
+                q = q[::-1] if q is not None else None
+            out[dest if b - a >= min_len else "short"].append((seg_name(head, a, b, st), s, q))
+    return out
+
+
+def autotune(records, primers, config: str, keep: bool = True, min_qual: float = 7.0,
+             sample: int = 10000, fasta: bool = False) -> float:
+    labs = labels(primers)
+    rules = parse_config(config, [p[0] for p in primers])
+    pool = [s for _, s, q in records if fasta or mean_qual(q) >= min_qual][:sample]
+    best, best_n = None, -1
+    for q in AUTOTUNE_CUTOFFS:
+        c = sum(1 for s in pool if segments(read_hits(labs, s, q), rules, keep))
+        if c > best_n:
+            best, best_n = q, c
+    return best
+
+
+def batch_hit_counts(primers, cutoff: float, blob, offsets, lengths, threads: int):
+    """Per-read hit counts over all labels, on `threads` pthreads (the bench's CPU baseline)."""
+    labs = labels(primers)
+    arr = (ctypes.c_char_p * len(labs))(*[s.encode() for _, s in labs])
+    pl = (ctypes.c_int * len(labs))(*[len(s) for _, s in labs])
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(lengths, dtype=np.uint32)
+    out = np.zeros(len(lens), dtype=np.int32)
+    _lib().orc_chop_batch(arr, pl, len(labs), float(cutoff), blob.ctypes.data, offs.ctypes.data,
+                          lens.ctypes.data, len(lens), int(threads), out.ctypes.data)
+    return out
