@@ -37,13 +37,16 @@
 //                 move every block's ranges into read order (block order = read order), so the
 //                 host receives read-ordered hits and segments without a sort.
 // A block whose hits overflow its LDS list (reads with hundreds of primer hits) is re-run with
-// fewer reads per block (64 -> 8 -> 1); a staging overflow re-runs with larger buffers.
+// fewer reads per block (64 -> 8 -> 1); a single read that still overflows is redone by
+// chop_big_kernel (one block per such read, hit list in global memory sized by the exact count
+// the LDS pass measured, parallel rank sort); a staging overflow re-runs with larger buffers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstddef>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "dmx_internal.h"
 
@@ -82,7 +85,10 @@ struct ChopArgs {
     uint32_t* nhit;            // per read
     uint32_t* nseg;
     uint32_t* blk;             // per block: hit base, hits, segment base, segments
-    unsigned long long* ctr;   // [0] hits, [1] segments, [2] flags (bit 0: LDS list overflow)
+    unsigned long long* ctr;   // [0] hits, [1] segments, [2] flags (bit 0: LDS list overflow),
+                               // [3] reads overflowing alone (rpb == 1)
+    uint32_t* ovf;             // rpb == 1: (read, exact hit count) of each overflowing read
+    uint64_t ovf_cap;
 };
 
 struct ChopOrderArgs {
@@ -95,10 +101,10 @@ struct ChopOrderArgs {
     dmx_chop_seg* segs;
 };
 
-__device__ __forceinline__ void chop_push(uint32_t* s_nh, dmx_chop_hit* s_hit, uint32_t read,
-                                          int lab, int dist, uint32_t stop) {
-    const uint32_t i = atomicAdd(s_nh, 1u);
-    if (i < kChopHitCap) {
+__device__ __forceinline__ void chop_push(uint32_t* s_nh, dmx_chop_hit* s_hit, uint32_t cap,
+                                          uint32_t read, int lab, int dist, uint32_t stop) {
+    const uint32_t i = atomicAdd(s_nh, 1u);   // keeps counting past cap: the exact hit count
+    if (i < cap) {
         dmx_chop_hit h;
         h.read = read;
         h.label = (int16_t)lab;
@@ -110,9 +116,10 @@ __device__ __forceinline__ void chop_push(uint32_t* s_nh, dmx_chop_hit* s_hit, u
 }
 
 // One (segment, label) task: D(j) over the owned columns (s0, s0 + kChopSeg] of the read.
+// s_nh / s_hit: the block's hit counter and list (LDS, or global memory in chop_big_kernel).
 __device__ __forceinline__ void chop_scan(const ChopArgs& A, const ChopLabel& L, int lab,
                                           uint32_t read, uint32_t si, uint32_t* s_nh,
-                                          dmx_chop_hit* s_hit) {
+                                          dmx_chop_hit* s_hit, uint32_t cap) {
     const uint32_t n = A.lens[read];
     const uint64_t off = A.offs[read];
     const int m = L.m, k = L.k;
@@ -152,13 +159,13 @@ __device__ __forceinline__ void chop_scan(const ChopArgs& A, const ChopLabel& L,
                     }
                 } else if (run) {
                     run = false;
-                    if (owned) chop_push(s_nh, s_hit, read, lab, best, bstop);
+                    if (owned) chop_push(s_nh, s_hit, cap, read, lab, best, bstop);
                 }
             }
         }
         if (p + 16u >= send && !run) return;
     }
-    if (run && owned) chop_push(s_nh, s_hit, read, lab, best, bstop);
+    if (run && owned) chop_push(s_nh, s_hit, cap, read, lab, best, bstop);
 }
 
 // Start of the shortest optimal alignment ending at `stop`: the reverse-complement label R
@@ -244,12 +251,21 @@ __global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
             if (s_pre[mid] <= sg) lo = mid;
             else hi = mid - 1u;
         }
-        chop_scan(A, s_lab[lab], lab, r0 + lo, sg - s_pre[lo], &s_nh, s_hit);
+        chop_scan(A, s_lab[lab], lab, r0 + lo, sg - s_pre[lo], &s_nh, s_hit, kChopHitCap);
     }
     __syncthreads();
     const uint32_t nh = s_nh;
     if (nh > kChopHitCap) {   // block-uniform: the host re-runs with fewer reads per block
-        if (threadIdx.x == 0) atomicOr(&A.ctr[2], 1ull);
+        if (threadIdx.x == 0) {
+            atomicOr(&A.ctr[2], 1ull);
+            if (A.rpb == 1) {   // a read alone: redone by chop_big_kernel
+                const unsigned long long i = atomicAdd(&A.ctr[3], 1ull);
+                if (i < A.ovf_cap) {
+                    A.ovf[2 * i] = r0;
+                    A.ovf[2 * i + 1] = nh;
+                }
+            }
+        }
         return;
     }
 
@@ -350,6 +366,91 @@ __global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
     }
 }
 
+// One read whose hits overflow the LDS list (rpb == 1 pass): the same scan, with the hit list in
+// global memory (scratch[base .. base + count), count = the exact number the LDS pass counted),
+// a parallel rank sort (keys (start, stop, label) are distinct), one lane pairing.
+__global__ __launch_bounds__(kChopBlock) void chop_big_kernel(ChopArgs A, const uint64_t* base,
+                                                              dmx_chop_hit* scratch,
+                                                              dmx_chop_hit* sorted,
+                                                              uint32_t* counter) {
+    __shared__ ChopLabel s_lab[kChopMaxLabels];
+    __shared__ int8_t s_rule[kChopMaxLabels * kChopMaxLabels];
+    __shared__ int8_t s_rstrand[kChopMaxRules];
+    __shared__ uint32_t s_ns, s_hbase, s_sbase;
+    const ChopPanel* P = A.panel;
+    const int NL = P->n_labels;
+    const bool keep = P->keep != 0;
+    for (int i = threadIdx.x; i < NL * (int)(sizeof(ChopLabel) / 8); i += blockDim.x)
+        reinterpret_cast<uint64_t*>(s_lab)[i] = reinterpret_cast<const uint64_t*>(P->lab)[i];
+    for (int i = threadIdx.x; i < kChopMaxLabels * kChopMaxLabels; i += blockDim.x)
+        s_rule[i] = P->rule[i];
+    if (threadIdx.x < kChopMaxRules) s_rstrand[threadIdx.x] = P->rstrand[threadIdx.x];
+    __syncthreads();
+    const uint32_t read = A.ovf[2 * blockIdx.x];
+    const uint32_t cap = (uint32_t)(base[blockIdx.x + 1] - base[blockIdx.x]);
+    dmx_chop_hit* H = scratch + base[blockIdx.x];
+    dmx_chop_hit* Sh = sorted + base[blockIdx.x];
+    uint32_t* cnt = counter + blockIdx.x;
+    const uint32_t nsegs = (A.lens[read] + kChopSeg - 1u) / kChopSeg;
+    for (uint32_t task = threadIdx.x; task < nsegs * (uint32_t)NL; task += blockDim.x) {
+        const uint32_t sg = task / (uint32_t)NL;
+        const int lab = (int)(task - sg * (uint32_t)NL);
+        chop_scan(A, s_lab[lab], lab, read, sg, cnt, H, cap);
+    }
+    __syncthreads();
+    const uint32_t nh = min(*cnt, cap);
+    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x) {
+        dmx_chop_hit h = H[i];
+        h.start = chop_start(A, s_lab[h.label ^ 1], h.read, h.dist, (uint32_t)h.stop);
+        H[i] = h;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x) {
+        const dmx_chop_hit x = H[i];
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < nh; ++j) rank += hit_less(H[j], x) ? 1u : 0u;
+        Sh[rank] = x;
+    }
+    __syncthreads();
+    dmx_chop_seg* G = reinterpret_cast<dmx_chop_seg*>(H);   // H is free now
+    if (threadIdx.x == 0) {
+        uint32_t ns = 0;
+        for (uint32_t a = 0; a + 1 < nh;) {
+            const dmx_chop_hit h1 = Sh[a], h2 = Sh[a + 1];
+            const int ri = s_rule[h1.label * kChopMaxLabels + h2.label];
+            if (ri >= 0) {
+                dmx_chop_seg sg;
+                sg.read = read;
+                const int32_t x0 = keep ? h1.start : h1.stop;
+                const int32_t x1 = keep ? h2.stop : h2.start;
+                sg.start = x0;
+                sg.stop = max(x0, x1);
+                sg.strand = (int16_t)s_rstrand[ri];
+                sg.rule = (int16_t)ri;
+                G[ns++] = sg;
+                a += 2;
+            } else {
+                ++a;
+            }
+        }
+        s_ns = ns;
+        s_hbase = (uint32_t)atomicAdd(&A.ctr[0], (unsigned long long)nh);
+        s_sbase = (uint32_t)atomicAdd(&A.ctr[1], (unsigned long long)ns);
+        A.blk[4 * read + 0] = s_hbase;   // rpb == 1: block index = read index
+        A.blk[4 * read + 1] = nh;
+        A.blk[4 * read + 2] = s_sbase;
+        A.blk[4 * read + 3] = ns;
+        A.nhit[read] = nh;
+        A.nseg[read] = ns;
+    }
+    __syncthreads();
+    const uint64_t hb = s_hbase, sb = s_sbase;
+    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x)
+        if (hb + i < A.hit_cap) A.hits[hb + i] = Sh[i];
+    for (uint32_t i = threadIdx.x; i < s_ns; i += blockDim.x)
+        if (sb + i < A.seg_cap) A.segs[sb + i] = G[i];
+}
+
 // Exclusive scan of the per-block hit / segment counts (one block; a few 100k entries).
 __global__ __launch_bounds__(1024) void chop_blkscan_kernel(const uint32_t* blk, uint32_t nb,
                                                             uint32_t* off) {
@@ -411,6 +512,13 @@ struct ChopState {
     uint32_t* d_blkoff = nullptr;
     size_t blk_cap = 0;
     unsigned long long* d_ctr = nullptr;
+    uint32_t* d_ovf = nullptr;            // rpb == 1 overflow list (read, count)
+    size_t ovf_cap = 0;
+    uint64_t* d_ovf_base = nullptr;       // chop_big_kernel: hit-list bases, scratch, counters
+    dmx_chop_hit* d_big = nullptr;
+    size_t big_cap = 0;
+    uint32_t* d_big_cnt = nullptr;
+    size_t big_reads_cap = 0;
     uint64_t n_hits = 0, n_segs = 0;
     size_t n_reads = 0;
     bool done = false;
@@ -422,8 +530,9 @@ struct ChopState {
 void chop_release(Ctx* c) {
     ChopState* s = c->chop;
     if (!s) return;
-    void* bufs[] = {s->d_panel, s->d_hstage, s->d_hits, s->d_sstage, s->d_segs,
-                    s->d_nhit,  s->d_nseg,   s->d_blk,  s->d_blkoff, s->d_ctr};
+    void* bufs[] = {s->d_panel, s->d_hstage, s->d_hits,    s->d_sstage, s->d_segs,
+                    s->d_nhit,  s->d_nseg,   s->d_blk,     s->d_blkoff, s->d_ctr,
+                    s->d_ovf,   s->d_ovf_base, s->d_big,   s->d_big_cnt};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (auto& e : s->ev)
@@ -633,6 +742,12 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
         A.nseg = s->d_nseg;
         A.blk = s->d_blk;
         A.ctr = s->d_ctr;
+        if (rpb == 1 && s->ovf_cap < n) {
+            CHOP_CK(dev_realloc(&s->d_ovf, 2 * n));
+            s->ovf_cap = n;
+        }
+        A.ovf = s->d_ovf;
+        A.ovf_cap = rpb == 1 ? s->ovf_cap : 0;
         CHOP_CK(hipEventRecord(s->ev[0], st));
         if (nb) hipLaunchKernelGGL(chop_kernel, dim3(nb), dim3(kChopBlock), 0, st, A);
         CHOP_CK(hipGetLastError());
@@ -640,14 +755,36 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
         CHOP_CK(hipMemcpyAsync(ctr, s->d_ctr, 4 * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost, st));
         CHOP_CK(hipStreamSynchronize(st));
-        if (ctr[2] & 1ull) {
-            if (rpb == 1) {
-                c->err = "dmx_chop_exec: a read has more than " + std::to_string(kChopHitCap) +
-                         " primer hits";
-                return DMX_E_UNSUPPORTED;
-            }
+        if ((ctr[2] & 1ull) && rpb > 1) {
             rpb = rpb > 8 ? 8u : 1u;
             continue;
+        }
+        if (ctr[2] & 1ull) {   // rpb == 1: redo each overflowing read with a global hit list
+            const size_t no = (size_t)ctr[3];
+            std::vector<uint32_t> ovf(2 * no);
+            CHOP_CK(hipMemcpy(ovf.data(), s->d_ovf, ovf.size() * 4, hipMemcpyDeviceToHost));
+            std::vector<uint64_t> base(no + 1, 0);
+            for (size_t i = 0; i < no; ++i) base[i + 1] = base[i] + ovf[2 * i + 1];
+            if (s->big_cap < base[no] || !s->d_big) {
+                CHOP_CK(dev_realloc(&s->d_big, 2 * base[no]));
+                s->big_cap = base[no];
+            }
+            if (s->big_reads_cap < no + 1 || !s->d_ovf_base) {
+                CHOP_CK(dev_realloc(&s->d_ovf_base, no + 1));
+                CHOP_CK(dev_realloc(&s->d_big_cnt, no + 1));
+                s->big_reads_cap = no + 1;
+            }
+            CHOP_CK(hipMemcpyAsync(s->d_ovf_base, base.data(), (no + 1) * 8,
+                                   hipMemcpyHostToDevice, st));
+            CHOP_CK(hipMemsetAsync(s->d_big_cnt, 0, (no + 1) * 4, st));
+            hipLaunchKernelGGL(chop_big_kernel, dim3((uint32_t)no), dim3(kChopBlock), 0, st, A,
+                               (const uint64_t*)s->d_ovf_base, s->d_big, s->d_big + s->big_cap,
+                               s->d_big_cnt);
+            CHOP_CK(hipGetLastError());
+            CHOP_CK(hipEventRecord(s->ev[1], st));
+            CHOP_CK(hipMemcpyAsync(ctr, s->d_ctr, 4 * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, st));
+            CHOP_CK(hipStreamSynchronize(st));
         }
         if (ctr[0] >= (1ull << 32) || ctr[1] >= (1ull << 32)) {
             c->err = "dmx_chop_exec: more than 2^32 hits in one batch";

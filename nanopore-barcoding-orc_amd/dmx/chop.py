@@ -17,7 +17,8 @@ given).  QC: a FASTQ read whose mean quality (-10 log10 of the mean error probab
 is below -Q goes to -K if given, else is dropped.  Cutoff -q: maximum edit distance as a
 fraction of the primer length (k = int(q * m)); without -q it is tuned on the first -Y
 QC-passing reads of the first batch over 0.05, 0.10, ..., 0.40 (the value giving the most reads
-with a segment; ties -> the smaller).  -k is accepted and unused (-b and -c define primers and
+with exactly one segment — spurious hits at loose cutoffs split reads into fused "rescues";
+ties -> the smaller).  -k is accepted and unused (-b and -c define primers and
 layout); only -m edlib is implemented.
 """
 from __future__ import annotations
@@ -156,13 +157,14 @@ class Chopper:
         return nseg, segs
 
     def autotune(self, sample_idx) -> float:
-        """The cutoff of AUTOTUNE_CUTOFFS with the most sampled reads having a segment."""
+        """The cutoff of AUTOTUNE_CUTOFFS with the most sampled reads having exactly one
+        segment (ties -> the smaller)."""
         best, best_n = AUTOTUNE_CUTOFFS[0], -1
         for q in AUTOTUNE_CUTOFFS:
             self.set_cutoff(q)
             self.ctx.chop_exec()
             nseg = self.ctx.chop_fetch(segs=False)[0]
-            c = int((nseg[sample_idx] > 0).sum())
+            c = int((nseg[sample_idx] == 1).sum())
             if c > best_n:
                 best, best_n = q, c
         return best

@@ -24,8 +24,8 @@ options:
             0 segments -> unclassified (record unchanged); 1 -> pass (short if < -z);
             >= 2 -> every segment rescued (short if < -z); '-' segments reverse-complemented;
             segment records named "{start}:{stop}|{id} strand=+|-" + the original comment
-  autotune  without -q: the cutoff of 0.05, 0.10, ..., 0.40 giving the most reads with a
-            segment among the first -Y QC-passing reads (ties -> the smaller)
+  autotune  without -q: the cutoff of 0.05, 0.10, ..., 0.40 giving the most reads with
+            exactly one segment among the first -Y QC-passing reads (ties -> the smaller)
 
 Only tests/ (and bench.py's cpu_baseline leg, through `batch_hit_counts`) use this module, as
 the checker of libdmx's `dmx_chop_*` (HIP) path and of the `bin/pychopper` drop-in.
@@ -231,7 +231,7 @@ def autotune(records, primers, config: str, keep: bool = True, min_qual: float =
     pool = [s for _, s, q in records if fasta or mean_qual(q) >= min_qual][:sample]
     best, best_n = None, -1
     for q in AUTOTUNE_CUTOFFS:
-        c = sum(1 for s in pool if segments(read_hits(labs, s, q), rules, keep))
+        c = sum(1 for s in pool if len(segments(read_hits(labs, s, q), rules, keep)) == 1)
         if c > best_n:
             best, best_n = q, c
     return best

@@ -172,7 +172,8 @@ def test_chop_hits_and_segments_match_oracle(ctx, cutoff, keep):
     assert S == eS
     assert np.bincount([h[0] for h in eH], minlength=len(seqs)).tolist() == nhit.tolist()
     assert np.bincount([s[0] for s in eS], minlength=len(seqs)).tolist() == nseg.tolist()
-    assert sum(1 for x in nseg if x == 1) > 0.5 * len(seqs)
+    if cutoff <= 0.2:   # at 0.3 (k = 17 of 58) spurious hits break most reads' pairing
+        assert sum(1 for x in nseg if x == 1) > 0.5 * len(seqs)
 
 
 @pytest.mark.gpu
@@ -209,6 +210,26 @@ def test_chop_random_primer_panels(ctx):
         assert S == eS, (trial, rules)
     st = ctx.chop_stats()
     assert st["chop"] >= 0.0
+
+
+@pytest.mark.gpu
+def test_chop_reads_beyond_the_lds_hit_list(ctx):
+    """Long reads with thousands of hits (6-nt primers, one error allowed): the 1-read re-run
+    still overflows the 512-entry LDS list, so chop_big_kernel redoes those reads with a hit list
+    in global memory; reads around them take the normal path."""
+    rng = np.random.default_rng(41)
+    primers = [(f"P{i}", "".join(rng.choice(list("ACGT"), size=6))) for i in range(8)]
+    rules = [(0, 3, 0), (2, 1, 1), (4, 5, 0), (7, 6, 1)]
+    seqs = ["".join(rng.choice(list("ACGT"), size=int(rng.integers(4000, 9000))))
+            if i % 3 == 0 else "".join(rng.choice(list("ACGT"), size=int(rng.integers(0, 300))))
+            for i in range(40)]
+    for keep in (True, False):
+        nseg, nhit, H, S = _gpu(ctx, seqs, primers, rules, 0.2, keep)
+        eH, eS = _oracle(seqs, primers, rules, 0.2, keep)
+        assert H == eH
+        assert S == eS
+        assert int(nhit.max()) > 512
+        assert ctx.chop_stats()["reads_per_block"] == 1
 
 
 def _records(rng, n):
