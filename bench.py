@@ -108,14 +108,17 @@ def chop_cpu_baseline(threads: int, cutoff: float, target_s: float = 12.0):
                       "installed)"}
 
 
-def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutoff, gen_s):
+def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutoff, gen_s,
+              label_lens):
     """pychopper-style reorientation (01_pychopper.sh).  Dominant kernel: dmx::chop_kernel."""
     L = lengths.astype(np.float64)
     alg_bytes = (float(np.sum(np.ceil(L / 4) + np.ceil(L / 8) + 12.0)) + 8.0 * len(L)
                  + 16.0 * (n_hits + n_segs))
     kern_ms = ms["chop"] / K
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-    cols = float(np.sum(L + np.maximum(np.ceil(L / 512) - 1, 0) * 116)) * 4   # + warm-up, 4 labels
+    # Myers columns: every label over the read, plus m + k warm-up columns per later segment
+    extra = np.maximum(np.ceil(L / 512) - 1, 0)
+    cols = sum(float(np.sum(L + extra * (m + int(cutoff * m)))) for m in label_lens)
     return {
         "metric": "Mreads/s pychopper-style reorientation (01_pychopper.sh: -m edlib -p, "
                   "M13 SP5/SP27 primers)",
@@ -403,7 +406,8 @@ def chop_main(args, ctx, packed, tune, lengths, gen_s, world, rank, dist, on_gpu
         elapsed = float(tt.item())
     K = args.steps
     value = args.reads * world * K / elapsed / 1e6
-    out = chop_line(args, world, K, value, elapsed, ms, lengths, tot[0], tot[1], cutoff, gen_s)
+    out = chop_line(args, world, K, value, elapsed, ms, lengths, tot[0], tot[1], cutoff, gen_s,
+                    [len(p[1]) for p in primers for _ in (0, 1)])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = chop_cpu_baseline(args.cpu_threads, cutoff)
     if rank == 0:

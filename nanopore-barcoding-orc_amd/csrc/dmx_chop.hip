@@ -24,8 +24,9 @@
 //   chop_kernel   a block owns up to 64 consecutive reads.  Its lanes take (512-column segment,
 //                 label) tasks, labels fastest, so the lanes of one segment load the same packed
 //                 words.  A lane runs the 64-bit Myers/Hyyro step of the demux scans (labels
-//                 <= 64 nt) from 2m columns before its segment — exact from the segment's first
-//                 column on, because an alignment of cost <= m spans <= 2m columns — follows
+//                 <= 64 nt) from m + k columns before its segment — exact for every D <= k from
+//                 the segment's first column on, as an alignment of cost <= k spans <= m + k
+//                 columns — follows
 //                 runs of D <= k (a run crossing the segment end is followed to its end) and
 //                 appends the runs that start inside its segment to an LDS hit list (one LDS
 //                 atomic each).  After a barrier one lane per hit finds its start (an anchored
@@ -117,6 +118,9 @@ __device__ __forceinline__ void chop_push(uint32_t* s_nh, dmx_chop_hit* s_hit, u
 
 // One (segment, label) task: D(j) over the owned columns (s0, s0 + kChopSeg] of the read.
 // s_nh / s_hit: the block's hit counter and list (LDS, or global memory in chop_big_kernel).
+// HB: the last row's bit is in the low (0) or high (1) 32-bit half for every label, or -1
+// (mixed: selected per step).
+template <int HB>
 __device__ __forceinline__ void chop_scan(const ChopArgs& A, const ChopLabel& L, int lab,
                                           uint32_t read, uint32_t si, uint32_t* s_nh,
                                           dmx_chop_hit* s_hit, uint32_t cap) {
@@ -126,9 +130,13 @@ __device__ __forceinline__ void chop_scan(const ChopArgs& A, const ChopLabel& L,
     const uint32_t hbit = (uint32_t)(m - 1);
     const uint32_t s0 = si * kChopSeg, s1 = s0 + kChopSeg;
     const uint32_t send = min(n, s1);
-    // warm-up: columns >= ws + 2m carry exact values (D(i, j) <= i, so an optimal alignment of
-    // rows 1..i spans at most i + D <= 2i columns); column s0 decides run ownership exactly
-    const uint32_t ws = s0 > (uint32_t)(2 * m) ? s0 - (uint32_t)(2 * m) : 0u;
+    // warm-up: starting at ws, the scan's D(m, j) is the true value whenever an optimal
+    // alignment starts at or after ws, and never below it.  An alignment of cost c <= k spans
+    // at most m + c columns, so from column ws + m + k on every D <= k is exact and every
+    // D > k stays > k: run membership and run minima are exact from column s0 on, which
+    // decides run ownership.
+    const uint32_t wu = (uint32_t)(m + k);
+    const uint32_t ws = s0 > wu ? s0 - wu : 0u;
     uint64_t pv = ~0ull, mv = 0ull;
     int d = m;
     bool run = false, owned = false;
@@ -145,7 +153,7 @@ __device__ __forceinline__ void chop_scan(const ChopArgs& A, const ChopLabel& L,
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             if ((uint32_t)q < cnt) {
-                myers_step<-1>(eqv[q], pv, mv, d, hbit);
+                myers_step<HB>(eqv[q], pv, mv, d, hbit);
                 const uint32_t j = p + (uint32_t)q + 1u;
                 if (d <= k) {
                     if (!run) {
@@ -207,6 +215,7 @@ __device__ __forceinline__ bool hit_less(const dmx_chop_hit& a, const dmx_chop_h
     return a.label < b.label;
 }
 
+template <int HB>
 __global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
     __shared__ ChopLabel s_lab[kChopMaxLabels];
     __shared__ int8_t s_rule[kChopMaxLabels * kChopMaxLabels];
@@ -251,7 +260,7 @@ __global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
             if (s_pre[mid] <= sg) lo = mid;
             else hi = mid - 1u;
         }
-        chop_scan(A, s_lab[lab], lab, r0 + lo, sg - s_pre[lo], &s_nh, s_hit, kChopHitCap);
+        chop_scan<HB>(A, s_lab[lab], lab, r0 + lo, sg - s_pre[lo], &s_nh, s_hit, kChopHitCap);
     }
     __syncthreads();
     const uint32_t nh = s_nh;
@@ -395,7 +404,7 @@ __global__ __launch_bounds__(kChopBlock) void chop_big_kernel(ChopArgs A, const 
     for (uint32_t task = threadIdx.x; task < nsegs * (uint32_t)NL; task += blockDim.x) {
         const uint32_t sg = task / (uint32_t)NL;
         const int lab = (int)(task - sg * (uint32_t)NL);
-        chop_scan(A, s_lab[lab], lab, read, sg, cnt, H, cap);
+        chop_scan<-1>(A, s_lab[lab], lab, read, sg, cnt, H, cap);
     }
     __syncthreads();
     const uint32_t nh = min(*cnt, cap);
@@ -525,6 +534,7 @@ struct ChopState {
     hipEvent_t ev[4] = {};
     float ms[2] = {0.f, 0.f};
     uint32_t rpb = kChopReads;
+    int hb = -1;   // chop_kernel variant: last-row bit in the high (1) / low (0) half, or mixed
 };
 
 void chop_release(Ctx* c) {
@@ -676,6 +686,12 @@ extern "C" int dmx_chop_set(dmx_ctx* c, const char* const* primers, const int* p
     if (!s->d_panel) CHOP_CK(hipMalloc((void**)&s->d_panel, sizeof(ChopPanel)));
     CHOP_CK(hipMemcpyAsync(s->d_panel, &P, sizeof(ChopPanel), hipMemcpyHostToDevice, c->stream));
     CHOP_CK(hipStreamSynchronize(c->stream));
+    bool hi = true, lo = true;
+    for (int l = 0; l < P.n_labels; ++l) {
+        hi = hi && P.lab[l].m > 32;
+        lo = lo && P.lab[l].m <= 32;
+    }
+    s->hb = hi ? 1 : (lo ? 0 : -1);
     s->host = P;
     s->set = true;
     s->done = false;
@@ -749,7 +765,11 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
         A.ovf = s->d_ovf;
         A.ovf_cap = rpb == 1 ? s->ovf_cap : 0;
         CHOP_CK(hipEventRecord(s->ev[0], st));
-        if (nb) hipLaunchKernelGGL(chop_kernel, dim3(nb), dim3(kChopBlock), 0, st, A);
+        if (nb) {
+            if (s->hb == 1) hipLaunchKernelGGL(chop_kernel<1>, dim3(nb), dim3(kChopBlock), 0, st, A);
+            else if (s->hb == 0) hipLaunchKernelGGL(chop_kernel<0>, dim3(nb), dim3(kChopBlock), 0, st, A);
+            else hipLaunchKernelGGL(chop_kernel<-1>, dim3(nb), dim3(kChopBlock), 0, st, A);
+        }
         CHOP_CK(hipGetLastError());
         CHOP_CK(hipEventRecord(s->ev[1], st));
         CHOP_CK(hipMemcpyAsync(ctr, s->d_ctr, 4 * sizeof(unsigned long long),
