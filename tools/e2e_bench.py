@@ -8,8 +8,10 @@ FASTQ.gz (level 1, parallel members, via libdmx_io), then times
           on plain FASTQ (01_pychopper.sh:57 writes *_pass.fastq uncompressed), on our
           multi-member .gz (parallel inflate) and on a single-member .gz (sequential inflate)
   calls : the 13 bin/cutadapt calls of 02_cutadapt_loop.sh:64-103 (per-call drop-in)
+  pychopper (--pychopper): bin/pychopper with 01_pychopper.sh:45-57's flags on the .gz input
 and prints one JSON line with reads/s for each.  Usage:
   python tools/e2e_bench.py --reads 1000000 [--workload c2] [--threads 16] [--skip-calls]
+                            [--skip-fused] [--pychopper]
 """
 from __future__ import annotations
 
@@ -29,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "nanopore-barcoding-orc_amd")
 sys.path.insert(0, PKG)
 
-from dmx import nio, panel, synth  # noqa: E402
+from dmx import chop, nio, panel, synth  # noqa: E402
 
 
 def write_fastq(path_plain: str, d: dict, seed: int, chunk: int = 100_000) -> int:
@@ -83,6 +85,8 @@ def main():
     ap.add_argument("--workload", default="c2")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--skip-calls", action="store_true")
+    ap.add_argument("--skip-fused", action="store_true")
+    ap.add_argument("--pychopper", action="store_true")
     ap.add_argument("--workdir", default=None)
     a = ap.parse_args()
     wd = a.workdir or tempfile.mkdtemp(prefix="dmx_e2e_")
@@ -111,8 +115,23 @@ def main():
     res = {"workload": a.workload, "reads": a.reads, "threads": a.threads,
            "input_fastq_bytes": raw_bytes, "input_gz_bytes": gz_bytes, "gen_s": round(gen_s, 1)}
 
-    for tag, path in (("fused_plain", plain), ("fused_gz_members", gz),
-                      ("fused_gz_single", gz1)):
+    if a.pychopper:   # 01_pychopper.sh:45-57, PASS to a file as the script's redirect does
+        po = os.path.join(wd, "pychopper_out")
+        os.makedirs(po, exist_ok=True)
+        cmd = [os.path.join(PKG, "bin", "pychopper"), "-b", chop.PRIMERS_FASTA,
+               "-c", chop.CONFIG_FILE, "-k", "LSK114", "-Q", "10", "-w", f"{po}/rescued.fastq",
+               "-u", f"{po}/unclass.fastq", "-l", f"{po}/short.fastq", "-S", f"{po}/stats.out",
+               "-p", "-t", str(a.threads), "-m", "edlib", gz]
+        t = time.perf_counter()
+        with open(f"{po}/pass.fastq", "wb") as fh:
+            p = subprocess.run(cmd, check=True, stdout=fh, stderr=subprocess.PIPE, text=True)
+        ps = time.perf_counter() - t
+        res["pychopper_gz_s"] = round(ps, 3)
+        res["pychopper_gz_reads_per_s"] = round(a.reads / ps, 1)
+        res["pychopper_report"] = p.stderr.strip().splitlines()[-1] if p.stderr.strip() else ""
+    for tag, path in ((() if a.skip_fused else (("fused_plain", plain),
+                                                  ("fused_gz_members", gz),
+                                                  ("fused_gz_single", gz1)))):
         t = time.perf_counter()
         p = subprocess.run([os.path.join(PKG, "bin", "dmx-demux-loop"), path, "-j",
                             str(a.threads), "--outdir", os.path.join(wd, tag)], check=True,
