@@ -200,8 +200,9 @@ int dmx_chop_exec(dmx_ctx* ctx, uint64_t* n_hits, uint64_t* n_segs);
  * segments left to right, hits by (start, stop, label)). */
 int dmx_chop_fetch(dmx_ctx* ctx, uint32_t* n_seg, uint32_t* n_hit, dmx_chop_seg* segs,
                    size_t seg_cap, dmx_chop_hit* hits, size_t hit_cap);
-/* Device time (ms) of the last dmx_chop_exec: [0] chop_kernel (its final launch), [1] the
- * read-order compaction.  Returns the reads per block the final launch used. */
+/* Device time (ms) of the last dmx_chop_exec: [0] chop_kernel (and chop_big_kernel when blocks
+ * overflowed), [1] the read-order compaction.  Returns the number of 64-read blocks redone with
+ * global hit lists (more primer hits than the 512-entry LDS list holds). */
 int dmx_chop_stats(dmx_ctx* ctx, float* ms, int n_ms);
 
 #ifdef __cplusplus

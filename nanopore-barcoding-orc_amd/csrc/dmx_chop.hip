@@ -37,10 +37,10 @@
 //   chop_blkscan_kernel, chop_order_kernel
 //                 move every block's ranges into read order (block order = read order), so the
 //                 host receives read-ordered hits and segments without a sort.
-// A block whose hits overflow its LDS list (reads with hundreds of primer hits) is re-run with
-// fewer reads per block (64 -> 8 -> 1); a single read that still overflows is redone by
-// chop_big_kernel (one block per such read, hit list in global memory sized by the exact count
-// the LDS pass measured, parallel rank sort); a staging overflow re-runs with larger buffers.
+// A block whose hits overflow its LDS list (reads with hundreds of primer hits) is redone alone
+// by chop_big_kernel: hit lists in global memory sized by the exact count the LDS pass measured,
+// counting scatter by read, parallel rank sort per read; a staging overflow re-runs with larger
+// buffers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -78,7 +78,7 @@ struct ChopArgs {
     const uint32_t* nmask;
     const uint64_t* offs;
     const uint32_t* lens;
-    uint32_t n_reads, rpb;
+    uint32_t n_reads;
     const ChopPanel* panel;
     dmx_chop_hit* hits;        // staging: block ranges in reservation order
     dmx_chop_seg* segs;
@@ -87,8 +87,8 @@ struct ChopArgs {
     uint32_t* nseg;
     uint32_t* blk;             // per block: hit base, hits, segment base, segments
     unsigned long long* ctr;   // [0] hits, [1] segments, [2] flags (bit 0: LDS list overflow),
-                               // [3] reads overflowing alone (rpb == 1)
-    uint32_t* ovf;             // rpb == 1: (read, exact hit count) of each overflowing read
+                               // [3] blocks overflowing their LDS hit list
+    uint32_t* ovf;             // (block, exact hit count) of each such block
     uint64_t ovf_cap;
 };
 
@@ -215,30 +215,23 @@ __device__ __forceinline__ bool hit_less(const dmx_chop_hit& a, const dmx_chop_h
     return a.label < b.label;
 }
 
-template <int HB>
-__global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
-    __shared__ ChopLabel s_lab[kChopMaxLabels];
-    __shared__ int8_t s_rule[kChopMaxLabels * kChopMaxLabels];
-    __shared__ int8_t s_rstrand[kChopMaxRules];
-    __shared__ uint32_t s_pre[kChopReads + 1], s_off[kChopReads + 1], s_soff[kChopReads + 1];
-    __shared__ uint32_t s_cnt[kChopReads], s_sc[kChopReads];
-    __shared__ dmx_chop_hit s_hit[kChopHitCap];
-    __shared__ dmx_chop_hit s_srt[kChopHitCap];
-    __shared__ uint32_t s_nh, s_hbase, s_sbase;
-    const ChopPanel* P = A.panel;
-    const int NL = P->n_labels;
-    const bool keep = P->keep != 0;
-    for (int i = threadIdx.x; i < NL * (int)(sizeof(ChopLabel) / 8); i += blockDim.x)
+__device__ __forceinline__ void chop_load_panel(const ChopPanel* P, ChopLabel* s_lab,
+                                                int8_t* s_rule, int8_t* s_rstrand) {
+    for (int i = threadIdx.x; i < P->n_labels * (int)(sizeof(ChopLabel) / 8); i += blockDim.x)
         reinterpret_cast<uint64_t*>(s_lab)[i] = reinterpret_cast<const uint64_t*>(P->lab)[i];
     for (int i = threadIdx.x; i < kChopMaxLabels * kChopMaxLabels; i += blockDim.x)
         s_rule[i] = P->rule[i];
     if (threadIdx.x < kChopMaxRules) s_rstrand[threadIdx.x] = P->rstrand[threadIdx.x];
-    const uint32_t r0 = blockIdx.x * A.rpb;
-    const uint32_t nr = min(A.rpb, A.n_reads - r0);
-    if (threadIdx.x < nr) s_cnt[threadIdx.x] = (A.lens[r0 + threadIdx.x] + kChopSeg - 1u) / kChopSeg;
+}
+
+// s_pre[t] = first (segment) task of read r0 + t, s_pre[nr] = the block's segments; s_cnt is
+// left zeroed.  Every thread must call it.
+__device__ __forceinline__ void chop_segment_prefix(const ChopArgs& A, uint32_t r0, uint32_t nr,
+                                                    uint32_t* s_cnt, uint32_t* s_pre) {
+    if (threadIdx.x < nr)
+        s_cnt[threadIdx.x] = (A.lens[r0 + threadIdx.x] + kChopSeg - 1u) / kChopSeg;
     __syncthreads();
     if (threadIdx.x == 0) {
-        s_nh = 0u;
         uint32_t acc = 0;
         for (uint32_t t = 0; t < nr; ++t) {
             s_pre[t] = acc;
@@ -248,31 +241,116 @@ __global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
         s_pre[nr] = acc;
     }
     __syncthreads();
+}
+
+// Last t in [0, nr) with pre[t] <= x.
+__device__ __forceinline__ uint32_t chop_last_le(const uint32_t* pre, uint32_t nr, uint32_t x) {
+    uint32_t lo = 0, hi = nr - 1u;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1u) >> 1;
+        if (pre[mid] <= x) lo = mid;
+        else hi = mid - 1u;
+    }
+    return lo;
+}
+
+// Once every read's hits are sorted in srt[s_off[t] .. s_off[t + 1]): one lane per read pairs
+// them greedily into seg[s_off[t] ...] (seg must not alias srt), the block reserves its output
+// ranges (one atomic per list) and writes them.  srt / seg: LDS (chop_kernel) or global scratch
+// (chop_big_kernel).  Every thread must call it.
+__device__ void chop_pair_write(const ChopArgs& A, uint32_t b, uint32_t r0, uint32_t nr,
+                                uint32_t nh, bool keep, const int8_t* s_rule,
+                                const int8_t* s_rstrand, const dmx_chop_hit* srt,
+                                dmx_chop_seg* seg, const uint32_t* s_off, uint32_t* s_sc,
+                                uint32_t* s_soff, uint32_t* s_base) {
+    if (threadIdx.x < nr) {
+        const uint32_t t = threadIdx.x;
+        const uint32_t o = s_off[t], c = s_off[t + 1] - o;
+        uint32_t ns = 0;
+        for (uint32_t a = 0; a + 1 < c;) {
+            const dmx_chop_hit h1 = srt[o + a], h2 = srt[o + a + 1];
+            const int ri = s_rule[h1.label * kChopMaxLabels + h2.label];
+            if (ri >= 0) {
+                dmx_chop_seg sg;
+                sg.read = h1.read;
+                const int32_t x0 = keep ? h1.start : h1.stop;
+                const int32_t x1 = keep ? h2.stop : h2.start;
+                sg.start = x0;
+                sg.stop = max(x0, x1);
+                sg.strand = (int16_t)s_rstrand[ri];
+                sg.rule = (int16_t)ri;
+                seg[o + ns] = sg;
+                ++ns;
+                a += 2;
+            } else {
+                ++a;
+            }
+        }
+        s_sc[t] = ns;
+        A.nhit[r0 + t] = c;
+        A.nseg[r0 + t] = ns;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t t = 0; t < nr; ++t) {
+            s_soff[t] = acc;
+            acc += s_sc[t];
+        }
+        s_soff[nr] = acc;
+        s_base[0] = (uint32_t)atomicAdd(&A.ctr[0], (unsigned long long)nh);
+        s_base[1] = (uint32_t)atomicAdd(&A.ctr[1], (unsigned long long)acc);
+        A.blk[4 * b + 0] = s_base[0];
+        A.blk[4 * b + 1] = nh;
+        A.blk[4 * b + 2] = s_base[1];
+        A.blk[4 * b + 3] = acc;
+    }
+    __syncthreads();
+    const uint64_t hb = s_base[0], sb = s_base[1];
+    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x)
+        if (hb + i < A.hit_cap) A.hits[hb + i] = srt[i];
+    const uint32_t nsg = s_soff[nr];
+    for (uint32_t i = threadIdx.x; i < nsg; i += blockDim.x) {
+        const uint32_t t = chop_last_le(s_soff, nr, i);
+        if (sb + i < A.seg_cap) A.segs[sb + i] = seg[s_off[t] + (i - s_soff[t])];
+    }
+}
+
+template <int HB>
+__global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
+    __shared__ ChopLabel s_lab[kChopMaxLabels];
+    __shared__ int8_t s_rule[kChopMaxLabels * kChopMaxLabels];
+    __shared__ int8_t s_rstrand[kChopMaxRules];
+    __shared__ uint32_t s_pre[kChopReads + 1], s_off[kChopReads + 1], s_soff[kChopReads + 1];
+    __shared__ uint32_t s_cnt[kChopReads], s_sc[kChopReads];
+    __shared__ dmx_chop_hit s_hit[kChopHitCap];
+    __shared__ dmx_chop_hit s_srt[kChopHitCap];
+    __shared__ uint32_t s_nh, s_base[2];
+    chop_load_panel(A.panel, s_lab, s_rule, s_rstrand);
+    const int NL = A.panel->n_labels;
+    const bool keep = A.panel->keep != 0;
+    const uint32_t r0 = blockIdx.x * kChopReads;
+    const uint32_t nr = min(kChopReads, A.n_reads - r0);
+    if (threadIdx.x == 0) s_nh = 0u;
+    chop_segment_prefix(A, r0, nr, s_cnt, s_pre);
 
     // 1. scans: (segment, label) tasks, labels fastest
     const uint32_t total = s_pre[nr] * (uint32_t)NL;
     for (uint32_t task = threadIdx.x; task < total; task += blockDim.x) {
         const uint32_t sg = task / (uint32_t)NL;
         const int lab = (int)(task - sg * (uint32_t)NL);
-        uint32_t lo = 0, hi = nr - 1u;   // last read whose first segment is <= sg
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1u) >> 1;
-            if (s_pre[mid] <= sg) lo = mid;
-            else hi = mid - 1u;
-        }
-        chop_scan<HB>(A, s_lab[lab], lab, r0 + lo, sg - s_pre[lo], &s_nh, s_hit, kChopHitCap);
+        const uint32_t t = chop_last_le(s_pre, nr, sg);
+        chop_scan<HB>(A, s_lab[lab], lab, r0 + t, sg - s_pre[t], &s_nh, s_hit, kChopHitCap);
     }
     __syncthreads();
     const uint32_t nh = s_nh;
-    if (nh > kChopHitCap) {   // block-uniform: the host re-runs with fewer reads per block
+    if (nh > kChopHitCap) {   // block-uniform: redone by chop_big_kernel with the exact count
         if (threadIdx.x == 0) {
             atomicOr(&A.ctr[2], 1ull);
-            if (A.rpb == 1) {   // a read alone: redone by chop_big_kernel
-                const unsigned long long i = atomicAdd(&A.ctr[3], 1ull);
-                if (i < A.ovf_cap) {
-                    A.ovf[2 * i] = r0;
-                    A.ovf[2 * i + 1] = nh;
-                }
+            const unsigned long long i = atomicAdd(&A.ctr[3], 1ull);
+            if (i < A.ovf_cap) {
+                A.ovf[2 * i] = blockIdx.x;
+                A.ovf[2 * i + 1] = nh;
             }
         }
         return;
@@ -303,12 +381,9 @@ __global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
     }
     __syncthreads();
 
-    // 3. one lane per read: sort its hits by (start, stop, label), pair them greedily.  The
-    // segments of read t land in s_hit[s_off[t] ...] (free now; a read has <= hits/2 segments).
-    dmx_chop_seg* s_seg = reinterpret_cast<dmx_chop_seg*>(s_hit);
+    // 3. one lane per read: insertion-sort its few hits by (start, stop, label)
     if (threadIdx.x < nr) {
-        const uint32_t t = threadIdx.x;
-        const uint32_t o = s_off[t], c = s_off[t + 1] - o;
+        const uint32_t o = s_off[threadIdx.x], c = s_off[threadIdx.x + 1] - o;
         for (uint32_t a = 1; a < c; ++a) {
             const dmx_chop_hit x = s_srt[o + a];
             uint32_t b = a;
@@ -318,146 +393,84 @@ __global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
             }
             s_srt[o + b] = x;
         }
-        uint32_t ns = 0;
-        for (uint32_t a = 0; a + 1 < c;) {
-            const dmx_chop_hit h1 = s_srt[o + a], h2 = s_srt[o + a + 1];
-            const int ri = s_rule[h1.label * kChopMaxLabels + h2.label];
-            if (ri >= 0) {
-                dmx_chop_seg sg;
-                sg.read = h1.read;
-                const int32_t x0 = keep ? h1.start : h1.stop;
-                const int32_t x1 = keep ? h2.stop : h2.start;
-                sg.start = x0;
-                sg.stop = max(x0, x1);
-                sg.strand = (int16_t)s_rstrand[ri];
-                sg.rule = (int16_t)ri;
-                s_seg[o + ns] = sg;
-                ++ns;
-                a += 2;
-            } else {
-                ++a;
-            }
-        }
-        s_sc[t] = ns;
-        A.nhit[r0 + t] = c;
-        A.nseg[r0 + t] = ns;
     }
     __syncthreads();
-
-    // 4. reserve the block's ranges (one atomic per list), write
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (uint32_t t = 0; t < nr; ++t) {
-            s_soff[t] = acc;
-            acc += s_sc[t];
-        }
-        s_soff[nr] = acc;
-        s_hbase = (uint32_t)atomicAdd(&A.ctr[0], (unsigned long long)nh);
-        s_sbase = (uint32_t)atomicAdd(&A.ctr[1], (unsigned long long)acc);
-        A.blk[4 * blockIdx.x + 0] = s_hbase;
-        A.blk[4 * blockIdx.x + 1] = nh;
-        A.blk[4 * blockIdx.x + 2] = s_sbase;
-        A.blk[4 * blockIdx.x + 3] = acc;
-    }
-    __syncthreads();
-    const uint64_t hb = s_hbase, sb = s_sbase;
-    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x)
-        if (hb + i < A.hit_cap) A.hits[hb + i] = s_srt[i];
-    const uint32_t nsg = s_soff[nr];
-    for (uint32_t i = threadIdx.x; i < nsg; i += blockDim.x) {
-        uint32_t lo = 0, hi = nr - 1u;   // last read whose first segment is <= i
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1u) >> 1;
-            if (s_soff[mid] <= i) lo = mid;
-            else hi = mid - 1u;
-        }
-        if (sb + i < A.seg_cap) A.segs[sb + i] = s_seg[s_off[lo] + (i - s_soff[lo])];
-    }
+    // 4. pair and write; the segments of read t land in s_hit[s_off[t] ...] (free now)
+    chop_pair_write(A, blockIdx.x, r0, nr, nh, keep, s_rule, s_rstrand, s_srt,
+                    reinterpret_cast<dmx_chop_seg*>(s_hit), s_off, s_sc, s_soff, s_base);
 }
 
-// One read whose hits overflow the LDS list (rpb == 1 pass): the same scan, with the hit list in
-// global memory (scratch[base .. base + count), count = the exact number the LDS pass counted),
-// a parallel rank sort (keys (start, stop, label) are distinct), one lane pairing.
+// A block of chop_kernel whose hits overflowed its LDS list (reads with hundreds of primer
+// hits), redone with the hit lists in global memory: H = scratch[base .. base + count) and
+// T = temp[...] of the same size, count = the exact number the LDS pass counted.  Counting
+// scatter by read into T, a parallel rank sort of every read's range back into H (the keys
+// (start, stop, label) of one read are distinct), then the same pairing and output as
+// chop_kernel (one range per 64-read block, so the read-order compaction is unchanged).
 __global__ __launch_bounds__(kChopBlock) void chop_big_kernel(ChopArgs A, const uint64_t* base,
                                                               dmx_chop_hit* scratch,
-                                                              dmx_chop_hit* sorted,
+                                                              dmx_chop_hit* temp,
                                                               uint32_t* counter) {
     __shared__ ChopLabel s_lab[kChopMaxLabels];
     __shared__ int8_t s_rule[kChopMaxLabels * kChopMaxLabels];
     __shared__ int8_t s_rstrand[kChopMaxRules];
-    __shared__ uint32_t s_ns, s_hbase, s_sbase;
-    const ChopPanel* P = A.panel;
-    const int NL = P->n_labels;
-    const bool keep = P->keep != 0;
-    for (int i = threadIdx.x; i < NL * (int)(sizeof(ChopLabel) / 8); i += blockDim.x)
-        reinterpret_cast<uint64_t*>(s_lab)[i] = reinterpret_cast<const uint64_t*>(P->lab)[i];
-    for (int i = threadIdx.x; i < kChopMaxLabels * kChopMaxLabels; i += blockDim.x)
-        s_rule[i] = P->rule[i];
-    if (threadIdx.x < kChopMaxRules) s_rstrand[threadIdx.x] = P->rstrand[threadIdx.x];
-    __syncthreads();
-    const uint32_t read = A.ovf[2 * blockIdx.x];
+    __shared__ uint32_t s_pre[kChopReads + 1], s_off[kChopReads + 1], s_soff[kChopReads + 1];
+    __shared__ uint32_t s_cnt[kChopReads], s_sc[kChopReads];
+    __shared__ uint32_t s_base[2];
+    chop_load_panel(A.panel, s_lab, s_rule, s_rstrand);
+    const int NL = A.panel->n_labels;
+    const bool keep = A.panel->keep != 0;
+    const uint32_t b = A.ovf[2 * blockIdx.x];
+    const uint32_t r0 = b * kChopReads;
+    const uint32_t nr = min(kChopReads, A.n_reads - r0);
     const uint32_t cap = (uint32_t)(base[blockIdx.x + 1] - base[blockIdx.x]);
     dmx_chop_hit* H = scratch + base[blockIdx.x];
-    dmx_chop_hit* Sh = sorted + base[blockIdx.x];
+    dmx_chop_hit* T = temp + base[blockIdx.x];
     uint32_t* cnt = counter + blockIdx.x;
-    const uint32_t nsegs = (A.lens[read] + kChopSeg - 1u) / kChopSeg;
-    for (uint32_t task = threadIdx.x; task < nsegs * (uint32_t)NL; task += blockDim.x) {
+    chop_segment_prefix(A, r0, nr, s_cnt, s_pre);
+    const uint32_t total = s_pre[nr] * (uint32_t)NL;
+    for (uint32_t task = threadIdx.x; task < total; task += blockDim.x) {
         const uint32_t sg = task / (uint32_t)NL;
         const int lab = (int)(task - sg * (uint32_t)NL);
-        chop_scan<-1>(A, s_lab[lab], lab, read, sg, cnt, H, cap);
+        const uint32_t t = chop_last_le(s_pre, nr, sg);
+        chop_scan<-1>(A, s_lab[lab], lab, r0 + t, sg - s_pre[t], cnt, H, cap);
     }
     __syncthreads();
-    const uint32_t nh = min(*cnt, cap);
+    const uint32_t nh = min(atomicAdd(cnt, 0u), cap);
     for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x) {
         dmx_chop_hit h = H[i];
         h.start = chop_start(A, s_lab[h.label ^ 1], h.read, h.dist, (uint32_t)h.stop);
         H[i] = h;
+        atomicAdd(&s_cnt[h.read - r0], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t t = 0; t < nr; ++t) {
+            s_off[t] = acc;
+            acc += s_cnt[t];
+            s_cnt[t] = 0u;
+        }
+        s_off[nr] = acc;
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x) {
-        const dmx_chop_hit x = H[i];
-        uint32_t rank = 0;
-        for (uint32_t j = 0; j < nh; ++j) rank += hit_less(H[j], x) ? 1u : 0u;
-        Sh[rank] = x;
+        const dmx_chop_hit h = H[i];
+        const uint32_t t = h.read - r0;
+        T[s_off[t] + atomicAdd(&s_cnt[t], 1u)] = h;
     }
     __syncthreads();
-    dmx_chop_seg* G = reinterpret_cast<dmx_chop_seg*>(H);   // H is free now
-    if (threadIdx.x == 0) {
-        uint32_t ns = 0;
-        for (uint32_t a = 0; a + 1 < nh;) {
-            const dmx_chop_hit h1 = Sh[a], h2 = Sh[a + 1];
-            const int ri = s_rule[h1.label * kChopMaxLabels + h2.label];
-            if (ri >= 0) {
-                dmx_chop_seg sg;
-                sg.read = read;
-                const int32_t x0 = keep ? h1.start : h1.stop;
-                const int32_t x1 = keep ? h2.stop : h2.start;
-                sg.start = x0;
-                sg.stop = max(x0, x1);
-                sg.strand = (int16_t)s_rstrand[ri];
-                sg.rule = (int16_t)ri;
-                G[ns++] = sg;
-                a += 2;
-            } else {
-                ++a;
-            }
+    for (uint32_t t = 0; t < nr; ++t) {   // block-uniform
+        const uint32_t o = s_off[t], c = s_off[t + 1] - o;
+        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
+            const dmx_chop_hit x = T[o + i];
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < c; ++j) rank += hit_less(T[o + j], x) ? 1u : 0u;
+            H[o + rank] = x;
         }
-        s_ns = ns;
-        s_hbase = (uint32_t)atomicAdd(&A.ctr[0], (unsigned long long)nh);
-        s_sbase = (uint32_t)atomicAdd(&A.ctr[1], (unsigned long long)ns);
-        A.blk[4 * read + 0] = s_hbase;   // rpb == 1: block index = read index
-        A.blk[4 * read + 1] = nh;
-        A.blk[4 * read + 2] = s_sbase;
-        A.blk[4 * read + 3] = ns;
-        A.nhit[read] = nh;
-        A.nseg[read] = ns;
     }
     __syncthreads();
-    const uint64_t hb = s_hbase, sb = s_sbase;
-    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x)
-        if (hb + i < A.hit_cap) A.hits[hb + i] = Sh[i];
-    for (uint32_t i = threadIdx.x; i < s_ns; i += blockDim.x)
-        if (sb + i < A.seg_cap) A.segs[sb + i] = G[i];
+    chop_pair_write(A, b, r0, nr, nh, keep, s_rule, s_rstrand, H,
+                    reinterpret_cast<dmx_chop_seg*>(T), s_off, s_sc, s_soff, s_base);
 }
 
 // Exclusive scan of the per-block hit / segment counts (one block; a few 100k entries).
@@ -521,19 +534,18 @@ struct ChopState {
     uint32_t* d_blkoff = nullptr;
     size_t blk_cap = 0;
     unsigned long long* d_ctr = nullptr;
-    uint32_t* d_ovf = nullptr;            // rpb == 1 overflow list (read, count)
-    size_t ovf_cap = 0;
+    uint32_t* d_ovf = nullptr;            // overflowing blocks (block, count), blk_cap entries
     uint64_t* d_ovf_base = nullptr;       // chop_big_kernel: hit-list bases, scratch, counters
     dmx_chop_hit* d_big = nullptr;
     size_t big_cap = 0;
     uint32_t* d_big_cnt = nullptr;
-    size_t big_reads_cap = 0;
+    size_t big_blocks_cap = 0;
     uint64_t n_hits = 0, n_segs = 0;
     size_t n_reads = 0;
     bool done = false;
     hipEvent_t ev[4] = {};
     float ms[2] = {0.f, 0.f};
-    uint32_t rpb = kChopReads;
+    size_t n_big = 0;   // blocks redone by chop_big_kernel in the last exec
     int hb = -1;   // chop_kernel variant: last-row bit in the high (1) / low (0) half, or mixed
 };
 
@@ -731,16 +743,16 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
         CHOP_CK(dev_realloc(&s->d_segs, cap));
         s->seg_cap = cap;
     }
-    uint32_t rpb = kChopReads;
     unsigned long long ctr[4] = {0, 0, 0, 0};
-    uint32_t nb = 0;
+    const uint32_t nb = (uint32_t)((n + kChopReads - 1) / kChopReads);
+    if (s->blk_cap < nb || !s->d_blk) {
+        CHOP_CK(dev_realloc(&s->d_blk, 4 * (size_t)nb));
+        CHOP_CK(dev_realloc(&s->d_blkoff, 2 * (size_t)nb));
+        CHOP_CK(dev_realloc(&s->d_ovf, 2 * (size_t)nb));
+        s->blk_cap = nb;
+    }
+    size_t n_big = 0;
     for (;;) {
-        nb = (uint32_t)((n + rpb - 1) / rpb);
-        if (s->blk_cap < nb || !s->d_blk) {
-            CHOP_CK(dev_realloc(&s->d_blk, 4 * (size_t)nb));
-            CHOP_CK(dev_realloc(&s->d_blkoff, 2 * (size_t)nb));
-            s->blk_cap = nb;
-        }
         CHOP_CK(hipMemsetAsync(s->d_ctr, 0, 4 * sizeof(unsigned long long), st));
         ChopArgs A;
         A.seq = c->d_seq;
@@ -748,7 +760,6 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
         A.offs = c->d_offs;
         A.lens = c->d_lens;
         A.n_reads = (uint32_t)n;
-        A.rpb = rpb;
         A.panel = s->d_panel;
         A.hits = s->d_hstage;
         A.segs = s->d_sstage;
@@ -758,12 +769,8 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
         A.nseg = s->d_nseg;
         A.blk = s->d_blk;
         A.ctr = s->d_ctr;
-        if (rpb == 1 && s->ovf_cap < n) {
-            CHOP_CK(dev_realloc(&s->d_ovf, 2 * n));
-            s->ovf_cap = n;
-        }
         A.ovf = s->d_ovf;
-        A.ovf_cap = rpb == 1 ? s->ovf_cap : 0;
+        A.ovf_cap = nb;
         CHOP_CK(hipEventRecord(s->ev[0], st));
         if (nb) {
             if (s->hb == 1) hipLaunchKernelGGL(chop_kernel<1>, dim3(nb), dim3(kChopBlock), 0, st, A);
@@ -775,12 +782,9 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
         CHOP_CK(hipMemcpyAsync(ctr, s->d_ctr, 4 * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost, st));
         CHOP_CK(hipStreamSynchronize(st));
-        if ((ctr[2] & 1ull) && rpb > 1) {
-            rpb = rpb > 8 ? 8u : 1u;
-            continue;
-        }
-        if (ctr[2] & 1ull) {   // rpb == 1: redo each overflowing read with a global hit list
-            const size_t no = (size_t)ctr[3];
+        n_big = 0;
+        if (ctr[2] & 1ull) {   // blocks whose hits overflowed the LDS list: redo them alone
+            const size_t no = (size_t)std::min<unsigned long long>(ctr[3], nb);
             std::vector<uint32_t> ovf(2 * no);
             CHOP_CK(hipMemcpy(ovf.data(), s->d_ovf, ovf.size() * 4, hipMemcpyDeviceToHost));
             std::vector<uint64_t> base(no + 1, 0);
@@ -789,10 +793,10 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
                 CHOP_CK(dev_realloc(&s->d_big, 2 * base[no]));
                 s->big_cap = base[no];
             }
-            if (s->big_reads_cap < no + 1 || !s->d_ovf_base) {
+            if (s->big_blocks_cap < no + 1 || !s->d_ovf_base) {
                 CHOP_CK(dev_realloc(&s->d_ovf_base, no + 1));
                 CHOP_CK(dev_realloc(&s->d_big_cnt, no + 1));
-                s->big_reads_cap = no + 1;
+                s->big_blocks_cap = no + 1;
             }
             CHOP_CK(hipMemcpyAsync(s->d_ovf_base, base.data(), (no + 1) * 8,
                                    hipMemcpyHostToDevice, st));
@@ -805,6 +809,7 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
             CHOP_CK(hipMemcpyAsync(ctr, s->d_ctr, 4 * sizeof(unsigned long long),
                                    hipMemcpyDeviceToHost, st));
             CHOP_CK(hipStreamSynchronize(st));
+            n_big = no;
         }
         if (ctr[0] >= (1ull << 32) || ctr[1] >= (1ull << 32)) {
             c->err = "dmx_chop_exec: more than 2^32 hits in one batch";
@@ -827,7 +832,7 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
         }
         break;
     }
-    s->rpb = rpb;
+    s->n_big = n_big;
     CHOP_CK(hipEventRecord(s->ev[2], st));
     if (nb) {
         hipLaunchKernelGGL(chop_blkscan_kernel, dim3(1), dim3(1024), 0, st,
@@ -886,5 +891,5 @@ extern "C" int dmx_chop_stats(dmx_ctx* c, float* ms, int n_ms) {
         return DMX_E_STATE;
     }
     for (int i = 0; i < n_ms && i < 2; ++i) ms[i] = s->ms[i];
-    return (int)s->rpb;
+    return (int)s->n_big;
 }

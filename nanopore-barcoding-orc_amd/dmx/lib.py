@@ -291,8 +291,8 @@ class Context:
 
     def chop_stats(self):
         ms = (ctypes.c_float * 2)()
-        rpb = self._check(self._L.dmx_chop_stats(self._h, ms, 2), "dmx_chop_stats")
-        return {"chop": float(ms[0]), "order": float(ms[1]), "reads_per_block": int(rpb)}
+        nbig = self._check(self._L.dmx_chop_stats(self._h, ms, 2), "dmx_chop_stats")
+        return {"chop": float(ms[0]), "order": float(ms[1]), "big_blocks": int(nbig)}
 
     def n_counts(self) -> int:
         a1 = 0 if self.mode == MODE_SINGLE else self.panel_sizes[1]
