@@ -282,3 +282,37 @@ def test_pychopper_dropin_matches_oracle(tmp_path, q):
     assert int(st[("Classification", "QC_fail")]) == len(exp["qcfail"])
     assert int(st[("Classification", "Unusable")]) == len(exp["unclass"])
     assert len(exp["pass"]) > 0.6 * len(seqs)
+
+
+@pytest.mark.gpu
+def test_pychopper_fasta_and_empty_inputs(tmp_path):
+    """FASTA input (no qualities: no QC, FASTA outputs) matches the oracle; an empty input still
+    creates every output and reports cutoff NA."""
+    names, seqs, _ = _records(np.random.default_rng(37), 300)
+    fa = tmp_path / "in.fasta"
+    fa.write_text("".join(f">{n}\n{s}\n" for n, s in zip(names, seqs)))
+    out = {k: str(tmp_path / f"{k}.fasta") for k in ("rescued", "unclass", "short")}
+    cmd = [BIN, "-b", chop.PRIMERS_FASTA, "-c", chop.CONFIG_FILE, "-q", "0.15", "-p",
+           "-w", out["rescued"], "-u", out["unclass"], "-l", out["short"], "-m", "edlib", str(fa),
+           str(tmp_path / "pass.fasta")]
+    subprocess.run(cmd, check=True)
+    primers, text = _ref_setup()
+    exp = ochop.chop_records([(n, s, None) for n, s in zip(names, seqs)], primers, text, 0.15,
+                             keep=True, min_len=50, fasta=True)
+
+    def read_fa(path):
+        lines = open(path).read().split("\n")
+        return [(lines[i][1:], lines[i + 1]) for i in range(0, len(lines) - 1, 2)]
+
+    assert read_fa(str(tmp_path / "pass.fasta")) == [(h, s) for h, s, _ in exp["pass"]]
+    for k in ("rescued", "unclass", "short"):
+        assert read_fa(out[k]) == [(h, s) for h, s, _ in exp[k]]
+    empty = tmp_path / "empty.fastq"
+    empty.write_text("")
+    stats = tmp_path / "empty_stats.out"
+    subprocess.run([BIN, "-b", chop.PRIMERS_FASTA, "-c", chop.CONFIG_FILE, "-u",
+                    str(tmp_path / "e_unclass.fastq"), "-S", str(stats), str(empty),
+                    str(tmp_path / "e_pass.fastq")], check=True)
+    assert os.path.getsize(tmp_path / "e_pass.fastq") == 0
+    assert os.path.exists(tmp_path / "e_unclass.fastq")
+    assert "Parameters\tcutoff\tNA" in stats.read_text()
