@@ -31,6 +31,7 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CUs x 4 SIMD32 x 2.4 GHz, 32-bit lane-ops
 VALU_CEILING = 48.5e12       # measured: v_bitop3 chains, full occupancy (tools/microbench)
 FILTER_OPS_PER_COLUMN = 30.7  # PMC: SQ_INSTS_VALU x 64 / filter columns (profiles/r1_pmc_*)
+CHOP_OPS_PER_COLUMN = 48.67   # PMC: same for chop_kernel (profiles/r1_pmc_summary_chop_c2_10M.txt)
 
 
 def filter_algorithmic_bytes(lengths: np.ndarray, n_windows: int) -> float:
@@ -43,7 +44,7 @@ def filter_algorithmic_bytes(lengths: np.ndarray, n_windows: int) -> float:
 
 
 def pmc_traffic(workload: str, reads: int):
-    """HBM bytes per filter launch from the committed rocprofv3 PMC summary (FETCH_SIZE and
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary (FETCH_SIZE and
     WRITE_SIZE passes, corrected per MI355X_MICROARCH.md), if one exists for this workload."""
     path = os.path.join(ROOT, "profiles", "filter_pmc_traffic.json")
     try:
@@ -119,6 +120,7 @@ def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutof
     # Myers columns: every label over the read, plus m + k warm-up columns per later segment
     extra = np.maximum(np.ceil(L / 512) - 1, 0)
     cols = sum(float(np.sum(L + extra * (m + int(cutoff * m)))) for m in label_lens)
+    traffic, traffic_src = pmc_traffic("chop", args.reads)
     return {
         "metric": "Mreads/s pychopper-style reorientation (01_pychopper.sh: -m edlib -p, "
                   "M13 SP5/SP27 primers)",
@@ -132,11 +134,19 @@ def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutof
                                "-p, inputs resident in HBM",
                    "cutoff": cutoff, "reads_per_gpu": args.reads, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": round(alg_bytes),
                      "kernel": "dmx::chop_kernel", "avg_launch_ms": round(kern_ms, 3),
                      "note": "VALU-bound bit-vector scan (DESIGN.md §8d)"},
-        "valu": {"columns_per_s": cols / (kern_ms / 1e3)},
+        "valu": {"columns_per_s": cols / (kern_ms / 1e3),
+                 "lane_ops_per_column": CHOP_OPS_PER_COLUMN,
+                 "lane_ops_per_s": cols / (kern_ms / 1e3) * CHOP_OPS_PER_COLUMN,
+                 "frac_of_measured_ceiling": cols / (kern_ms / 1e3) * CHOP_OPS_PER_COLUMN
+                 / VALU_CEILING,
+                 "measured_ceiling_lane_ops_per_s": VALU_CEILING,
+                 "source": "ops/column = SQ_INSTS_VALU x 64 / Myers columns of the timed launch "
+                           "(cutoff 0.15, profiles/r1_pmc_summary_chop_c2_10M.txt)"},
         "stage_ms_per_step": {k: round(v / K, 3) for k, v in ms.items()},
         "hits_per_read": round(n_hits / max(1, len(L)), 4),
         "segments_per_read": round(n_segs / max(1, len(L)), 4),
