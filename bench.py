@@ -31,7 +31,7 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CUs x 4 SIMD32 x 2.4 GHz, 32-bit lane-ops
 VALU_CEILING = 48.5e12       # measured: v_bitop3 chains, full occupancy (tools/microbench)
 FILTER_OPS_PER_COLUMN = 30.7  # PMC: SQ_INSTS_VALU x 64 / filter columns (profiles/r1_pmc_*)
-CHOP_OPS_PER_COLUMN = 48.67   # PMC: same for chop_kernel (profiles/r1_pmc_summary_chop_c2_10M.txt)
+CHOP_OPS_PER_COLUMN = 46.47   # PMC: same for chop_kernel (profiles/r1_pmc_summary_chop_c2_10M.txt)
 
 
 def filter_algorithmic_bytes(lengths: np.ndarray, n_windows: int) -> float:

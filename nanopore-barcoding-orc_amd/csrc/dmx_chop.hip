@@ -151,23 +151,34 @@ __device__ __forceinline__ void chop_scan(const ChopArgs& A, const ChopLabel& L,
         for (int q = 0; q < 16; ++q)
             eqv[q] = L.peq[((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            if ((uint32_t)q < cnt) {
-                myers_step<HB>(eqv[q], pv, mv, d, hbit);
-                const uint32_t j = p + (uint32_t)q + 1u;
-                if (d <= k) {
-                    if (!run) {
-                        run = true;
-                        owned = j > s0 && j <= s1;
-                        best = d;
-                        bstop = j;
-                    } else if (d < best) {
-                        best = d;
-                        bstop = j;
+        for (int h = 0; h < 16; h += 8) {
+            // quiet stretch: outside a run with d > k + 8, |D(j) - D(j-1)| <= 1 keeps the next 8
+            // columns above k, so when every lane of the wave is quiet and has 8 columns left
+            // they take bare steps (no run tracking, no per-column exec masking).
+            if (__all(!run && d > k + 8 && cnt >= (uint32_t)h + 8u)) {
+#pragma unroll
+                for (int q = h; q < h + 8; ++q) myers_step<HB>(eqv[q], pv, mv, d, hbit);
+                continue;
+            }
+#pragma unroll
+            for (int q = h; q < h + 8; ++q) {
+                if ((uint32_t)q < cnt) {
+                    myers_step<HB>(eqv[q], pv, mv, d, hbit);
+                    const uint32_t j = p + (uint32_t)q + 1u;
+                    if (d <= k) {
+                        if (!run) {
+                            run = true;
+                            owned = j > s0 && j <= s1;
+                            best = d;
+                            bstop = j;
+                        } else if (d < best) {
+                            best = d;
+                            bstop = j;
+                        }
+                    } else if (run) {
+                        run = false;
+                        if (owned) chop_push(s_nh, s_hit, cap, read, lab, best, bstop);
                     }
-                } else if (run) {
-                    run = false;
-                    if (owned) chop_push(s_nh, s_hit, cap, read, lab, best, bstop);
                 }
             }
         }
