@@ -511,6 +511,7 @@ int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uin
     }
     CK(hipStreamSynchronize(c->stream));
     c->executed = false;
+    chop_invalidate(c);
     return DMX_OK;
 }
 

@@ -574,6 +574,10 @@ void chop_release(Ctx* c) {
     c->chop = nullptr;
 }
 
+void chop_invalidate(Ctx* c) {
+    if (c->chop) c->chop->done = false;   // results belong to the previous resident batch
+}
+
 }  // namespace dmx
 
 using namespace dmx;

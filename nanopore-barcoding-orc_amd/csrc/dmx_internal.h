@@ -79,6 +79,7 @@ struct Ctx {
 };
 
 void chop_release(Ctx* c);
+void chop_invalidate(Ctx* c);   // a new dmx_load makes the last dmx_chop_exec's results stale
 int launch_round(Ctx* c, int round, hipStream_t st);
 int launch_finalize(Ctx* c, int round, hipStream_t st);
 

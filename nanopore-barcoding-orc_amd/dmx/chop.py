@@ -170,6 +170,16 @@ class Chopper:
         return best
 
 
+def sample_packed(p: lib.Packed, idx: np.ndarray) -> lib.Packed:
+    """The reads `idx` of a packed batch as a batch of their own (same packed words, truncated
+    after the last sampled read): the autotune runs over the sample only."""
+    offs = np.ascontiguousarray(p.offsets[idx])
+    lens = np.ascontiguousarray(p.lengths[idx])
+    end = int((offs + lens).max()) if len(idx) else 0
+    words = min(p.n_words, (end + lib.PACK_PAD + 31) // 32 * 2 + 4)
+    return lib.Packed(p.seq2b[:words], p.nmask[:words], offs, lens)
+
+
 def build_parser():
     p = argparse.ArgumentParser(prog="pychopper",
                                 description="dmx: MI355X drop-in for pychopper (-m edlib)")
@@ -236,9 +246,11 @@ def run(argv=None) -> int:
                         continue
                     qc_ok = (np.ones(n, dtype=bool) if batch.fasta
                              else batch.mean_qual() >= args.min_qual)
+                    if cutoff is None:   # tune on the -Y sample alone, then load the batch
+                        ctx.load(sample_packed(batch.packed,
+                                               np.nonzero(qc_ok)[0][:args.autotune_n]))
+                        cutoff = ch.autotune(np.arange(ctx._n_loaded))
                     ctx.load(batch.packed)
-                    if cutoff is None:
-                        cutoff = ch.autotune(np.nonzero(qc_ok)[0][:args.autotune_n])
                     ch.set_cutoff(cutoff)
                     nseg, segs = ch.run()
                     sink.write_rows(batch, *plan_rows(nseg, segs, batch.lens, qc_ok,

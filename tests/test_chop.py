@@ -232,6 +232,24 @@ def test_chop_reads_beyond_the_lds_hit_list(ctx):
         assert ctx.chop_stats()["big_blocks"] >= 1
 
 
+@pytest.mark.gpu
+def test_chop_fetch_after_new_load_is_refused(ctx):
+    """A dmx_load replaces the resident batch, so the previous dmx_chop_exec's results are stale:
+    dmx_chop_fetch must return DMX_E_STATE rather than copy the old batch's per-read counts into
+    buffers sized for the new one."""
+    rng = np.random.default_rng(5)
+    primers, text = _ref_setup()
+    rules = chop.parse_config(text, [p[0] for p in primers])
+    _gpu(ctx, _reads(rng, 300), primers, rules, 0.1, True)
+    blob, offs, lens = oracle.pack_ascii(_reads(rng, 20))
+    ctx.load(lib.pack(blob, offs, lens))
+    with pytest.raises(lib.DmxError, match=r"\(-5\)"):
+        ctx.chop_fetch()
+    ctx.chop_exec()
+    nseg, _, _, _ = ctx.chop_fetch()
+    assert len(nseg) == 20
+
+
 def _records(rng, n):
     seqs = _reads(rng, n)
     quals = []
