@@ -9,7 +9,10 @@ length mean 1.2 kb, synthetic 24 x 24 M13 panel, -e 0.1, --rc.
 
 Multi-GPU (torchrun): one process per GPU, reads sharded by contiguous range (rank r processes
 reads [r*N, (r+1)*N) of one seeded generation: weak scaling), one RCCL all-reduce of the
-per-bin counts per step (the only exchange the path has).
+per-bin counts per step inside libdmx (dmx_allreduce_counts on the library's stream; the only
+exchange the path has).  torch.distributed (gloo) is the control plane only: it hands rank 0's
+RCCL id to the other ranks, and carries the barrier and the max-over-ranks time.  At N=1 the
+step runs the same all-reduce on a single-rank communicator.
 
 Prints ONE JSON line on rank 0 (see README "Benchmark contract").
 """
@@ -260,14 +263,15 @@ def main():
     dist = None
     dev = local_rank
     # DMX_DIST_BACKEND=gloo: rehearse the N-rank path with several ranks sharing the GPUs of a
-    # smaller box (RCCL refuses two ranks on one device); the default is RCCL over xGMI.
+    # smaller box (RCCL refuses two ranks on one device: the counts then go over gloo); the
+    # default is libdmx's RCCL all-reduce over xGMI.
     backend = os.environ.get("DMX_DIST_BACKEND", "nccl")
     if world > 1:
         import torch
         import torch.distributed as tdist
         dev = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev)
-        tdist.init_process_group(backend)
+        tdist.init_process_group("gloo")   # control plane: id hand-off, barrier, max time
         dist = tdist
     on_gpu = backend == "nccl"
 
@@ -288,6 +292,11 @@ def main():
 
     linked = args.workload == "c5"
     ctx = lib.Context(dev)
+    if on_gpu and not chop_mode:   # the per-bin count exchange: RCCL inside libdmx
+        cid = [lib.comm_unique_id() if rank == 0 else None]
+        if dist is not None:
+            dist.broadcast_object_list(cid, src=0)
+        ctx.comm_init_rank(cid[0], world, rank)
     if chop_mode:
         return chop_main(args, ctx, packed, tune, lengths, gen_s, world, rank, dist, on_gpu)
     if linked:   # 04_cleaning_primers.sh:377: -g F...R per pair, no --rc
@@ -302,14 +311,10 @@ def main():
     del packed
 
     def allreduce_counts():
-        c = ctx.counts()
-        if dist is not None:
-            import torch
-            t = torch.from_numpy(c.astype(np.int64))
-            t = t.cuda() if on_gpu else t
-            dist.all_reduce(t)
-            c = t.cpu().numpy()
-        return c
+        if on_gpu:   # ncclAllReduce of the counts in HBM, ordered after the exec on its stream
+            return ctx.allreduce_counts()
+        from dmx import dist as ddist   # gloo rehearsal (ranks sharing a GPU)
+        return ddist.allreduce_counts(ctx.counts())
 
     def barrier_sync():
         ctx.sync()
@@ -354,7 +359,7 @@ def main():
         raise SystemExit(f"pipeline flags {flags}: cluster overflow or window violation")
     if dist is not None:
         import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
+        tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -411,7 +416,7 @@ def chop_main(args, ctx, packed, tune, lengths, gen_s, world, rank, dist, on_gpu
     elapsed = time.perf_counter() - t
     if dist is not None:
         import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
+        tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     K = args.steps

@@ -104,13 +104,35 @@ int dmx_device_count(void);
 /* Multi-GPU form of dmx_run: the batch (dmx_pack layout) is split into
  * n_ctx contiguous read ranges balanced by total length, each range runs on its own context
  * (one device each) from its own host thread, and results land in `out` in input order.
- * out_counts (optional, n_counts entries) receives the per-bin counts summed over the shards
- * (the exchange is a few hundred integers; the per-read results come to the host anyway).
- * Returns the number of count entries (or DMX_OK without out_counts), negative on error
+ * out_counts (optional, n_counts entries) receives the per-bin counts summed over the shards:
+ * when the contexts are one dmx_comm_init_all set (in that order), by an RCCL all-reduce of the
+ * devices' count arrays over xGMI; otherwise (e.g. several contexts sharing one device) on the
+ * host.  Returns the number of count entries (or DMX_OK without out_counts), negative on error
  * (message via dmx_last_error(ctxs[0])).  Contexts must share mode and panels. */
 int dmx_run_multi(dmx_ctx* const* ctxs, int n_ctx, const uint32_t* seq2b, const uint32_t* nmask,
                   const uint64_t* offsets, const uint32_t* lens, size_t n_words, size_t n_reads,
                   dmx_result* out, uint64_t* out_counts, size_t n_counts);
+
+/* ---- Multi-GPU count exchange (RCCL over xGMI) -------------------------------
+ * Replaces: the per-adapter totals of the reference's single cutadapt process per panel
+ * (scripts/02_cutadapt_loop.sh:64-72,91-103, `-j 24` workers on one node, report.py); sharded
+ * over GPUs, each shard's (A0+1)(A1+1)+2 counts are summed in HBM by one ncclAllReduce.
+ * One process, several GPUs: dmx_comm_init_all over contexts on distinct devices (ncclCommInitAll;
+ * rank k = ctxs[k]); dmx_run_multi then reduces its counts with RCCL.
+ * One process per GPU: rank 0 calls dmx_comm_unique_id and hands the DMX_COMM_ID_BYTES bytes to
+ * every rank (any control plane), each rank calls dmx_comm_init_rank (ncclCommInitRank; blocks
+ * until all ranks joined), then after each dmx_exec dmx_allreduce_counts (collective: every rank
+ * calls it) sums the ranks' counts in place on the context's stream and copies them to
+ * out_counts (optional); dmx_counts then returns the summed counts until the next dmx_exec.
+ * dmx_close releases the communicator. */
+#define DMX_COMM_ID_BYTES 128
+int dmx_comm_unique_id(uint8_t* id);
+int dmx_comm_init_rank(dmx_ctx* ctx, const uint8_t* id, int n_ranks, int rank);
+int dmx_comm_init_all(dmx_ctx* const* ctxs, int n_ctx);
+/* Number of ranks of the context's communicator (0 = none). */
+int dmx_comm_size(dmx_ctx* ctx);
+/* Returns the number of count entries, negative on error. */
+int dmx_allreduce_counts(dmx_ctx* ctx, uint64_t* out_counts, size_t n_out);
 
 /* Device-resident form (benchmarks / pipelined hosts): dmx_load copies a packed batch to HBM
  * once; dmx_exec enqueues the full pipeline on the context's stream (asynchronous); dmx_sync

@@ -66,6 +66,12 @@ int dev_alloc(Ctx* c, T** p, size_t count) {
 }
 
 
+// (A0+1)(A1+1) per-bin counts + 2 RC counts (include/dmx.h dmx_counts)
+size_t counts_size(const Ctx* c) {
+    const size_t a1 = c->mode == DMX_MODE_SINGLE ? 0 : (size_t)c->panel[1].n;
+    return ((size_t)c->panel[0].n + 1) * (a1 + 1) + 2;
+}
+
 int ensure_pipeline(Ctx* c) {
     const size_t n = c->n_reads;
     const bool linked = c->mode == DMX_MODE_LINKED;
@@ -117,8 +123,7 @@ int ensure_pipeline(Ctx* c) {
         c->win_cap = want_win;
         c->pair_cap = 4 * want_win;
     }
-    const size_t a1 = c->mode == DMX_MODE_SINGLE ? 0 : (size_t)c->panel[1].n;
-    const size_t nc = ((size_t)c->panel[0].n + 1) * (a1 + 1) + 2;
+    const size_t nc = counts_size(c);
     if (c->n_counts != nc) {
         int rc;
         if ((rc = dev_alloc(c, &c->d_counts, nc))) return rc;
@@ -163,6 +168,23 @@ int grow_clusters(Ctx* c) {
 
 }  // namespace
 
+namespace dmx {
+
+int reset_counts(Ctx* c) {
+    CK(hipSetDevice(c->device));
+    const size_t nc = counts_size(c);
+    if (c->n_counts != nc || !c->d_counts) {
+        int rc;
+        if ((rc = dev_alloc(c, &c->d_counts, nc))) return rc;
+        c->n_counts = nc;
+    }
+    CK(hipMemsetAsync(c->d_counts, 0, nc * sizeof(unsigned long long), c->stream));
+    CK(hipStreamSynchronize(c->stream));
+    return DMX_OK;
+}
+
+}  // namespace dmx
+
 
 extern "C" {
 
@@ -201,6 +223,7 @@ void dmx_close(dmx_ctx* c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     chop_release(c);
+    comm_release(c);
     void* bufs[] = {c->d_seq_alloc, c->d_nmask_alloc,     c->d_offs,     c->d_lens,      c->d_res,
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
                     c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_pairs, c->d_counters,
@@ -701,13 +724,22 @@ int dmx_run_multi(dmx_ctx* const* ctxs, int n_ctx, const uint32_t* seq2b, const 
         }
         for (int j = 1; j <= n_ctx; ++j) cut[j] = std::max(cut[j], cut[j - 1]);
     }
+    // one dmx_comm_init_all set over exactly these contexts: the counts are summed on the
+    // devices by RCCL; otherwise (contexts sharing a device, no communicator) on the host
+    bool rccl = out_counts && c0->comm_group != 0 && c0->comm_ranks == n_ctx;
+    for (int k = 1; k < n_ctx && rccl; ++k)
+        rccl = ctxs[k]->comm_group == c0->comm_group && ctxs[k]->comm_rank == k;
+    if (rccl && c0->comm_rank != 0) rccl = false;
     std::vector<int> rcs(n_ctx, DMX_OK);
     std::vector<std::vector<uint64_t>> cnt(n_ctx);
     auto shard = [&](int k) {
         dmx_ctx* c = ctxs[k];
         const size_t lo = cut[k], hi = cut[k + 1];
         const size_t n = hi - lo;
-        if (!n) return;   // nothing to run; its counts are zero
+        if (!n) {   // nothing to run; its counts are zero
+            if (rccl) rcs[k] = reset_counts(c);
+            return;
+        }
         uint64_t g0 = 0;
         {
             if (offsets[lo] < (uint64_t)DMX_PACK_PAD || offsets[lo] % kPackAlign) {
@@ -732,7 +764,7 @@ int dmx_run_multi(dmx_ctx* const* ctxs, int n_ctx, const uint32_t* seq2b, const 
         const size_t words =
             std::min(n_words - w0, (size_t)((end + DMX_PACK_PAD + 31) / 32 * 2 + 4));
         int rc = dmx_run(c, seq2b + w0, nmask + g0 / 32, offs.data(), lens + lo, words, n, out + lo);
-        if (rc == DMX_OK && out_counts) {
+        if (rc == DMX_OK && out_counts && !rccl) {
             cnt[k].assign(c->n_counts, 0);
             rc = dmx_counts(c, cnt[k].data(), cnt[k].size());
             if (rc > 0) rc = DMX_OK;
@@ -752,6 +784,7 @@ int dmx_run_multi(dmx_ctx* const* ctxs, int n_ctx, const uint32_t* seq2b, const 
             return rcs[k];
         }
     }
+    if (rccl) return allreduce_counts_group(ctxs, n_ctx, out_counts, n_counts);
     if (out_counts) {
         size_t nc = 0;
         for (int k = 0; k < n_ctx; ++k) nc = std::max(nc, cnt[k].size());

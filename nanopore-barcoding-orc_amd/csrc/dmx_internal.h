@@ -8,6 +8,8 @@
 #include "../../include/dmx.h"
 #include "dmx_device.h"
 
+struct ncclComm;   // RCCL (rccl/rccl.h: ncclComm_t = ncclComm*)
+
 namespace dmx {
 
 struct ChopState;   // read reorientation (dmx_chop.hip)
@@ -76,9 +78,16 @@ struct Ctx {
                               // [9+2r] after filter, [10+2r] after verify
     bool executed = false;
     ChopState* chop = nullptr;   // dmx_chop_* state, created by dmx_chop_set
+
+    // RCCL communicator for the per-bin count exchange (dmx_comm.cpp)
+    ncclComm* comm = nullptr;
+    int comm_ranks = 0, comm_rank = 0;
+    uint64_t comm_group = 0;     // nonzero: made by dmx_comm_init_all (one process, grouped calls)
 };
 
 void chop_release(Ctx* c);
+void comm_release(Ctx* c);
+int reset_counts(Ctx* c);      // size d_counts for the current panels/mode and zero it (sync)
 void chop_invalidate(Ctx* c);   // a new dmx_load makes the last dmx_chop_exec's results stale
 int launch_round(Ctx* c, int round, hipStream_t st);
 int launch_finalize(Ctx* c, int round, hipStream_t st);
@@ -87,3 +96,8 @@ int launch_finalize(Ctx* c, int round, hipStream_t st);
 
 // The public opaque handle (include/dmx.h) is the host context.
 struct dmx_ctx : dmx::Ctx {};
+
+namespace dmx {
+// dmx_run_multi's grouped RCCL count all-reduce (dmx_comm.cpp)
+int allreduce_counts_group(dmx_ctx* const* ctxs, int n_ctx, uint64_t* out, size_t n_out);
+}  // namespace dmx

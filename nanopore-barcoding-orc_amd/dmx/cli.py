@@ -96,7 +96,7 @@ def run(argv=None) -> int:
         _unsupported("--rc with linked adapters is not implemented")
 
     devices = _devices(args)
-    ctxs = [lib.Context(d) for d in devices]
+    ctxs = lib.open_group(devices)
     for ctx in ctxs:
         _configure(ctx, ads, linked, args)
     level = 1 if args.zlevel1 else args.compression_level
@@ -116,22 +116,26 @@ def run(argv=None) -> int:
     stats = Stats(ads)
     stats.rc_mode = bool(args.rc)
     t0 = time.perf_counter()
+    a1 = len(ads) if linked else 0
+    totals = np.zeros((len(ads) + 1, a1 + 1), dtype=np.int64)
     sink = nio.Sink(paths, fasta_out, level, threads=args.cores)
     try:
         with nio.Reader(args.input, args.batch_mb << 20, threads=args.cores) as reader:
             for batch in reader:
                 try:
                     if len(batch):
-                        if len(ctxs) == 1:
-                            res = ctxs[0].run(batch.packed)
-                        else:
-                            res, _ = lib.run_multi(ctxs, batch.packed)
+                        res, cnt = lib.run_batch(ctxs, batch.packed)
+                        totals += lib.bin_totals(cnt, len(ads), len(ads) if linked else 0)
                         plan = _plan(res, ads, linked, demux, unmatched_to, batch.lens, stats)
                         sink.write(batch, *plan)
                 finally:
                     batch.free()
     finally:
         sink.close()
+    # per-adapter totals: the devices' bin counts (summed over GPUs by RCCL) must agree with the
+    # per-read results the outputs were written from
+    dev = np.diagonal(totals[1:, 1:]) if linked else totals[1:, 0]
+    stats.check_totals(dev)
     stats.n_out = int(sink.n_written.sum())
     stats.bp_out = int(sink.bp_written.sum())
     if args.json:

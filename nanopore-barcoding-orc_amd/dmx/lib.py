@@ -5,8 +5,10 @@ library is missing or no GPU is visible, the calls raise — there is no CPU fal
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -30,7 +32,9 @@ EXPORTS = ["dmx_abi_version", "dmx_open", "dmx_close", "dmx_last_error", "dmx_se
            "dmx_set_panel_mixed", "dmx_set_mode", "dmx_pack_words", "dmx_pack", "dmx_run", "dmx_load", "dmx_exec",
            "dmx_sync", "dmx_fetch", "dmx_counts", "dmx_stats", "dmx_device_count",
            "dmx_run_multi", "dmx_locate", "dmx_chop_set", "dmx_chop_exec", "dmx_chop_fetch",
-           "dmx_chop_stats"]
+           "dmx_chop_stats", "dmx_comm_unique_id", "dmx_comm_init_rank", "dmx_comm_init_all",
+           "dmx_comm_size", "dmx_allreduce_counts"]
+COMM_ID_BYTES = 128
 
 LOC_IGNORE_CASE, LOC_ONLY_POSITIVE = 0x1, 0x2
 HIT_DTYPE = np.dtype([("seq", "<u8"), ("pattern", "<i4"), ("strand", "<i4"), ("start", "<i4"),
@@ -96,6 +100,11 @@ def load() -> ctypes.CDLL:
     L.dmx_chop_exec.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     L.dmx_chop_fetch.argtypes = [P, P, P, P, c_size, P, c_size]
     L.dmx_chop_stats.argtypes = [P, ctypes.POINTER(ctypes.c_float), c_int]
+    L.dmx_comm_unique_id.argtypes = [P]
+    L.dmx_comm_init_rank.argtypes = [P, P, c_int, c_int]
+    L.dmx_comm_init_all.argtypes = [ctypes.POINTER(P), c_int]
+    L.dmx_comm_size.argtypes = [P]
+    L.dmx_allreduce_counts.argtypes = [P, c_u64p, c_size]
     if L.dmx_abi_version() != 3:
         raise DmxError("libdmx ABI mismatch")
     _lib = L
@@ -303,6 +312,26 @@ class Context:
         self._check(self._L.dmx_counts(self._h, out.ctypes.data, len(out)), "dmx_counts")
         return out
 
+    # ---- RCCL count exchange (include/dmx.h "Multi-GPU count exchange") -----------------------
+    def comm_init_rank(self, comm_id: bytes, n_ranks: int, rank: int):
+        """Join an n_ranks RCCL communicator (one process per GPU); comm_id from
+        comm_unique_id() on rank 0.  Blocks until every rank has joined."""
+        buf = ctypes.create_string_buffer(bytes(comm_id), COMM_ID_BYTES)
+        with _stdout_to_stderr():
+            rc = self._L.dmx_comm_init_rank(self._h, buf, int(n_ranks), int(rank))
+        self._check(rc, "dmx_comm_init_rank")
+
+    def comm_size(self) -> int:
+        return self._check(self._L.dmx_comm_size(self._h), "dmx_comm_size")
+
+    def allreduce_counts(self) -> np.ndarray:
+        """Per-bin counts of the last exec summed over every rank (RCCL all-reduce in HBM on
+        this context's stream; collective)."""
+        out = np.zeros(self.n_counts(), dtype=np.uint64)
+        self._check(self._L.dmx_allreduce_counts(self._h, out.ctypes.data, len(out)),
+                    "dmx_allreduce_counts")
+        return out
+
     def stats(self):
         ms = (ctypes.c_float * 11)()
         cl = np.zeros(10, dtype=np.uint64)
@@ -320,6 +349,73 @@ class Context:
 def device_count() -> int:
     """Visible HIP devices (0 without a GPU)."""
     return int(load().dmx_device_count())
+
+
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """RCCL prints its version banner on stdout at initialisation; keep stdout for the callers'
+    own output (bench.py's one JSON line, CLI reports)."""
+    sys.stdout.flush()
+    libc = ctypes.CDLL(None)
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        libc.fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL communicator id (rank 0 draws it; every rank passes it to comm_init_rank)."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    with _stdout_to_stderr():
+        rc = load().dmx_comm_unique_id(buf)
+    if rc != 0:
+        raise DmxError(f"dmx_comm_unique_id failed ({rc})")
+    return buf.raw
+
+
+def comm_init_all(ctxs) -> bool:
+    """One RCCL communicator over contexts on distinct devices (ncclCommInitAll); run_multi then
+    sums its per-bin counts on the devices.  Returns False (no communicator) when contexts share
+    a device, where RCCL cannot place two ranks."""
+    if len({c.device for c in ctxs}) != len(ctxs):
+        return False
+    L = load()
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    with _stdout_to_stderr():
+        rc = L.dmx_comm_init_all(arr, len(ctxs))
+    if rc < 0:
+        msg = L.dmx_last_error(ctxs[0]._h)
+        raise DmxError(f"dmx_comm_init_all failed ({rc}): {msg.decode() if msg else ''}")
+    return True
+
+
+def open_group(devices) -> list:
+    """One context per device; contexts on distinct devices share one RCCL communicator
+    (dmx_comm_init_all), so run_batch sums their per-bin counts on the GPUs over xGMI."""
+    ctxs = [Context(d) for d in devices]
+    if len(ctxs) > 1:
+        comm_init_all(ctxs)
+    return ctxs
+
+
+def run_batch(ctxs, p: Packed):
+    """One packed batch on one or several contexts: (per-read results, per-bin counts).  With
+    several contexts the batch is sharded by dmx_run_multi (counts all-reduced by RCCL when the
+    contexts are one open_group communicator)."""
+    if len(ctxs) == 1:
+        res = ctxs[0].run(p)
+        return res, ctxs[0].counts()
+    return run_multi(ctxs, p)
+
+
+def bin_totals(counts: np.ndarray, a0: int, a1: int) -> np.ndarray:
+    """dmx_counts layout -> matrix [bin1 + 1, bin2 + 1] ((A0+1) x (A1+1); A1 = 0 in SINGLE mode;
+    row/column 0 = no match)."""
+    return np.asarray(counts[:(a0 + 1) * (a1 + 1)], dtype=np.int64).reshape(a0 + 1, a1 + 1)
 
 
 def run_multi(ctxs, p: Packed):

@@ -102,7 +102,7 @@ def run(argv=None) -> int:
     ads1, ads2 = aset1.adapters, aset2.adapters
     n1, n2 = [a.name for a in ads1], [a.name for a in ads2]
 
-    ctxs = [lib.Context(d) for d in _devices(args)]
+    ctxs = lib.open_group(_devices(args))
     for ctx in ctxs:
         ctx.set_panel(0, [a.seq for a in ads1], lib.DMX_FRONT | lib.DMX_RC, args.e_rate, 3)
         ctx.set_panel(1, [a.seq for a in ads2], lib.DMX_BACK | lib.DMX_RC, args.e_rate, 3)
@@ -138,6 +138,7 @@ def run(argv=None) -> int:
     bp2_out = np.zeros(len(n1), np.int64)
     prof = dict(read_wait=0.0, gpu=0.0, plan_write=0.0, drain=0.0)
     n2_out = np.zeros(len(n1), np.int64)
+    totals = np.zeros((len(n1) + 1, len(n2) + 1), dtype=np.int64)   # device bin counts
     try:
         with nio.Reader(infile, args.batch_mb << 20, threads=args.threads) as reader:
             while True:
@@ -150,10 +151,8 @@ def run(argv=None) -> int:
                     if not len(batch):
                         continue
                     tw = time.perf_counter()
-                    if len(ctxs) == 1:
-                        res = ctxs[0].run(batch.packed)
-                    else:
-                        res, _ = lib.run_multi(ctxs, batch.packed)
+                    res, cnt = lib.run_batch(ctxs, batch.packed)
+                    totals += lib.bin_totals(cnt, len(n1), len(n2))
                     prof["gpu"] += time.perf_counter() - tw
                     tw = time.perf_counter()
                     (s1, e1, o1), (s2, e2, o2, nrc2) = plan_rounds(res, batch.lens)
@@ -189,6 +188,10 @@ def run(argv=None) -> int:
     if os.environ.get("DMX_PROFILE_IO"):
         print("io profile (s): " + ", ".join(f"{k} {v:.3f}" for k, v in prof.items()),
               file=sys.stderr)
+    # the devices' (SP5, SP27) bin counts (RCCL-summed over GPUs) vs the per-read results
+    st1.check_totals(totals[1:, :].sum(axis=1))
+    for i, s in enumerate(st2):
+        s.check_totals(totals[i + 1, 1:])
     st1.n_out = int(sink1.n_written.sum())
     st1.bp_out = int(sink1.bp_written.sum())
     for i, s in enumerate(st2):

@@ -56,6 +56,14 @@ class Stats:
             if r[a]:
                 self.on_rc[a] += int(r[a])
 
+    def check_totals(self, totals):
+        """Per-adapter match totals counted on the GPU(s) (dmx_counts, all-reduced over devices)
+        must equal those derived from the per-read results."""
+        got = [int(x) for x in totals]
+        want = [self.matches[a] for a in range(len(self.adapters))]
+        if got != want:
+            raise RuntimeError(f"device bin counts {got} disagree with per-read results {want}")
+
     def to_json(self, argv, cores, in_path, error_rate):
         adapters = []
         for a, ad in enumerate(self.adapters):
