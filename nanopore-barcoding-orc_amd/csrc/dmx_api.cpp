@@ -119,9 +119,9 @@ int ensure_pipeline(Ctx* c) {
         int rc;
         if ((rc = dev_alloc(c, &c->d_win, want_win))) return rc;
         if ((rc = dev_alloc(c, &c->d_win2, want_win))) return rc;
-        if ((rc = dev_alloc(c, &c->d_pairs, 4 * want_win))) return rc;
+        if ((rc = dev_alloc(c, &c->d_tasks, 4 * want_win))) return rc;
         c->win_cap = want_win;
-        c->pair_cap = 4 * want_win;
+        c->task_cap = 4 * want_win;
     }
     const size_t nc = counts_size(c);
     if (c->n_counts != nc) {
@@ -149,9 +149,9 @@ int grow_windows(Ctx* c) {
     int rc;
     if ((rc = dev_alloc(c, &c->d_win, want))) return rc;
     if ((rc = dev_alloc(c, &c->d_win2, want))) return rc;
-    if ((rc = dev_alloc(c, &c->d_pairs, 4 * want))) return rc;
+    if ((rc = dev_alloc(c, &c->d_tasks, 4 * want))) return rc;
     c->win_cap = want;
-    c->pair_cap = 4 * want;
+    c->task_cap = 4 * want;
     return DMX_OK;
 }
 
@@ -204,8 +204,8 @@ int dmx_open(int device, dmx_ctx** out) {
     c->no_verify = nv && nv[0] == '1';
     const char* rs = std::getenv("DMX_RESOLVE");
     c->force_ring = rs && std::strcmp(rs, "ring") == 0;
-    const char* ns = std::getenv("DMX_SCREEN");   // index screen before the window scan
-    c->no_sieve = !(ns && ns[0] == '1');          // (experimental, off by default)
+    const char* ns = std::getenv("DMX_NO_SCREEN");   // A/B: no index screen before the
+    c->no_screen = ns && ns[0] == '1';               // window scan
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -226,7 +226,7 @@ void dmx_close(dmx_ctx* c) {
     comm_release(c);
     void* bufs[] = {c->d_seq_alloc, c->d_nmask_alloc,     c->d_offs,     c->d_lens,      c->d_res,
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
-                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_pairs, c->d_counters,
+                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_tasks, c->d_counters,
                     c->d_counts,    c->d_panel[0],  c->d_panel[1]};
     for (void* b : bufs)
         if (b) hipFree(b);
@@ -424,17 +424,19 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
             dp.off_max = mmax - pre;
             dp.m_max = mmax;
             // index screen: every adapter's middle block I_a = rows [pre, m - flen) fits a
-            // 32-bit word, and a piece keeps >= 16 candidate columns
-            int lmin = 64, lmx = 0;
+            // 32-bit word
+            int lmin = 64, lmx = 0, js = 0;
             for (int a = 0; a < n; ++a) {
                 lmin = std::min(lmin, lens[a] - pre - flen);
                 lmx = std::max(lmx, lens[a] - pre - flen);
+                js = std::max(js, lens[a] - pre + (int)hp.ad[a].kk);
             }
-            // FRONT panels only: a randomised sweep with the screen on (DMX_SCREEN=1) found 3
-            // of 1,075 cases where 3' (BACK) last-column cells of a prefix shorter than the
-            // shared prefix were screened out (absolute -e); the default path is exact there
-            hp.sieve = dp.where == kFront && lmin >= 1 && lmx <= 32 &&
-                       128 - 15 - 4 * kf - lmx - pre - flen - 1 >= 16;
+            hp.screen = lmin >= 1 && lmx <= 32;
+            dp.jsplit = js;
+            bool shared = true;   // rows <= pre: identical acceptance for every adapter
+            for (int a = 1; a < n; ++a)
+                for (int L = 0; L <= pre; ++L) shared &= hp.ad[a].acc[L] == hp.ad[0].acc[L];
+            dp.pshared = shared ? 1 : 0;
             for (int i = 0; i < pre; ++i) {
                 const uint8_t mask = iupac_mask(seqs[0][i]);
                 for (int code = 0; code < 4; ++code)
@@ -635,10 +637,10 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
     CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
     if (getenv("DMX_DEBUG_STATS"))
         fprintf(stderr,
-                "dmx stats: windows raw %u %u verified %u %u screen pieces %u %u (all-pass %u %u) "
-                "pairs %u %u cand %u %u %u %u\n",
-                cnt[4], cnt[5], cnt[10], cnt[11], cnt[18], cnt[22], cnt[19], cnt[23], cnt[12],
-                cnt[13], cnt[6], cnt[7], cnt[8], cnt[9]);
+                "dmx stats: windows raw %u %u verified %u %u screened tasks %u %u "
+                "(by 3' cells only %u %u) cand %u %u %u %u\n",
+                cnt[4], cnt[5], cnt[10], cnt[11], cnt[12], cnt[13], cnt[19], cnt[23], cnt[6],
+                cnt[7], cnt[8], cnt[9]);
     if (counts) {
         const bool b0 = c->band_ok[0] && !c->force_ring, b1 = c->band_ok[1] && !c->force_ring;
         const uint64_t v[10] = {cnt[0],
@@ -658,7 +660,7 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
         if (cnt[0] > c->cl_cap || cnt[1] > c->cl_cap) f |= 1;
         if (cnt[4] > c->win_cap || cnt[5] > c->win_cap) f |= 4;
         if (cnt[10] > c->win_cap || cnt[11] > c->win_cap) f |= 4;
-        if (cnt[12] > c->pair_cap || cnt[13] > c->pair_cap) f |= 4;
+        if (cnt[12] > c->task_cap || cnt[13] > c->task_cap) f |= 4;
         for (int x = 6; x < 10; ++x)
             if (cnt[x] > c->cand_cap) f |= 8;
         *flags = f;

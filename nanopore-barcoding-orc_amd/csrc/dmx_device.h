@@ -69,11 +69,21 @@ struct DevPanel {
     int32_t pre_len;
     int32_t off_min, off_max;
     int32_t m_max;
+    // Index screen: every adapter is P + I_a + S with |I_a| in 1..32.
+    int32_t jsplit;      // FRONT: a last-row cell at column j >= jsplit contains every row of I_a
+    int32_t pshared;     // acceptance tables agree on rows <= pre_len for every adapter, so a
+                         // 3' last-column cell inside P is identical for all adapters
     uint32_t pre_peq[8];
     DevAdapter ad[kMaxAdapters];
 };
 
 // A column range of one (item, orientation) that the per-adapter window scan must cover.
+// info (set by verify, read by the index screen): bits 0-7 = a lower bound of the shared-prefix
+// block's cost in every full alignment ending in the window (0 if not computed), bits 8-15 = the
+// same for the prefix block ending near the view end (3' last-column cells), bit 16 = some 3'
+// last-column cell inside the shared prefix (rows <= pre_len) may be accepted, bits 24-31 = the
+// prefix block's bound for 3' cells ending inside an index block (P within l_max - 1 + kf of the
+// end).
 struct Window {
     uint32_t item;
     uint8_t o;
@@ -81,20 +91,10 @@ struct Window {
     uint8_t strand;      // oriented view of the item (copied so the window scan needs no
     uint8_t bmin;        // dependent loads): strand, start, len, read length n, first nt off;
     uint32_t j1, j2;     // bmin = min suffix-block cost over the hits (255 = no hit)
-    uint32_t n, start, len, pad2;
+    uint32_t n, start, len, info;
     uint64_t off;
 };
 static_assert(sizeof(Window) == 40, "Window layout");
-
-// A window piece with the candidate column range [jlo, jhi] (a piece of the window's [j1, j2])
-// and the adapters that survived the index screen (bit a); the window scan runs only those.
-struct Pair {
-    uint32_t win;
-    uint32_t jlo, jhi;
-    uint32_t pad;
-    uint64_t mask;
-};
-static_assert(sizeof(Pair) == 24, "Pair layout");
 
 constexpr int kStageCap = 256;    // LDS staging of emitted records per block
 constexpr int kCandStageCap = 128; // per candidate list

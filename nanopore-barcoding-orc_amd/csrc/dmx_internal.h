@@ -15,7 +15,7 @@ namespace dmx {
 struct ChopState;   // read reorientation (dmx_chop.hip)
 
 struct HostPanel {
-    bool sieve = false;       // index screen usable (filter + verify, index blocks <= 32)
+    bool screen = false;      // index screen usable (filter + verify, index blocks 1..32)
     int n = 0;
     int n_orient = 1;
     bool set = false;
@@ -70,9 +70,9 @@ struct Ctx {
     uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows, [6+2r..] candidates, [10+r] verified windows, [16+4r..] diag
     unsigned long long* d_counts = nullptr;
     unsigned long long* d_linked = nullptr;
-    Pair* d_pairs = nullptr;             // window sieve survivors
-    size_t pair_cap = 0;
-    bool no_sieve = true;                // index screen on only with DMX_SCREEN=1   // linked mode: best pair key per read
+    Window* d_tasks = nullptr;           // index screen survivors (window piece of one adapter)
+    size_t task_cap = 0;
+    bool no_screen = false;              // DMX_NO_SCREEN=1: every window runs every adapter
     size_t n_counts = 0;
     hipEvent_t ev[13] = {};   // [3r..3r+2] round r stages, [6+r] finalize, [8] start,
                               // [9+2r] after filter, [10+2r] after verify

@@ -45,10 +45,10 @@ struct RoundArgs {
     Outcome* cand_out[2];
     uint32_t* cand_count;        // [2]
     uint32_t cand_cap;
-    int32_t sieve;               // 1: the window scan runs the sieve's surviving pairs
-    Pair* pairs;
-    uint32_t* pair_count;
-    uint32_t pair_cap;
+    int32_t screen;              // 1: the window scan runs the index screen's surviving pairs
+    Window* tasks;               // index screen survivors: window pieces of one adapter each
+    uint32_t* task_count;
+    uint32_t task_cap;
 };
 
 struct TaskView {
@@ -98,12 +98,17 @@ __device__ __forceinline__ uint32_t slot_of(const RoundArgs& R, uint32_t item, i
     return R.slot_div ? 2u * item + (uint32_t)(sub >= R.slot_div) : item;
 }
 
+// Row stride of the code-major match tables in LDS: lanes of one window read one code row at
+// consecutive adapters; windows sharing a wave read other codes' rows, shifted by 24 banks
+// (a power-of-two stride put every code's copy of adapter a in the same bank).
+constexpr int kPeqStride = kMaxAdapters + 24;
+
 __device__ __forceinline__ void load_panel_lds(const DevPanel* P, uint64_t* s_peq, int8_t* s_acc,
                                                int8_t* s_pacc) {
     const int A = P->n_adapters;
     for (int x = threadIdx.x; x < 8 * A; x += blockDim.x) {
         const int c = x / A, a = x % A;   // code-major, power-of-two row stride (no multiply)
-        s_peq[c * kMaxAdapters + a] = P->ad[a].peq[c];   // lanes of one read: consecutive words
+        s_peq[c * kPeqStride + a] = P->ad[a].peq[c];   // lanes of one read: consecutive words
     }
     for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) {
         s_acc[x] = P->ad[x / 72].acc[x % 72];
@@ -176,7 +181,7 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
 #define DMX_SCAN_STEP(q)                                                                  \
     {                                                                                     \
         const uint32_t code = ((codes >> (2 * (q))) & 3u) | (((nb >> (q)) & 1u) << 2);    \
-        myers_step(peq[code * kMaxAdapters], pv, mv, d, hbit);                                       \
+        myers_step(peq[code * kPeqStride], pv, mv, d, hbit);                              \
         if (d <= kk) {                                                                    \
             const uint32_t j = p0 + (q) + 1;                                              \
             const int lr = min(m, (int)j + d);                                            \
@@ -405,7 +410,7 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
 #define DMX_CAND_EQ                                                                       \
     uint64_t eqv[16];                                                                     \
     _Pragma("unroll") for (int q = 0; q < 16; ++q)                                        \
-        eqv[q] = peq[(((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)) * kMaxAdapters];
+        eqv[q] = peq[(((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)) * kPeqStride];
 
     uint32_t p0 = js;
     uint32_t ncodes, nnb;             // next chunk, prefetched one chunk ahead
@@ -518,7 +523,7 @@ __device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const Sink& si
 // Full scan (panels without a usable shared suffix): one lane per (item, orientation, adapter).
 template <bool BAND>
 __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
-    __shared__ uint64_t s_peq[8 * kMaxAdapters];
+    __shared__ uint64_t s_peq[8 * kPeqStride];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
     __shared__ int8_t s_pacc[72 * kMaxAdapters];
     DMX_STAGES
@@ -580,7 +585,7 @@ __device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskVi
     w.n = tv.n;
     w.start = tv.start;
     w.len = tv.len;
-    w.pad2 = 0;
+    w.info = 0;
     w.off = tv.off;
     return w;
 }
@@ -785,11 +790,16 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     if (threadIdx.x < 8) s_fpeq[threadIdx.x] = P->filter_peq[threadIdx.x];
     if (threadIdx.x < 72) s_pf[threadIdx.x] = P->pf[threadIdx.x];
     if (threadIdx.x == 0) s_wcnt = 0;
-    {   // hit threshold of the column after view position p: min(kf_far, pf[min(p+1+kf, 71)])
-        const int kf0 = P->kf;
-        const int far0 = min(kf0, (int)P->pf[71]);
-        s_thr[threadIdx.x] =
-            (int8_t)min(far0, (int)P->pf[min((int)threadIdx.x + 1 + kf0, 71)]);
+    {   // hit threshold of column j = p + 1 (view position p): the largest cost d <= kf_far that
+        // an acceptable last-row cell (m, j) of some adapter can have.  Its aligned adapter length
+        // is at most j + d, so d <= pf[min(71, j + d)]; b(j) <= d.  (Near the view start this is
+        // much tighter than d <= pf[j + kf]: a column j < min_overlap never hits.)
+        const int far0 = min((int)P->kf, (int)P->pf[71]);
+        const int j = (int)threadIdx.x + 1;
+        int t = -1;
+        for (int d = 0; d <= far0; ++d)
+            if (d <= (int)P->pf[min(j + d, 71)]) t = d;
+        s_thr[threadIdx.x] = (int8_t)t;
     }
 
     // segment counts per view, grouped by strand; block-wide exclusive scan
@@ -944,7 +954,7 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
         const uint32_t wi = base + threadIdx.x;
         if (wi < total) {
-            const Window w = R.win[wi];
+            Window w = R.win[wi];
             const int len = (int)w.len;
             const bool rows_free = (front && (int)w.j1 <= P->max_mk) || w.bmin == 255;
             // column ranges the prefix block must be evaluated on
@@ -959,6 +969,7 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
                 hi = len;
             }
             bool keep = rows_free && w.bmin != 255;    // near-start FRONT window: keep as is
+            uint32_t info = 0;                         // Window.info for the index screen
             if (!keep && hi >= 0) {
                 lo = max(lo, 0);
                 hi = min(hi, len);
@@ -975,10 +986,17 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
                 if (js < 0) js = 0;
                 uint32_t pv = ~0u, mv = 0u;
                 int d = L;
-                int dmin_rows = 1 << 20, dmin_end = 1 << 20;
+                int dmin_rows = 1 << 20, dmin_end = 1 << 20, dmin_near = 1 << 20;
+                // P ending this close to the end: 3' cells holding P and part of an index block
+                const int near_lo = len - (P->m_max - P->filter_len - L - 1) - kf;
                 const uint32_t hbit = (uint32_t)(L - 1);
                 const int rlo = w.bmin == 255 ? (1 << 30) : (int)w.j1 - P->off_max - kf;
                 const int rhi = (int)w.j2 - P->off_min + kf;
+                if (js == 0) {   // column 0 itself (3' panels: D(L, 0) = L)
+                    if (rlo <= 0 && rhi >= 0) dmin_rows = L;
+                    if (end_lo <= 0) dmin_end = L;
+                    if (near_lo <= 0) dmin_near = L;
+                }
                 for (int p0 = js; p0 < hi; p0 += 16) {
                     uint32_t codes, nb;
                     fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, (uint32_t)p0, codes,
@@ -990,19 +1008,31 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
                         const int j = p0 + q + 1;
                         if (j >= rlo && j <= rhi) dmin_rows = min(dmin_rows, d);
                         if (j >= end_lo) dmin_end = min(dmin_end, d);
+                        if (j >= near_lo) dmin_near = min(dmin_near, d);
                     }
                 }
                 if (!rows_free && (int)w.bmin + dmin_rows <= kf) keep = true;
+                // Index-screen bounds of the prefix block's cost: the restricted start is exact
+                // where D_pre <= kf and never lowers D, so min(dmin, kf + 1) is a lower bound of
+                // the true minimum as far as any test against a threshold <= kf can tell.
+                if (!rows_free) info = (uint32_t)min(dmin_rows, kf + 1);
                 if (w.lastcol) {
                     if (dmin_end <= kf) keep = true;                  // whole prefix block at end
+                    info |= (uint32_t)min(dmin_end, kf + 1) << 8;      // P ending near the end
+                    info |= (uint32_t)min(dmin_near, kf + 1) << 24;    // ... within l_max + kf
                     int dd = 0;                                       // prefix cells at column len
-                    for (int i = 1; i < L && !keep; ++i) {
+                    bool pcell = false;
+                    for (int i = 1; i <= L; ++i) {
                         dd += (int)((pv >> (i - 1)) & 1u) - (int)((mv >> (i - 1)) & 1u);
-                        if (dd <= (int)s_pf[i]) keep = true;
+                        pcell |= dd <= (int)s_pf[i];
                     }
-                    if (hi == 0) keep = true;                         // empty view: trivial
+                    if (pcell || hi == 0) {                           // (hi == 0: empty view)
+                        keep = true;
+                        info |= 1u << 16;
+                    }
                 }
             }
+            w.info = info;
             if (keep) st.push(w);
         }
         __syncthreads();
@@ -1011,244 +1041,180 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
     st.flush();
 }
 
-// Window scan: one lane per (window, adapter); block-uniform grid-stride over the device-side
-// window count so that the block can flush its staged records between strides.
 // ---------------------------------------------------------------------------------------------
-// index screen (before the window scan).  Every adapter of a filtered + verified panel is
-// P + I_a + S: the shared prefix P (pre_len rows), its own index block I_a (l_a <= 32 rows) and
-// the shared suffix S (filter_len rows).  A candidate cell of adapter a at column j in [jlo, jhi]
-// with cost d <= kk_a restricts to an alignment of I_a ending at a column x2 in
-// [j - s - kf, j - s + kf] (S spans s +- c_S read characters, c_S <= d <= kf) with cost
-// <= d - c_S <= kk_a - bmin (c_S >= b(j) >= the window's bmin).  So a 32-bit Myers of I_a alone
-// (free start in the read; FRONT windows at the view start with the zero column, which also
-// covers alignments that skip into or past I_a) over [x_lo, x_hi] = [jlo - s - kf, jhi - s + kf]
-// must reach cost <= kk_a - bmin somewhere, or adapter a has no candidate in the piece.
-// 3' windows at the view end (last-column cells (i, len), S or I_a cut by the read end) use
-// threshold kk_a, test the index block's last column rows too, and let every adapter through
-// when a prefix-only cell (i <= pre_len, identical for all adapters) may be accepted.
-// Survivors (window piece, adapter) go to the window scan, which decides every cell exactly.
-// One lane per window piece; adapters in a block-uniform loop (LDS broadcast of the index
-// vectors); the piece's read codes sit in a lane-private LDS column.
+// index screen (between verify and the window scan).  Every adapter of a filtered
+// + verified panel is P + I_a + S: the shared prefix P (pre_len rows), its own index block I_a
+// (l_a = m_a - pre_len - filter_len rows, 1..32) and the shared suffix S.  Splitting an alignment
+// at the block boundaries splits its cost: c_P + c_I + c_S <= d, where the I_a band is an
+// alignment of all of I_a ending at some column x2 with |j - x2 - |S|| <= c_S <= kf.
+//   last-row cells (m, j): c_S >= bmin (the filter's block cost at every hit column of the
+//     window), c_P >= the verify's prefix bound, so D_I(l_a, x2) <= kk_a - bmin - c_P for some
+//     x2 in [j1 - |S| - kf, j2 - |S| + kf].  FRONT cells at j < jsplit may skip rows of I_a at
+//     column 0: that part of a window (the "near piece") keeps every adapter.
+//   3' last-column cells (i, len): i <= pre_len is identical for every adapter (only the first
+//     adapter needs it when the acceptance tables agree); otherwise P ends within
+//     m_max - 1 - pre_len + kf columns of the end, at cost >= dPe (verify), and
+//     pre_len < i < pre_len + l_a needs dPn + D_I(i - pre_len, len) <= acc_a[i] (dPn: P ending
+//     within l_max - 1 + kf columns of the end);
+//     i >= pre_len + l_a needs dPe + D_I(l_a, x2) <= kk_a for some x2 in [len - |S| + 1 - kf, len].
+// D_I is the 32-bit Myers of I_a alone with a free start in the read, started l_a + kk_a + 1
+// columns before the first column of interest with D(i) = i: exact wherever D <= kk_a, never
+// lower.  One lane per (window, adapter); each survivor becomes one task record (the window
+// piece with the adapter in `info`), so the window scan runs full waves of surviving tasks.
 // ---------------------------------------------------------------------------------------------
-constexpr int kSieveChunks = 8;
-constexpr int kSieveSpan = 16 * kSieveChunks;     // view positions held per lane
+__device__ __forceinline__ Window make_task(Window w, uint32_t jlo, uint32_t jhi, bool lastcol,
+                                            int a) {
+    w.lastcol = lastcol ? 1 : 0;
+    w.j1 = jlo;
+    w.j2 = jhi;
+    w.info = (uint32_t)a;       // a task is a window piece of one adapter
+    return w;
+}
 
-__global__ __launch_bounds__(kScanBlock) void sieve_kernel(RoundArgs R) {
-    __shared__ uint32_t s_ipeq[kMaxAdapters * 8];  // index block I_a: bit r = row p + r
-    __shared__ Pair s_pair[kStageCap];
-    __shared__ uint32_t s_pc, s_pb;
-    __shared__ uint2 s_code[kSieveChunks][kScanBlock];
-    __shared__ int s_l[kMaxAdapters], s_kk[kMaxAdapters];
-    __shared__ int8_t s_acc0[72];
+__global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
+    __shared__ uint32_t s_ipeq[8 * kPeqStride];     // code-major: [c][a], bit r = row pre_len + r
     __shared__ int8_t s_acc[72 * kMaxAdapters];
-    __shared__ uint32_t s_ppeq[8];
-    __shared__ uint32_t s_pfx[kScanBlock];
+    __shared__ Window s_task[kStageCap];
+    __shared__ uint32_t s_tc, s_tb, s_nend;
     const DevPanel* P = R.panel;
     const int A = P->n_adapters;
     const int pl = P->pre_len, sl = P->filter_len, kf = P->kf;
     for (int x = threadIdx.x; x < 8 * A; x += blockDim.x) {
-        const int a = x >> 3, c = x & 7;
+        const int c = x / A, a = x % A;
         const int l = (int)P->ad[a].m - pl - sl;
         const uint64_t v = c < 4 ? (P->ad[a].peq[c] >> pl) : 0ull;
-        s_ipeq[x] = (uint32_t)(l >= 32 ? v : (v & ((1ull << l) - 1ull)));
+        s_ipeq[c * kPeqStride + a] = (uint32_t)(l >= 32 ? v : (v & ((1ull << l) - 1ull)));
     }
-    int lmax = 0;
-    for (int a = 0; a < A; ++a) lmax = max(lmax, (int)P->ad[a].m - pl - sl);
-    for (int x = threadIdx.x; x < A; x += blockDim.x) {
-        s_l[x] = (int)P->ad[x].m - pl - sl;
-        s_kk[x] = P->ad[x].kk;
-    }
-    if (threadIdx.x < 72) s_acc0[threadIdx.x] = P->ad[0].acc[threadIdx.x];
     for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
-    if (threadIdx.x < 8) s_ppeq[threadIdx.x] = P->pre_peq[threadIdx.x];
-    if (threadIdx.x == 0) s_pc = 0;
+    if (threadIdx.x == 0) {
+        s_tc = 0;
+        s_nend = 0;
+    }
     __syncthreads();
-    const Stage<Pair> st{s_pair, &s_pc, &s_pb, R.pairs, R.pair_count, R.pair_cap, R.flags, 4u};
-    const Window* wl = R.win2;                        // screen runs only with verification
-    const uint32_t total = min(*R.win2_count, R.win_cap);
+    const Stage<Window> st{s_task, &s_tc, &s_tb, R.tasks, R.task_count, R.task_cap, R.flags, 4u};
+    const Window* wl = R.win2;
+    const uint32_t nwin = min(*R.win2_count, R.win_cap);
+    const uint32_t total = nwin * (uint32_t)A;    // host: win_cap * A < 2^32
     const bool front = P->where == kFront;
-    // candidate columns per piece: x_hi - xs + 15 <= kSieveSpan (host checks cr >= 16)
-    const int cr = kSieveSpan - 15 - 4 * kf - lmax - pl - sl - 1;
+    const int jsplit = front ? P->jsplit : 0;
+    const bool pshared = P->pshared != 0;
 
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
-        // pieces of this block's windows, flattened so every lane takes one piece per round
-        {
-            const uint32_t wi = base + threadIdx.x;
-            uint32_t np = 0;
-            if (wi < total) {
-                const Window w = wl[wi];
-                np = (w.j2 - w.j1) / (uint32_t)cr + 1;
-            }
-            s_pfx[threadIdx.x] = np;
-        }
-        __syncthreads();
-        for (uint32_t dlt = 1; dlt < kScanBlock; dlt <<= 1) {   // inclusive scan
-            const uint32_t x = threadIdx.x >= dlt ? s_pfx[threadIdx.x - dlt] : 0u;
-            __syncthreads();
-            s_pfx[threadIdx.x] += x;
-            __syncthreads();
-        }
-        const uint32_t npieces = s_pfx[kScanBlock - 1];
-        for (uint32_t pb = 0; pb < npieces; pb += kScanBlock) {
-            const uint32_t pi = pb + threadIdx.x;
-            const bool act = pi < npieces;
-            Window w;
-            uint32_t wi = 0, jlo = 1, jhi = 0;
-            if (act) {
-                uint32_t lo = 0, hi = kScanBlock - 1;  // first lane with inclusive prefix > pi
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (s_pfx[mid] > pi) hi = mid;
-                    else lo = mid + 1;
+        const uint32_t t = base + threadIdx.x;
+        if (t < total) {
+            const uint32_t wi = t / (uint32_t)A;
+            const int a = (int)(t - wi * (uint32_t)A);
+            const Window w = wl[wi];
+            const DevAdapter& ad = P->ad[a];
+            const int len = (int)w.len, j1 = (int)w.j1, j2 = (int)w.j2;
+            const int l = (int)ad.m - pl - sl, kk = ad.kk;
+            const int bm = w.bmin;
+            const int dP = (int)(w.info & 255u), dPe = (int)((w.info >> 8) & 255u);
+            const int dPn = (int)(w.info >> 24);
+            const bool lastc = !front && w.lastcol;
+            // the near piece [j1, min(j2, jsplit - 1)] keeps every adapter
+            if (j1 < jsplit) st.push(make_task(w, (uint32_t)j1, (uint32_t)min(j2, jsplit - 1),
+                                               false, a));
+            const int jr = max(j1, jsplit);               // far piece: last-row cells [jr, j2]
+            const int thr = kk - bm - dP;                 // (bm = 255: no hit column, no rows)
+            const bool rows = bm != 255 && jr <= j2 && thr >= 0;
+            // P-only last-column cells: identical for every adapter, the first one wins ties;
+            // an empty view keeps every adapter
+            bool pass = lastc && (len == 0 || (((w.info >> 16) & 1u) && (a == 0 || !pshared)));
+            bool by_end = true;                           // (diagnostic: no last-row reason)
+            const int thr_e = kk - dPe;                   // 3' cells holding all of I_a
+            if (!pass && (rows || lastc)) {
+                const int xr_lo = jr - sl - kf, xr_hi = j2 - sl + kf;
+                const int xe_lo = len - sl + 1 - kf;
+                int xs = 1 << 30, xe = -1;
+                if (rows) {
+                    xs = xr_lo;
+                    xe = min(xr_hi, len);
                 }
-                const uint32_t before = lo ? s_pfx[lo - 1] : 0u;
-                wi = base + lo;
-                w = wl[wi];
-                jlo = w.j1 + (pi - before) * (uint32_t)cr;
-                jhi = min(w.j2, jlo + (uint32_t)cr - 1);
-            } else {
-                w.j1 = 1;
-                w.j2 = 0;
-                w.lastcol = 0;
-                w.len = 0;
-                w.bmin = 255;
-            }
-            const int len = (int)w.len;
-            const bool lastc = act && !front && w.lastcol && jhi == w.j2;
-            const int bm = w.bmin == 255 ? 0 : (int)w.bmin;
-            bool all = false;
-            // FRONT columns j <= s + kf may hold S-only partial alignments (P and I_a skipped at
-            // column 0): identical for every adapter, so every adapter keeps that sub-range
-            if (act && front && (int)jlo <= sl + kf) {
-                const uint32_t jh = min(jhi, (uint32_t)(sl + kf));
-                Pair pr;
-                pr.win = wi;
-                pr.jlo = jlo;
-                pr.jhi = jh;
-                pr.pad = 0;
-                pr.mask = A >= 64 ? ~0ull : ((1ull << A) - 1ull);
-                st.push(pr);
-                jlo = jh + 1;
-            }
-            const bool act2 = act && jlo <= jhi;
-            const int x_lo = (int)jlo - sl - kf;               // index end columns
-            const int x_hi = lastc ? len : min(len, (int)jhi - sl + kf);
-            const int xp_lo = x_lo - lmax - kf;                // P end columns from here
-            const int xs = max(0, xp_lo - pl - kf - 1);        // restricted start (or column 0)
-            const bool zero = front && xs == 0;                // FRONT view start: zero column
-            const int nch = (act2 && x_hi > xs) ? (x_hi - xs + 15) / 16 : 0;
-            const int start = x_hi - 16 * nch;                 // chunk grid ends exactly at x_hi
-            for (int c = 0; c < nch; ++c) {
-                uint32_t cc, nn;
+                if (lastc) {
+                    xs = min(xs, xe_lo);
+                    xe = len;
+                }
+                // The I_a band starts where the P band ends: at or after x1 = jr - l - |S| - kf
+                // (last-row cells) or len - (m - 1 - pre_len) - kf (3' cells).  A restricted
+                // start D'(i, x0) = i at any x0 <= x1 gives every such band its cost or less, so
+                // the chunk grid (ending exactly at xe) starts at or before that column; columns in
+                // front of the view only lower D further.  Every column with D <= threshold thus
+                // tests <= threshold.
+                int x1 = 1 << 30;
+                if (rows) x1 = jr - l - sl - kf;
+                if (lastc) x1 = min(x1, len - ((int)ad.m - 1 - pl) - kf);
+                const int nch = (xe - x1 + 15) >> 4;
+                const int jb = xe - 16 * nch;
+                const int xrh = min(xr_hi, len);
+                const uint32_t* ip = s_ipeq + a;
+                const uint32_t hbit = (uint32_t)(l - 1);
+                uint32_t pv = ~0u, mv = 0u;
+                int d = l;
                 TaskView tv;
+                tv.read = 0;
                 tv.n = w.n;
                 tv.strand = w.strand;
                 tv.start = w.start;
                 tv.len = w.len;
                 tv.off = w.off;
-                fetch16s(R.seq, R.nmask, tv, start + 16 * c, cc, nn);
-                s_code[c][threadIdx.x] = make_uint2(cc, nn);
-            }
-            // shared prefix P: cP = min D_P(pl, x) over x in [xp_lo, x_hi] bounds the P part of
-            // every alignment in the piece; with 3' last-column cells also the rows at len
-            int cP = 1 << 20, cPe = 1 << 20;   // cPe: P ending within lmax + kf of len
-            {
-                const uint32_t neutral = zero ? ~0u : 0u;
-                uint32_t pv = zero ? 0u : ~0u, mv = 0u;
-                int d = zero ? 0 : pl;
-                if (zero && xp_lo <= 0) cP = 0;                // column 0 of the zero column
-                const int xe_lo = len - lmax - kf;
-                for (int c = 0; c < nch; ++c) {
-                    const int p0 = start + 16 * c;
-                    const uint2 cn = s_code[c][threadIdx.x];
-                    uint32_t e[16];
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) {
-                        e[q] = s_ppeq[((cn.x >> (2 * q)) & 3u) | (((cn.y >> q) & 1u) << 2)];
-                        if (p0 + q < xs) e[q] = neutral;
-                    }
-                    int mr = 1 << 20, me = 1 << 20;
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) {
-                        myers_step32(e[q], pv, mv, d, (uint32_t)(pl - 1));
-                        const int x = p0 + q + 1;
-                        mr = min(mr, x >= xp_lo ? d : (1 << 20));
-                        me = min(me, x >= xe_lo ? d : (1 << 20));
-                    }
-                    cP = min(cP, mr);
-                    cPe = min(cPe, me);
-                }
-                if (lastc && nch) {                    // prefix-only cells (i <= pl, at len)
-                    int dd = 0;
-                    for (int i = 1; i <= pl; ++i) {
-                        dd += (int)((pv >> (i - 1)) & 1u) - (int)((mv >> (i - 1)) & 1u);
-                        all |= dd <= (int)s_acc0[i];
-                    }
-                }
-            }
-            uint64_t smask = 0;
-            for (int a = 0; a < A; ++a) {
-                const int l = s_l[a];
-                const uint32_t hbit = (uint32_t)(l - 1);
-                const int thr = (lastc ? s_kk[a] : s_kk[a] - bm) - cP;
-                const uint32_t* ip = s_ipeq + 8 * a;
-                const uint32_t neutral = zero ? ~0u : 0u;      // keeps the initial column
-                uint32_t pv = zero ? 0u : ~0u, mv = 0u;
-                int d = zero ? 0 : l;
-                bool surv = all || (zero && x_lo <= 0 && thr >= 0);
-                for (int c = 0; c < nch; ++c) {
-                    const int p0 = start + 16 * c;
-                    const uint2 cn = s_code[c][threadIdx.x];
+                tv.o = w.o;
+                tv.a = a;
+                uint32_t c0 = 0, n0 = 0, c1 = 0, n1 = 0;   // two chunks in flight
+                if (nch > 0) fetch16s(R.seq, R.nmask, tv, jb, c0, n0);
+                if (nch > 1) fetch16s(R.seq, R.nmask, tv, jb + 16, c1, n1);
+                for (int k = 0; k < nch && !pass; ++k) {
+                    const int p0 = jb + 16 * k;
+                    const uint32_t codes = c0, nb = n0;
+                    c0 = c1;
+                    n0 = n1;
+                    if (k + 2 < nch) fetch16s(R.seq, R.nmask, tv, p0 + 32, c1, n1);
+                    // this chunk's columns p0+1 .. p0+16: the threshold of the regions it touches
+                    // and the first column counted (earlier ones are warm-up)
+                    const bool inR = rows && p0 + 16 >= xr_lo && p0 + 1 <= xrh;
+                    const bool inE = lastc && p0 + 16 >= xe_lo;
+                    const int tk = max(inR ? thr : -1, inE ? thr_e : -1);
+                    const int qlo = min(inR ? xr_lo : (1 << 30), inE ? xe_lo : (1 << 30)) - p0 - 1;
                     uint32_t eq[16];
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) {
-                        eq[q] = ip[((cn.x >> (2 * q)) & 3u) | (((cn.y >> q) & 1u) << 2)];
-                        if (p0 + q < xs) eq[q] = neutral;
+                    for (int q = 0; q < 16; ++q) eq[q] = ip[((codes >> (2 * q)) & 3u) * kPeqStride];
+                    if (__builtin_amdgcn_ballot_w64(nb != 0u)) {   // a non-ACGT byte: no match
+#pragma unroll
+                        for (int q = 0; q < 16; ++q)
+                            eq[q] &= ~(uint32_t)__builtin_amdgcn_sbfe((int)nb, q, 1);
                     }
-                    uint32_t hits = 0;
+                    int cm = 127;
 #pragma unroll
                     for (int q = 0; q < 16; ++q) {
                         myers_step32(eq[q], pv, mv, d, hbit);
-                        hits |= d <= thr ? (1u << q) : 0u;
+                        cm = min(cm, q >= qlo ? d : 127);
                     }
-                    // index end columns x = p0 + q + 1 in [x_lo, x_hi]
-                    const int lo = x_lo - p0 - 1, hi = x_hi - p0 - 1;
-                    const uint32_t mlo = lo <= 0 ? 0xFFFFu : (lo >= 16 ? 0u : (0xFFFFu << lo));
-                    const uint32_t mhi =
-                        hi >= 15 ? 0xFFFFu : (hi < 0 ? 0u : (0xFFFFu >> (15 - hi)));
-                    surv |= (hits & mlo & mhi & 0xFFFFu) != 0u;
+                    pass = cm <= tk;
+                    by_end = !inR;
                 }
-                if (lastc && !surv && nch) {           // cells (pl + r, len): P + part of I_a
+                if (lastc && !pass) {   // partial I_a at the read end: cells (pl + r, len)
                     int dd = 0;
-                    for (int r = 1; r < l; ++r) {
+                    for (int r = 1; r < l && !pass; ++r) {
                         dd += (int)((pv >> (r - 1)) & 1u) - (int)((mv >> (r - 1)) & 1u);
-                        surv |= cPe + dd <= (int)s_acc[a * 72 + pl + r];
+                        pass = dPn + dd <= (int)s_acc[72 * a + pl + r];
                     }
                 }
-                if (surv) smask |= 1ull << a;
             }
-            if (act2 && smask) {
-                Pair pr;
-                pr.win = wi;
-                pr.jlo = jlo;
-                pr.jhi = jhi;
-                pr.pad = 0;
-                pr.mask = smask;
-                st.push(pr);
+            if (pass) {
+                st.push(make_task(w, (uint32_t)jr, (uint32_t)j2, lastc, a));
+                if (by_end) atomicAdd(&s_nend, 1u);
             }
-            const int np = __syncthreads_count(act);   // also orders the staged count
-            const int na = __syncthreads_count(all);
-            if (threadIdx.x == 0) {
-                atomicAdd(&R.diag[2], (uint32_t)np);   // pieces (diagnostic)
-                atomicAdd(&R.diag[3], (uint32_t)na);   // pieces passing every adapter
-            }
-            if (s_pc > kStageCap / 2) st.flush();
         }
-        __syncthreads();                               // s_pfx is rewritten next
+        __syncthreads();                               // staged count is block-uniform here
+        if (s_tc > kStageCap / 2) st.flush();
     }
     st.flush();
+    if (threadIdx.x == 0 && s_nend) atomicAdd(&R.diag[3], s_nend);     // by 3' cells only
 }
 
+// Window scan: one lane per (window, adapter) — or, after the index screen, per surviving
+// (piece, adapter) — in a block-uniform grid stride over the device-side count, so that the
+// block can flush its staged records between strides.
 // One (window or piece, adapter) task of the window scan.
 template <bool BAND, class ClStage, class Sink>
 __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, int a, int A,
@@ -1287,7 +1253,7 @@ __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, 
 #endif
 template <bool BAND>
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_WSCAN_WAVES))) void wscan_kernel(RoundArgs R) {
-    __shared__ uint64_t s_peq[8 * kMaxAdapters];
+    __shared__ uint64_t s_peq[8 * kPeqStride];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
     __shared__ int8_t s_pacc[72 * kMaxAdapters];
     __shared__ Cluster s_cl[BAND ? 1 : kStageCap];
@@ -1310,52 +1276,24 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     const int A = R.panel->n_adapters;
     const Window* wl = R.panel->pre_len ? R.win2 : R.win;
     const uint32_t* wc = R.panel->pre_len ? R.win2_count : R.win_count;
-    if (R.sieve) {
-        // screened pieces: block-wise flattening of the survivor masks into (piece, adapter)
-        __shared__ uint32_t s_pre[kScanBlock];
-        const uint32_t np = min(*R.pair_count, R.pair_cap);
-        for (uint32_t base = blockIdx.x * blockDim.x; base < np; base += gridDim.x * blockDim.x) {
-            const uint32_t pi = base + threadIdx.x;
-            const uint64_t mk = pi < np ? R.pairs[pi].mask : 0ull;
-            s_pre[threadIdx.x] = (uint32_t)__popcll(mk);
-            __syncthreads();
-            for (uint32_t dlt = 1; dlt < kScanBlock; dlt <<= 1) {
-                const uint32_t x = threadIdx.x >= dlt ? s_pre[threadIdx.x - dlt] : 0u;
+    if (R.screen) {   // the index screen's surviving (window piece, adapter) tasks
+        const uint32_t nt = min(*R.task_count, R.task_cap);
+        const uint32_t stride = gridDim.x * blockDim.x;
+        uint32_t ti = blockIdx.x * blockDim.x + threadIdx.x;
+        Window wn;                                     // the next task, loaded one ahead
+        if (ti < nt) wn = R.tasks[ti];
+        for (uint32_t base = blockIdx.x * blockDim.x; base < nt; base += stride, ti += stride) {
+            const Window w = wn;
+            if (ti + stride < nt) wn = R.tasks[ti + stride];
+            if (ti < nt) wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, st, sink);
+            if constexpr (BAND) {
+                __builtin_amdgcn_wave_barrier();
+                if (sink.st[0].count() > kWaveCandCap / 2) sink.st[0].flush();
+                if (sink.st[1].count() > kWaveCandCap / 2) sink.st[1].flush();
+            } else {
                 __syncthreads();
-                s_pre[threadIdx.x] += x;
-                __syncthreads();
+                if (s_clcnt > kStageCap / 2) st.flush();
             }
-            const uint32_t ntask = s_pre[kScanBlock - 1];
-            for (uint32_t tb = 0; tb < ntask; tb += kScanBlock) {
-                const uint32_t ti = tb + threadIdx.x;
-                if (ti < ntask) {
-                    uint32_t lo = 0, hi = kScanBlock - 1;   // first record with prefix > ti
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (s_pre[mid] > ti) hi = mid;
-                        else lo = mid + 1;
-                    }
-                    const Pair pr = R.pairs[base + lo];
-                    uint32_t k = ti - (lo ? s_pre[lo - 1] : 0u);   // k-th set bit of the mask
-                    uint64_t mk2 = pr.mask;
-                    while (k--) mk2 &= mk2 - 1ull;
-                    const int a = __ffsll((unsigned long long)mk2) - 1;
-                    Window w = wl[pr.win];
-                    w.lastcol = (w.lastcol && pr.jhi == w.j2) ? 1 : 0;
-                    w.j1 = pr.jlo;
-                    w.j2 = pr.jhi;
-                    wscan_task<BAND>(R, w, a, A, s_peq, s_acc, s_pacc, st, sink);
-                }
-                if constexpr (BAND) {
-                    __builtin_amdgcn_wave_barrier();
-                    if (sink.st[0].count() > kWaveCandCap / 2) sink.st[0].flush();
-                    if (sink.st[1].count() > kWaveCandCap / 2) sink.st[1].flush();
-                } else {
-                    __syncthreads();
-                    if (s_clcnt > kStageCap / 2) st.flush();
-                }
-            }
-            __syncthreads();                           // s_pre is rewritten next
         }
         if constexpr (BAND) {
             __builtin_amdgcn_wave_barrier();
@@ -1672,7 +1610,7 @@ __device__ __forceinline__ void band_dp2(const uint8_t* rm, const uint32_t* seq,
     fetch16s(seq, nmask, tv, base + 16, w1, n1);
     fetch16s(seq, nmask, tv, base + 32, w2, n2);
     int o = 0;
-    uint32_t rnext = rm[0];
+    uint32_t rnext = rm[0];           // rm[i * kMaxAdapters]: row i's match mask (row-major table)
     for (int i = 1; i <= ie; ++i) {
         if (o == 16) {                 // uniform: every lane advances one row per iteration
             w0 = w1;
@@ -1686,7 +1624,7 @@ __device__ __forceinline__ void band_dp2(const uint8_t* rm, const uint32_t* seq,
         const uint32_t codes = o ? __builtin_amdgcn_alignbit(w1, w0, 2 * o) : w0;
         const uint32_t nb = ((n1 << 16) | n0) >> o;
         const uint32_t rmask = rnext;
-        rnext = rm[min(i, 63)];
+        rnext = rm[min(i, 63) * kMaxAdapters];
         int lc = INF, lp = 0;          // left neighbour (same row, already updated)
 #pragma unroll
         for (int k = 0; k < W; ++k) {
@@ -1728,17 +1666,20 @@ __device__ __forceinline__ void band_dp2(const uint8_t* rm, const uint32_t* seq,
 // its candidates (key order = locate's / best_match's / ReverseComplementer's selection order).
 template <int W>
 __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
-    __shared__ uint8_t s_rm[kMaxAdapters * 64];   // s_rm[a * 64 + i]: bit c = char i matches c
+    // s_rm[i * kMaxAdapters + a]: bit c = adapter a's char i matches read code c.  Row-major, so
+    // the lanes of a wave (one row i, different adapters) read neighbouring bytes: no bank
+    // conflicts (an adapter-major table put every adapter's row i in one of 4 banks).
+    __shared__ uint8_t s_rm[kMaxAdapters * 64];
     __shared__ uint32_t s_q[256];
     __shared__ uint32_t s_qi, s_qe, s_n;
     const DevPanel* P = R.panel;
     const int A = P->n_adapters;
     for (int x = threadIdx.x; x < 64 * A; x += blockDim.x) {
-        const DevAdapter& ad = P->ad[x >> 6];
-        const int i = x & 63;
+        const int a = x >> 6, i = x & 63;
+        const DevAdapter& ad = P->ad[a];
         uint32_t r = 0;
         for (int c = 0; c < 4; ++c) r |= (uint32_t)((ad.peq[c] >> i) & 1ull) << c;
-        s_rm[x] = (uint8_t)r;
+        s_rm[i * kMaxAdapters + a] = (uint8_t)r;
     }
     if (threadIdx.x == 0) {
         s_qi = 0;
@@ -1806,10 +1747,10 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
             tv.a = c.a;
             int c2, origin, score;
             if (threadIdx.x < ni)
-                band_dp2<W, false>(s_rm + 64 * c.a, R.seq, R.nmask, tv, ad.where == kFront, iend,
+                band_dp2<W, false>(s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend,
                                    j, c2, origin, score);
             else
-                band_dp2<W, true>(s_rm + 64 * c.a, R.seq, R.nmask, tv, ad.where == kFront, iend,
+                band_dp2<W, true>(s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend,
                                   j, c2, origin, score);
             if (c2 != cost) atomicOr(R.flags, 2u);    // band / scan disagreement: bug
             const int lr = iend + (origin < 0 ? origin : 0);
@@ -2178,10 +2119,11 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     }
     R.cand_count = c->d_counters + 6 + 2 * round;
     R.cand_cap = (uint32_t)c->cand_cap;
-    R.sieve = (band && hp.filter && hp.verify && hp.sieve && !linked && !c->no_sieve) ? 1 : 0;
-    R.pairs = c->d_pairs;
-    R.pair_count = c->d_counters + 12 + round;
-    R.pair_cap = (uint32_t)c->pair_cap;
+    R.screen = (hp.filter && hp.verify && hp.screen && !linked && !c->no_screen &&
+                (uint64_t)c->win_cap * (uint64_t)hp.n < (1ull << 32)) ? 1 : 0;
+    R.tasks = c->d_tasks;
+    R.task_count = c->d_counters + 12 + round;
+    R.task_cap = (uint32_t)c->task_cap;
     hipEventRecord(c->ev[round * 3 + 0], st);
     if (hp.filter && !linked) {   // linked primers: short, no shared suffix block; plain scan
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
@@ -2191,8 +2133,8 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         if (hp.verify)
             hipLaunchKernelGGL(verify_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
         hipEventRecord(c->ev[10 + 2 * round], st);
-        if (R.sieve)
-            hipLaunchKernelGGL(sieve_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
+        if (R.screen)
+            hipLaunchKernelGGL(iscreen_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         if (band) hipLaunchKernelGGL(wscan_kernel<true>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(wscan_kernel<false>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
     } else if (grid > 0) {

@@ -128,13 +128,13 @@ def test_error_rates_and_filter_toggle(ctx, e, monkeypatch):
     ctx.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC, e)
     ctx.set_mode(lib.MODE_TWO_ROUND)
     _assert_same(ctx.run(lib.pack(d["blob"], d["offsets"], d["lengths"])), exp)
-    monkeypatch.setenv("DMX_SCREEN", "1")
+    monkeypatch.setenv("DMX_NO_SCREEN", "1")
     with lib.Context(0) as c4:
         c4.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC, e)
         c4.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC, e)
         c4.set_mode(lib.MODE_TWO_ROUND)
         _assert_same(c4.run(lib.pack(d["blob"], d["offsets"], d["lengths"])), exp)
-    monkeypatch.delenv("DMX_SCREEN")
+    monkeypatch.delenv("DMX_NO_SCREEN")
     monkeypatch.setenv("DMX_NO_VERIFY", "1")
     with lib.Context(0) as c3:
         c3.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC, e)
