@@ -160,6 +160,20 @@ int dmx_counts(dmx_ctx* ctx, uint64_t* out_counts, size_t n_out);
 int dmx_stats(dmx_ctx* ctx, float* stage_ms, int n_stage, uint64_t* counts, int n_counts,
               int* flags);
 
+/* Diagnostics (tests and tools only): copy an intermediate list of the last dmx_exec to the host
+ * (up to cap_bytes; returns the list's size in bytes, negative on error).  The window and task
+ * lists are shared by both rounds, so after a two-round exec only round 1's are resident; the
+ * candidate lists are per round.  Records are the library's internal layouts (40-byte windows /
+ * tasks / candidates; DMX_DBG_FLAGS: the 4-byte pipeline flags word). */
+#define DMX_DBG_WINDOWS 0
+#define DMX_DBG_VERIFIED 1
+#define DMX_DBG_TASKS_NARROW 2
+#define DMX_DBG_TASKS_WIDE 3
+#define DMX_DBG_CANDS0 4
+#define DMX_DBG_CANDS1 5
+#define DMX_DBG_FLAGS 6
+int dmx_debug_fetch(dmx_ctx* ctx, int what, int round, void* out, size_t cap_bytes);
+
 /* ---- Residual-primer failsafe: exact degenerate-motif location (`seqkit locate -d`) ---------
  * Replaces: `seqkit locate -d --pattern-file PRIMERS ENDS` in the failsafe of
  * scripts/04_cleaning_primers.sh:397-460 (`:422`; seqkit v2, not vendored).  Every occurrence

@@ -140,6 +140,19 @@ struct Stage {
     }
 };
 
+// Block-uniform snapshot of LDS staging counters for a flush decision.  Every thread reads them
+// between two barriers: without the second one a fast wave could skip the flush, start the next
+// round and push (raising a counter) before a slow wave has read it; the slow wave would then
+// flush alone and its barriers would pair with the other waves' loop barriers, so the flush would
+// copy slots whose pushes had not landed (lost and duplicated records, found at scale by
+// tools/determinism.py).
+__device__ __forceinline__ uint32_t stage_count(const uint32_t* c) {
+    __syncthreads();
+    const uint32_t v = *c;
+    __syncthreads();
+    return v;
+}
+
 // A view of a read: strand 0 = the read as given, strand 1 = its reverse complement; the view
 // is positions [start, start+len) of that strand.
 struct ItemView {

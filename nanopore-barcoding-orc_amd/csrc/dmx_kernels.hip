@@ -46,9 +46,9 @@ struct RoundArgs {
     uint32_t* cand_count;        // [2]
     uint32_t cand_cap;
     int32_t screen;              // 1: the window scan runs the index screen's surviving pairs
-    Window* tasks;               // index screen survivors: window pieces of one adapter each
-    uint32_t* task_count;
-    uint32_t task_cap;
+    Window* tasks;               // index screen survivors: window pieces of one adapter each, two
+    uint32_t* task_count[2];     // lists by piece width ([0] <= kShortTask columns at [0, cap),
+    uint32_t task_cap;           // [1] wider at [cap, 2 cap)) so a wave's lanes scan alike spans
 };
 
 struct TaskView {
@@ -921,8 +921,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             }
             if (S.have) st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb));
         }
-        __syncthreads();                               // staged count is block-uniform here
-        if (s_wcnt > kStageCap / 2) st.flush();
+        if (stage_count(&s_wcnt) > kStageCap / 2) st.flush();
     }
     st.flush();
 }
@@ -1035,8 +1034,7 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
             w.info = info;
             if (keep) st.push(w);
         }
-        __syncthreads();
-        if (s_wc > kStageCap / 2) st.flush();
+        if (stage_count(&s_wc) > kStageCap / 2) st.flush();
     }
     st.flush();
 }
@@ -1062,6 +1060,8 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
 // lower.  One lane per (window, adapter); each survivor becomes one task record (the window
 // piece with the adapter in `info`), so the window scan runs full waves of surviving tasks.
 // ---------------------------------------------------------------------------------------------
+constexpr int kShortTask = 16;   // task lists: candidate columns j2 - j1 <= 16, or wider
+
 __device__ __forceinline__ Window make_task(Window w, uint32_t jlo, uint32_t jhi, bool lastcol,
                                             int a) {
     w.lastcol = lastcol ? 1 : 0;
@@ -1074,8 +1074,8 @@ __device__ __forceinline__ Window make_task(Window w, uint32_t jlo, uint32_t jhi
 __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
     __shared__ uint32_t s_ipeq[8 * kPeqStride];     // code-major: [c][a], bit r = row pre_len + r
     __shared__ int8_t s_acc[72 * kMaxAdapters];
-    __shared__ Window s_task[kStageCap];
-    __shared__ uint32_t s_tc, s_tb, s_nend;
+    __shared__ Window s_task[2][kStageCap / 2];
+    __shared__ uint32_t s_tc[2], s_tb[2], s_nend;
     const DevPanel* P = R.panel;
     const int A = P->n_adapters;
     const int pl = P->pre_len, sl = P->filter_len, kf = P->kf;
@@ -1087,11 +1087,14 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
     }
     for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
     if (threadIdx.x == 0) {
-        s_tc = 0;
+        s_tc[0] = s_tc[1] = 0;
         s_nend = 0;
     }
     __syncthreads();
-    const Stage<Window> st{s_task, &s_tc, &s_tb, R.tasks, R.task_count, R.task_cap, R.flags, 4u};
+    const Stage<Window, kStageCap / 2> stl[2] = {
+        {s_task[0], &s_tc[0], &s_tb[0], R.tasks, R.task_count[0], R.task_cap, R.flags, 4u},
+        {s_task[1], &s_tc[1], &s_tb[1], R.tasks + R.task_cap, R.task_count[1], R.task_cap,
+         R.flags, 4u}};
     const Window* wl = R.win2;
     const uint32_t nwin = min(*R.win2_count, R.win_cap);
     const uint32_t total = nwin * (uint32_t)A;    // host: win_cap * A < 2^32
@@ -1099,12 +1102,20 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
     const int jsplit = front ? P->jsplit : 0;
     const bool pshared = P->pshared != 0;
 
-    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    Window wn;                                         // this lane's next window, loaded ahead
+    {
+        const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+        if (t0 < total) wn = wl[t0 / (uint32_t)A];
+    }
+    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride) {
         const uint32_t t = base + threadIdx.x;
+        const Window w0n = wn;
+        if (t + stride < total) wn = wl[(t + stride) / (uint32_t)A];
         if (t < total) {
             const uint32_t wi = t / (uint32_t)A;
             const int a = (int)(t - wi * (uint32_t)A);
-            const Window w = wl[wi];
+            const Window& w = w0n;
             const DevAdapter& ad = P->ad[a];
             const int len = (int)w.len, j1 = (int)w.j1, j2 = (int)w.j2;
             const int l = (int)ad.m - pl - sl, kk = ad.kk;
@@ -1113,8 +1124,10 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
             const int dPn = (int)(w.info >> 24);
             const bool lastc = !front && w.lastcol;
             // the near piece [j1, min(j2, jsplit - 1)] keeps every adapter
-            if (j1 < jsplit) st.push(make_task(w, (uint32_t)j1, (uint32_t)min(j2, jsplit - 1),
-                                               false, a));
+            if (j1 < jsplit) {
+                const int jh = min(j2, jsplit - 1);
+                stl[jh - j1 > kShortTask].push(make_task(w, (uint32_t)j1, (uint32_t)jh, false, a));
+            }
             const int jr = max(j1, jsplit);               // far piece: last-row cells [jr, j2]
             const int thr = kk - bm - dP;                 // (bm = 255: no hit column, no rows)
             const bool rows = bm != 255 && jr <= j2 && thr >= 0;
@@ -1201,14 +1214,18 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
                 }
             }
             if (pass) {
-                st.push(make_task(w, (uint32_t)jr, (uint32_t)j2, lastc, a));
+                stl[j2 - jr > kShortTask].push(make_task(w, (uint32_t)jr, (uint32_t)j2, lastc, a));
                 if (by_end) atomicAdd(&s_nend, 1u);
             }
         }
-        __syncthreads();                               // staged count is block-uniform here
-        if (s_tc > kStageCap / 2) st.flush();
+        __syncthreads();                               // pushes done; then every wave reads
+        const uint32_t c0 = s_tc[0], c1 = s_tc[1];     // the counts before any wave goes on
+        __syncthreads();                               // (see stage_count)
+        if (c0 > (uint32_t)kStageCap / 4) stl[0].flush();
+        if (c1 > (uint32_t)kStageCap / 4) stl[1].flush();
     }
-    st.flush();
+    stl[0].flush();
+    stl[1].flush();
     if (threadIdx.x == 0 && s_nend) atomicAdd(&R.diag[3], s_nend);     // by 3' cells only
 }
 
@@ -1277,24 +1294,26 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     const Window* wl = R.panel->pre_len ? R.win2 : R.win;
     const uint32_t* wc = R.panel->pre_len ? R.win2_count : R.win_count;
     if (R.screen) {   // the index screen's surviving (window piece, adapter) tasks
-        const uint32_t nt = min(*R.task_count, R.task_cap);
-        const uint32_t stride = gridDim.x * blockDim.x;
+      const uint32_t stride = gridDim.x * blockDim.x;
+      for (int list = 0; list < 2; ++list) {          // narrow pieces, then wide ones
+        const Window* tl = R.tasks + (size_t)list * R.task_cap;
+        const uint32_t nt = min(*R.task_count[list], R.task_cap);
         uint32_t ti = blockIdx.x * blockDim.x + threadIdx.x;
         Window wn;                                     // the next task, loaded one ahead
-        if (ti < nt) wn = R.tasks[ti];
+        if (ti < nt) wn = tl[ti];
         for (uint32_t base = blockIdx.x * blockDim.x; base < nt; base += stride, ti += stride) {
             const Window w = wn;
-            if (ti + stride < nt) wn = R.tasks[ti + stride];
+            if (ti + stride < nt) wn = tl[ti + stride];
             if (ti < nt) wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, st, sink);
             if constexpr (BAND) {
                 __builtin_amdgcn_wave_barrier();
                 if (sink.st[0].count() > kWaveCandCap / 2) sink.st[0].flush();
                 if (sink.st[1].count() > kWaveCandCap / 2) sink.st[1].flush();
             } else {
-                __syncthreads();
-                if (s_clcnt > kStageCap / 2) st.flush();
+                if (stage_count(&s_clcnt) > kStageCap / 2) st.flush();
             }
         }
+      }
         if constexpr (BAND) {
             __builtin_amdgcn_wave_barrier();
             sink.st[0].flush();
@@ -1318,8 +1337,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             if (sink.st[0].count() > kWaveCandCap / 2) sink.st[0].flush();
             if (sink.st[1].count() > kWaveCandCap / 2) sink.st[1].flush();
         } else {
-            __syncthreads();                         // make the staged counts block-uniform
-            if (s_clcnt > kStageCap / 2) st.flush();
+            if (stage_count(&s_clcnt) > kStageCap / 2) st.flush();
         }
     }
     if constexpr (BAND) {
@@ -2122,8 +2140,9 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     R.screen = (hp.filter && hp.verify && hp.screen && !linked && !c->no_screen &&
                 (uint64_t)c->win_cap * (uint64_t)hp.n < (1ull << 32)) ? 1 : 0;
     R.tasks = c->d_tasks;
-    R.task_count = c->d_counters + 12 + round;
-    R.task_cap = (uint32_t)c->task_cap;
+    R.task_count[0] = c->d_counters + 12 + round;
+    R.task_count[1] = c->d_counters + 24 + round;
+    R.task_cap = (uint32_t)(c->task_cap / 2);
     hipEventRecord(c->ev[round * 3 + 0], st);
     if (hp.filter && !linked) {   // linked primers: short, no shared suffix block; plain scan
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;

@@ -23,6 +23,7 @@ import numpy as np
 
 from . import __version__
 from . import fastx, lib, nio, panel
+from . import report
 from .report import Stats
 
 
@@ -115,6 +116,7 @@ def run(argv=None) -> int:
 
     stats = Stats(ads)
     stats.rc_mode = bool(args.rc)
+    stats.min_overlap = args.overlap
     t0 = time.perf_counter()
     a1 = len(ads) if linked else 0
     totals = np.zeros((len(ads) + 1, a1 + 1), dtype=np.int64)
@@ -126,7 +128,8 @@ def run(argv=None) -> int:
                     if len(batch):
                         res, cnt = lib.run_batch(ctxs, batch.packed)
                         totals += lib.bin_totals(cnt, len(ads), len(ads) if linked else 0)
-                        plan = _plan(res, ads, linked, demux, unmatched_to, batch.lens, stats)
+                        plan = _plan(res, ads, linked, demux, unmatched_to, batch.lens, stats,
+                                     batch.packed)
                         sink.write(batch, *plan)
                 finally:
                     batch.free()
@@ -145,7 +148,7 @@ def run(argv=None) -> int:
         print(f"This is dmx {__version__} (cutadapt 4.9-compatible demultiplexer on MI355X)")
         print(f"Command line parameters: {' '.join(argv)}")
         print(f"Finished in {time.perf_counter() - t0:.3f} s on {len(ctxs)} GPU(s)\n")
-        stats.summary()
+        stats.summary(error_rate=args.error_rate)
     for ctx in ctxs:
         ctx.close()
     return 0
@@ -192,7 +195,7 @@ def _configure(ctx, ads, linked, args):
     ctx.set_mode(lib.MODE_SINGLE)
 
 
-def _plan(res, ads, linked, demux, unmatched_to, lens, stats):
+def _plan(res, ads, linked, demux, unmatched_to, lens, stats, packed=None):
     """Per-read output index, trim coordinates and orientation (vectorised), and statistics.
 
     -g (FRONT): RemoveBeforeMatch keeps seq[rstop:]; -a (BACK): RemoveAfterMatch keeps
@@ -238,6 +241,10 @@ def _plan(res, ads, linked, demux, unmatched_to, lens, stats):
         fr = is_front[matched]
         stats.add_matches(bm[fr], "front", m1_rstop[matched][fr], e1[fr])
         stats.add_matches(bm[~fr], "back", (lens - m1_rstart)[matched][~fr], e1[~fr])
+        if packed is not None:   # 3' adapters: the base before the match, on the matched view
+            ib = np.nonzero(matched & ~is_front)[0]
+            stats.add_adjacent(bin1[ib], report.view_codes(packed, ib, rc[ib].astype(np.int64),
+                                                           m1_rstart[ib] - 1))
     rc8 = rc.astype(np.uint8)
     return out_idx.astype(np.int32), start.astype(np.int32), stop.astype(np.int32), rc8, rc8
 

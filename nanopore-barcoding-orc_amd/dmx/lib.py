@@ -33,7 +33,7 @@ EXPORTS = ["dmx_abi_version", "dmx_open", "dmx_close", "dmx_last_error", "dmx_se
            "dmx_sync", "dmx_fetch", "dmx_counts", "dmx_stats", "dmx_device_count",
            "dmx_run_multi", "dmx_locate", "dmx_chop_set", "dmx_chop_exec", "dmx_chop_fetch",
            "dmx_chop_stats", "dmx_comm_unique_id", "dmx_comm_init_rank", "dmx_comm_init_all",
-           "dmx_comm_size", "dmx_allreduce_counts"]
+           "dmx_comm_size", "dmx_allreduce_counts", "dmx_debug_fetch"]
 COMM_ID_BYTES = 128
 
 LOC_IGNORE_CASE, LOC_ONLY_POSITIVE = 0x1, 0x2
@@ -47,6 +47,19 @@ CHOP_HIT_DTYPE = np.dtype([("read", "<u4"), ("label", "<i2"), ("dist", "<i2"), (
 CHOP_SEG_DTYPE = np.dtype([("read", "<u4"), ("start", "<i4"), ("stop", "<i4"),
                            ("strand", "<i2"), ("rule", "<i2")])
 assert CHOP_HIT_DTYPE.itemsize == 16 and CHOP_SEG_DTYPE.itemsize == 16
+
+
+# internal record layouts exposed by dmx_debug_fetch (csrc/dmx_device.h Window / Cand)
+WINDOW_DTYPE = np.dtype([("item", "<u4"), ("o", "u1"), ("lastcol", "u1"), ("strand", "u1"),
+                         ("bmin", "u1"), ("j1", "<u4"), ("j2", "<u4"), ("n", "<u4"),
+                         ("start", "<u4"), ("len", "<u4"), ("info", "<u4"), ("off", "<u8")])
+CAND_DTYPE = np.dtype([("item", "<u4"), ("sub", "<u2"), ("iend", "u1"), ("cost", "u1"),
+                       ("j", "<u4"), ("n", "<u4"), ("start", "<u4"), ("len", "<u4"),
+                       ("strand", "u1"), ("o", "u1"), ("a", "u1"), ("pad", "u1"), ("pad2", "<u4"),
+                       ("off", "<u8")])
+assert WINDOW_DTYPE.itemsize == 40 and CAND_DTYPE.itemsize == 40
+DBG_WINDOWS, DBG_VERIFIED, DBG_TASKS_NARROW, DBG_TASKS_WIDE, DBG_CANDS0, DBG_CANDS1, DBG_FLAGS = \
+    range(7)
 
 
 class DmxError(RuntimeError):
@@ -105,6 +118,7 @@ def load() -> ctypes.CDLL:
     L.dmx_comm_init_all.argtypes = [ctypes.POINTER(P), c_int]
     L.dmx_comm_size.argtypes = [P]
     L.dmx_allreduce_counts.argtypes = [P, c_u64p, c_size]
+    L.dmx_debug_fetch.argtypes = [P, c_int, c_int, P, c_size]
     if L.dmx_abi_version() != 3:
         raise DmxError("libdmx ABI mismatch")
     _lib = L
@@ -331,6 +345,16 @@ class Context:
         self._check(self._L.dmx_allreduce_counts(self._h, out.ctypes.data, len(out)),
                     "dmx_allreduce_counts")
         return out
+
+    def debug_fetch(self, what: int, rnd: int = 0) -> np.ndarray:
+        """An intermediate list of the last exec (diagnostics: include/dmx.h dmx_debug_fetch)."""
+        nb = self._check(self._L.dmx_debug_fetch(self._h, what, rnd, None, 0), "dmx_debug_fetch")
+        buf = np.zeros(nb, dtype=np.uint8)
+        self._check(self._L.dmx_debug_fetch(self._h, what, rnd, buf.ctypes.data if nb else None,
+                                            nb), "dmx_debug_fetch")
+        if what == DBG_FLAGS:
+            return buf.view(np.uint32)
+        return buf.view(CAND_DTYPE if what in (DBG_CANDS0, DBG_CANDS1) else WINDOW_DTYPE)
 
     def stats(self):
         ms = (ctypes.c_float * 11)()

@@ -27,6 +27,7 @@ import numpy as np
 
 from . import __version__, lib, nio, panel
 from .cli import _devices
+from . import report
 from .report import Stats
 
 INVALID_SP27 = ("SP27_009", "SP27_010", "SP27_011", "SP27_012")   # 02_cutadapt_loop.sh:114-118
@@ -176,7 +177,7 @@ def run(argv=None) -> int:
                     n2w = np.where(m2, nrc2, o1 + u2rc).astype(np.uint8)
                     sink2.write(batch, idx2, s2w, e2w, o2w, n2w)
                     _round_stats(st1, st2, res, batch.lens, m1, m2, b1, b2, s1, s2w, e2w,
-                                 bp2_out, n2_out)
+                                 bp2_out, n2_out, batch.packed)
                     prof["plan_write"] += time.perf_counter() - tw
                 finally:
                     batch.free()
@@ -213,7 +214,8 @@ def run(argv=None) -> int:
     return 0
 
 
-def _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w, bp2_out, n2_out):
+def _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w, bp2_out, n2_out,
+                 packed=None):
     lens = lens.astype(np.int64)
     n = len(res)
     rc1 = res["rc1"] == 1
@@ -226,6 +228,19 @@ def _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w, bp2_out, n2_
     # round 2, one report per SP5 bin: its input is that bin's round-1 output
     len1 = lens - s1
     rc2 = (res["rc2"] == 1) & m1
+    adj = None
+    if packed is not None:
+        # base before each round-2 (3') match, on the round-2 view: the round-1 output
+        # T1 = orient(read, rc1)[s1:], reverse-complemented when rc2 — position p of it is
+        # orient(read, rc1)[s1 + p], or orient(read, 1 - rc1)[p] on the reverse complement
+        hit_all = np.nonzero(m1 & m2)[0]
+        p = res["m2_rstart"].astype(np.int64)[hit_all] - 1
+        r1 = res["rc1"].astype(np.int64)[hit_all]
+        two = res["rc2"].astype(np.int64)[hit_all] == 1
+        codes = report.view_codes(packed, hit_all, np.where(two, 1 - r1, r1),
+                                  np.where(two, p, np.where(p >= 0, s1[hit_all] + p, -1)))
+        adj = np.full(n, 4, np.int64)
+        adj[hit_all] = codes
     for i, s in enumerate(st2):
         sel = m1 & (b1 == i)
         if not sel.any():
@@ -238,6 +253,8 @@ def _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w, bp2_out, n2_
         s.add_counts(b2[hit], rc2[hit], len(s.adapters))
         s.add_matches(b2[hit], "back", len1[hit] - res["m2_rstart"].astype(np.int64)[hit],
                       res["m2_errors"].astype(np.int64)[hit])
+        if adj is not None:
+            s.add_adjacent(b2[hit], adj[hit])
         # reads the per-call cutadapt would write (all of them: unknown included), before the
         # script's cleanup deletes files
         n2_out[i] += int(sel.sum())
