@@ -167,11 +167,10 @@ int dmx_stats(dmx_ctx* ctx, float* stage_ms, int n_stage, uint64_t* counts, int 
  * tasks / candidates; DMX_DBG_FLAGS: the 4-byte pipeline flags word). */
 #define DMX_DBG_WINDOWS 0
 #define DMX_DBG_VERIFIED 1
-#define DMX_DBG_TASKS_NARROW 2
-#define DMX_DBG_TASKS_WIDE 3
-#define DMX_DBG_CANDS0 4
-#define DMX_DBG_CANDS1 5
-#define DMX_DBG_FLAGS 6
+#define DMX_DBG_TASKS 2
+#define DMX_DBG_CANDS0 3
+#define DMX_DBG_CANDS1 4
+#define DMX_DBG_FLAGS 5
 int dmx_debug_fetch(dmx_ctx* ctx, int what, int round, void* out, size_t cap_bytes);
 
 /* ---- Residual-primer failsafe: exact degenerate-motif location (`seqkit locate -d`) ---------

@@ -638,9 +638,9 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
     if (getenv("DMX_DEBUG_STATS"))
         fprintf(stderr,
                 "dmx stats: windows raw %u %u verified %u %u screened tasks %u %u "
-                "+ wide %u %u (by 3' cells only %u %u) cand %u %u %u %u\n",
-                cnt[4], cnt[5], cnt[10], cnt[11], cnt[12], cnt[13], cnt[24], cnt[25], cnt[19],
-                cnt[23], cnt[6], cnt[7], cnt[8], cnt[9]);
+                "(by 3' cells only %u %u) cand %u %u %u %u\n",
+                cnt[4], cnt[5], cnt[10], cnt[11], cnt[12], cnt[13], cnt[19], cnt[23], cnt[6],
+                cnt[7], cnt[8], cnt[9]);
     if (counts) {
         const bool b0 = c->band_ok[0] && !c->force_ring, b1 = c->band_ok[1] && !c->force_ring;
         const uint64_t v[10] = {cnt[0],
@@ -660,8 +660,7 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
         if (cnt[0] > c->cl_cap || cnt[1] > c->cl_cap) f |= 1;
         if (cnt[4] > c->win_cap || cnt[5] > c->win_cap) f |= 4;
         if (cnt[10] > c->win_cap || cnt[11] > c->win_cap) f |= 4;
-        for (int x : {12, 13, 24, 25})   // task lists (two halves of d_tasks)
-            if (cnt[x] > c->task_cap / 2) f |= 4;
+        if (cnt[12] > c->task_cap || cnt[13] > c->task_cap) f |= 4;
         for (int x = 6; x < 10; ++x)
             if (cnt[x] > c->cand_cap) f |= 8;
         *flags = f;
@@ -684,8 +683,7 @@ int dmx_debug_fetch(dmx_ctx* c, int what, int round, void* out, size_t cap_bytes
     switch (what) {
         case DMX_DBG_WINDOWS: src = c->d_win; bytes = std::min<size_t>(cnt[4 + round], c->win_cap) * sizeof(Window); break;
         case DMX_DBG_VERIFIED: src = c->d_win2; bytes = std::min<size_t>(cnt[10 + round], c->win_cap) * sizeof(Window); break;
-        case DMX_DBG_TASKS_NARROW: src = c->d_tasks; bytes = std::min<size_t>(cnt[12 + round], c->task_cap / 2) * sizeof(Window); break;
-        case DMX_DBG_TASKS_WIDE: src = c->d_tasks + c->task_cap / 2; bytes = std::min<size_t>(cnt[24 + round], c->task_cap / 2) * sizeof(Window); break;
+        case DMX_DBG_TASKS: src = c->d_tasks; bytes = std::min<size_t>(cnt[12 + round], c->task_cap) * sizeof(Window); break;
         case DMX_DBG_CANDS0: src = c->d_cand[round][0]; bytes = std::min<size_t>(cnt[6 + 2 * round], c->cand_cap) * sizeof(Cand); break;
         case DMX_DBG_CANDS1: src = c->d_cand[round][1]; bytes = std::min<size_t>(cnt[7 + 2 * round], c->cand_cap) * sizeof(Cand); break;
         case DMX_DBG_FLAGS: src = nullptr; bytes = 4; break;

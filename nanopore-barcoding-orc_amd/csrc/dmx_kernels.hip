@@ -46,9 +46,9 @@ struct RoundArgs {
     uint32_t* cand_count;        // [2]
     uint32_t cand_cap;
     int32_t screen;              // 1: the window scan runs the index screen's surviving pairs
-    Window* tasks;               // index screen survivors: window pieces of one adapter each, two
-    uint32_t* task_count[2];     // lists by piece width ([0] <= kShortTask columns at [0, cap),
-    uint32_t task_cap;           // [1] wider at [cap, 2 cap)) so a wave's lanes scan alike spans
+    Window* tasks;               // index screen survivors: window pieces of one adapter each
+    uint32_t* task_count;
+    uint32_t task_cap;
 };
 
 struct TaskView {
@@ -297,6 +297,7 @@ struct WaveStage {
 };
 
 constexpr int kWaveCandCap = 64;
+constexpr int kWaveWinCap = 64;   // per-wave window / task staging (filter, verify, screen)
 
 struct WaveCandSink {
     WaveStage<Cand, kWaveCandCap> st[2];
@@ -614,7 +615,8 @@ __device__ __forceinline__ void filter_chunk(uint32_t codes, uint32_t nb, uint32
                                              SegState& S, const uint32_t* s_fpeq,
                                              const int8_t* s_thr, uint32_t hbit, int kf,
                                              int kf_far, uint32_t gap, uint32_t hit_from,
-                                             const Stage<Window>& st, uint32_t item, int o,
+                                             const WaveStage<Window, kWaveWinCap>& st,
+                                             uint32_t item, int o,
                                              const TaskView& tv) {
     uint32_t eq[16];
 #pragma unroll
@@ -713,7 +715,8 @@ __device__ __forceinline__ void filter_segment(const RoundArgs& R, const TaskVie
                                                uint32_t P0, uint32_t P1, SegState& S,
                                                const uint32_t* s_fpeq, const int8_t* s_thr,
                                                uint32_t hbit, int kf, int kf_far, uint32_t gap,
-                                               uint32_t hit_from, const Stage<Window>& st,
+                                               uint32_t hit_from,
+                                               const WaveStage<Window, kWaveWinCap>& st,
                                                uint32_t item, int o) {
     const bool rev = tv.strand != 0;
     const int64_t g = rev ? (int64_t)tv.off + (int64_t)tv.n - 1 - tv.start - P0 - (kSegSpan - 1)
@@ -771,8 +774,8 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     __shared__ uint32_t s_fpeq[8];
     __shared__ int8_t s_pf[72];
     __shared__ __attribute__((aligned(16))) int8_t s_thr[kScanBlock];
-    __shared__ Window s_win[kStageCap];
-    __shared__ uint32_t s_wcnt, s_wbase;
+    __shared__ Window s_win[kScanBlock / 64][kWaveWinCap];   // per-wave window staging
+    __shared__ uint32_t s_wcnt[kScanBlock / 64];
     __shared__ uint32_t s_pre[2][kSegViewsPerBlock];   // per strand: segments before view v
     __shared__ uint32_t s_tot[2][kScanBlock];
     const DevPanel* P = R.panel;
@@ -789,7 +792,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     const uint32_t SEG = (uint32_t)kSegSpan - W;       // host guarantees W <= 96
     if (threadIdx.x < 8) s_fpeq[threadIdx.x] = P->filter_peq[threadIdx.x];
     if (threadIdx.x < 72) s_pf[threadIdx.x] = P->pf[threadIdx.x];
-    if (threadIdx.x == 0) s_wcnt = 0;
+    if (threadIdx.x < kScanBlock / 64) s_wcnt[threadIdx.x] = 0;
     {   // hit threshold of column j = p + 1 (view position p): the largest cost d <= kf_far that
         // an acceptable last-row cell (m, j) of some adapter can have.  Its aligned adapter length
         // is at most j + d, so d <= pf[min(71, j + d)]; b(j) <= d.  (Near the view start this is
@@ -852,7 +855,9 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     }
     __syncthreads();
     const uint32_t T0 = s_tot[0][kScanBlock - 1], T1 = s_tot[1][kScanBlock - 1];
-    const Stage<Window> st{s_win, &s_wcnt, &s_wbase, R.win, R.win_count, R.win_cap, R.flags, 4u};
+    const uint32_t wv = threadIdx.x >> 6;   // windows staged per wave: no block barriers below
+    const WaveStage<Window, kWaveWinCap> st{s_win[wv], &s_wcnt[wv], R.win, R.win_count,
+                                            R.win_cap, R.flags, 4u};
 
     const bool front = P->where == kFront;
     const uint32_t hbit = (uint32_t)(L - 1);
@@ -921,8 +926,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             }
             if (S.have) st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb));
         }
-        if (stage_count(&s_wcnt) > kStageCap / 2) st.flush();
+        __builtin_amdgcn_wave_barrier();
+        if (st.count() > kWaveWinCap / 2) st.flush();
     }
+    __builtin_amdgcn_wave_barrier();
     st.flush();
 }
 
@@ -1060,7 +1067,6 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
 // lower.  One lane per (window, adapter); each survivor becomes one task record (the window
 // piece with the adapter in `info`), so the window scan runs full waves of surviving tasks.
 // ---------------------------------------------------------------------------------------------
-constexpr int kShortTask = 16;   // task lists: candidate columns j2 - j1 <= 16, or wider
 
 __device__ __forceinline__ Window make_task(Window w, uint32_t jlo, uint32_t jhi, bool lastcol,
                                             int a) {
@@ -1074,8 +1080,8 @@ __device__ __forceinline__ Window make_task(Window w, uint32_t jlo, uint32_t jhi
 __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
     __shared__ uint32_t s_ipeq[8 * kPeqStride];     // code-major: [c][a], bit r = row pre_len + r
     __shared__ int8_t s_acc[72 * kMaxAdapters];
-    __shared__ Window s_task[2][kStageCap / 2];
-    __shared__ uint32_t s_tc[2], s_tb[2], s_nend;
+    __shared__ Window s_task[kScanBlock / 64][kWaveWinCap];   // per-wave task staging
+    __shared__ uint32_t s_tc[kScanBlock / 64], s_nend;
     const DevPanel* P = R.panel;
     const int A = P->n_adapters;
     const int pl = P->pre_len, sl = P->filter_len, kf = P->kf;
@@ -1086,15 +1092,12 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
         s_ipeq[c * kPeqStride + a] = (uint32_t)(l >= 32 ? v : (v & ((1ull << l) - 1ull)));
     }
     for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
-    if (threadIdx.x == 0) {
-        s_tc[0] = s_tc[1] = 0;
-        s_nend = 0;
-    }
+    if (threadIdx.x < kScanBlock / 64) s_tc[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_nend = 0;
     __syncthreads();
-    const Stage<Window, kStageCap / 2> stl[2] = {
-        {s_task[0], &s_tc[0], &s_tb[0], R.tasks, R.task_count[0], R.task_cap, R.flags, 4u},
-        {s_task[1], &s_tc[1], &s_tb[1], R.tasks + R.task_cap, R.task_count[1], R.task_cap,
-         R.flags, 4u}};
+    const uint32_t wv = threadIdx.x >> 6;
+    const WaveStage<Window, kWaveWinCap> st{s_task[wv], &s_tc[wv], R.tasks, R.task_count,
+                                            R.task_cap, R.flags, 4u};
     const Window* wl = R.win2;
     const uint32_t nwin = min(*R.win2_count, R.win_cap);
     const uint32_t total = nwin * (uint32_t)A;    // host: win_cap * A < 2^32
@@ -1103,19 +1106,12 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
     const bool pshared = P->pshared != 0;
 
     const uint32_t stride = gridDim.x * blockDim.x;
-    Window wn;                                         // this lane's next window, loaded ahead
-    {
-        const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
-        if (t0 < total) wn = wl[t0 / (uint32_t)A];
-    }
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride) {
         const uint32_t t = base + threadIdx.x;
-        const Window w0n = wn;
-        if (t + stride < total) wn = wl[(t + stride) / (uint32_t)A];
         if (t < total) {
             const uint32_t wi = t / (uint32_t)A;
             const int a = (int)(t - wi * (uint32_t)A);
-            const Window& w = w0n;
+            const Window w = wl[wi];
             const DevAdapter& ad = P->ad[a];
             const int len = (int)w.len, j1 = (int)w.j1, j2 = (int)w.j2;
             const int l = (int)ad.m - pl - sl, kk = ad.kk;
@@ -1126,7 +1122,7 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
             // the near piece [j1, min(j2, jsplit - 1)] keeps every adapter
             if (j1 < jsplit) {
                 const int jh = min(j2, jsplit - 1);
-                stl[jh - j1 > kShortTask].push(make_task(w, (uint32_t)j1, (uint32_t)jh, false, a));
+                st.push(make_task(w, (uint32_t)j1, (uint32_t)jh, false, a));
             }
             const int jr = max(j1, jsplit);               // far piece: last-row cells [jr, j2]
             const int thr = kk - bm - dP;                 // (bm = 255: no hit column, no rows)
@@ -1214,18 +1210,16 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
                 }
             }
             if (pass) {
-                stl[j2 - jr > kShortTask].push(make_task(w, (uint32_t)jr, (uint32_t)j2, lastc, a));
+                st.push(make_task(w, (uint32_t)jr, (uint32_t)j2, lastc, a));
                 if (by_end) atomicAdd(&s_nend, 1u);
             }
         }
-        __syncthreads();                               // pushes done; then every wave reads
-        const uint32_t c0 = s_tc[0], c1 = s_tc[1];     // the counts before any wave goes on
-        __syncthreads();                               // (see stage_count)
-        if (c0 > (uint32_t)kStageCap / 4) stl[0].flush();
-        if (c1 > (uint32_t)kStageCap / 4) stl[1].flush();
+        __builtin_amdgcn_wave_barrier();
+        if (st.count() > kWaveWinCap / 2) st.flush();
     }
-    stl[0].flush();
-    stl[1].flush();
+    __builtin_amdgcn_wave_barrier();
+    st.flush();
+    __syncthreads();
     if (threadIdx.x == 0 && s_nend) atomicAdd(&R.diag[3], s_nend);     // by 3' cells only
 }
 
@@ -1295,16 +1289,15 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     const uint32_t* wc = R.panel->pre_len ? R.win2_count : R.win_count;
     if (R.screen) {   // the index screen's surviving (window piece, adapter) tasks
       const uint32_t stride = gridDim.x * blockDim.x;
-      for (int list = 0; list < 2; ++list) {          // narrow pieces, then wide ones
-        const Window* tl = R.tasks + (size_t)list * R.task_cap;
-        const uint32_t nt = min(*R.task_count[list], R.task_cap);
-        uint32_t ti = blockIdx.x * blockDim.x + threadIdx.x;
-        Window wn;                                     // the next task, loaded one ahead
-        if (ti < nt) wn = tl[ti];
-        for (uint32_t base = blockIdx.x * blockDim.x; base < nt; base += stride, ti += stride) {
-            const Window w = wn;
-            if (ti + stride < nt) wn = tl[ti + stride];
-            if (ti < nt) wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, st, sink);
+      {
+        const Window* tl = R.tasks;
+        const uint32_t nt = min(*R.task_count, R.task_cap);
+        for (uint32_t base = blockIdx.x * blockDim.x; base < nt; base += stride) {
+            const uint32_t ti = base + threadIdx.x;
+            if (ti < nt) {
+                const Window w = tl[ti];
+                wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, st, sink);
+            }
             if constexpr (BAND) {
                 __builtin_amdgcn_wave_barrier();
                 if (sink.st[0].count() > kWaveCandCap / 2) sink.st[0].flush();
@@ -2140,9 +2133,8 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     R.screen = (hp.filter && hp.verify && hp.screen && !linked && !c->no_screen &&
                 (uint64_t)c->win_cap * (uint64_t)hp.n < (1ull << 32)) ? 1 : 0;
     R.tasks = c->d_tasks;
-    R.task_count[0] = c->d_counters + 12 + round;
-    R.task_count[1] = c->d_counters + 24 + round;
-    R.task_cap = (uint32_t)(c->task_cap / 2);
+    R.task_count = c->d_counters + 12 + round;
+    R.task_cap = (uint32_t)c->task_cap;
     hipEventRecord(c->ev[round * 3 + 0], st);
     if (hp.filter && !linked) {   // linked primers: short, no shared suffix block; plain scan
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;

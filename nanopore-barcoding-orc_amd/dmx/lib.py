@@ -58,8 +58,7 @@ CAND_DTYPE = np.dtype([("item", "<u4"), ("sub", "<u2"), ("iend", "u1"), ("cost",
                        ("strand", "u1"), ("o", "u1"), ("a", "u1"), ("pad", "u1"), ("pad2", "<u4"),
                        ("off", "<u8")])
 assert WINDOW_DTYPE.itemsize == 40 and CAND_DTYPE.itemsize == 40
-DBG_WINDOWS, DBG_VERIFIED, DBG_TASKS_NARROW, DBG_TASKS_WIDE, DBG_CANDS0, DBG_CANDS1, DBG_FLAGS = \
-    range(7)
+DBG_WINDOWS, DBG_VERIFIED, DBG_TASKS, DBG_CANDS0, DBG_CANDS1, DBG_FLAGS = range(6)
 
 
 class DmxError(RuntimeError):

@@ -35,8 +35,7 @@ def run(d, env):
             lists = {nm: np.sort(ctx.debug_fetch(w, 0).view(np.uint8).reshape(-1, 40).view("V40")
                                  .ravel())
                      for nm, w in (("verified", lib.DBG_VERIFIED),
-                                   ("tasks_narrow", lib.DBG_TASKS_NARROW),
-                                   ("tasks_wide", lib.DBG_TASKS_WIDE),
+                                   ("tasks", lib.DBG_TASKS),
                                    ("cands0", lib.DBG_CANDS0), ("cands1", lib.DBG_CANDS1))}
             lists["flags"] = int(ctx.debug_fetch(lib.DBG_FLAGS)[0])
             ctx.set_mode(lib.MODE_TWO_ROUND)
@@ -80,7 +79,7 @@ def main():
                                         for k, v in s1["lists"].items() if k != "flags"},
            "round0_list_sizes": {k: [len(v), len(s2["lists"][k])]
                                  for k, v in s1["lists"].items() if k != "flags"}}
-    for k in ("tasks_wide", "tasks_narrow", "verified"):   # records in one run and not the other
+    for k in ("tasks", "verified"):   # records in one run and not the other
         x, y = s1["lists"][k], s2["lists"][k]
         if len(x) and not np.array_equal(x, y):
             only1 = np.setdiff1d(x, y)

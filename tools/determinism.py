@@ -20,9 +20,8 @@ sys.path.insert(0, os.path.join(ROOT, "nanopore-barcoding-orc_amd"))
 
 from dmx import lib, synth  # noqa: E402
 
-LISTS = (("verified", lib.DBG_VERIFIED), ("tasks_narrow", lib.DBG_TASKS_NARROW),
-         ("tasks_wide", lib.DBG_TASKS_WIDE), ("cands0", lib.DBG_CANDS0),
-         ("cands1", lib.DBG_CANDS1))
+LISTS = (("verified", lib.DBG_VERIFIED), ("tasks", lib.DBG_TASKS),
+         ("cands0", lib.DBG_CANDS0), ("cands1", lib.DBG_CANDS1))
 
 
 def canon(rec: np.ndarray) -> np.ndarray:
