@@ -330,7 +330,8 @@ def main():
         allreduce_counts()
 
     stage = {k: 0.0 for k in ("scan0", "resolve0", "finalize0", "scan1", "resolve1",
-                              "finalize1", "total", "filter0", "verify0", "filter1", "verify1")}
+                              "finalize1", "total", "filter0", "verify0", "filter1", "verify1",
+                              "screen0", "wscan0", "screen1", "wscan1")}
     clusters = np.zeros(2)
     windows = np.zeros(2)
     windows_raw = np.zeros(2)

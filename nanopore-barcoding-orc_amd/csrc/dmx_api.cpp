@@ -620,7 +620,7 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
     CK(hipSetDevice(c->device));
     CK(hipStreamSynchronize(c->stream));
     const int rounds = c->mode == DMX_MODE_SINGLE ? 1 : 2;
-    float t[11] = {};
+    float t[15] = {};
     for (int r = 0; r < rounds; ++r) {
         hipEventElapsedTime(&t[3 * r + 0], c->ev[3 * r + 0], c->ev[3 * r + 1]);
         hipEventElapsedTime(&t[3 * r + 1], c->ev[3 * r + 1], c->ev[3 * r + 2]);
@@ -629,10 +629,12 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
         if (f) {
             hipEventElapsedTime(&t[7 + 2 * r], c->ev[3 * r + 0], c->ev[9 + 2 * r]);
             hipEventElapsedTime(&t[8 + 2 * r], c->ev[9 + 2 * r], c->ev[10 + 2 * r]);
+            hipEventElapsedTime(&t[11 + 2 * r], c->ev[10 + 2 * r], c->ev[13 + r]);
+            hipEventElapsedTime(&t[12 + 2 * r], c->ev[13 + r], c->ev[3 * r + 1]);
         }
     }
     hipEventElapsedTime(&t[6], c->ev[8], c->ev[6 + rounds - 1]);
-    for (int i = 0; i < n_stage && i < 11; ++i) stage_ms[i] = t[i];
+    for (int i = 0; i < n_stage && i < 15; ++i) stage_ms[i] = t[i];
     uint32_t cnt[32];
     CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
     if (getenv("DMX_DEBUG_STATS"))
@@ -643,7 +645,7 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
                 cnt[7], cnt[8], cnt[9]);
     if (counts) {
         const bool b0 = c->band_ok[0] && !c->force_ring, b1 = c->band_ok[1] && !c->force_ring;
-        const uint64_t v[10] = {cnt[0],
+        const uint64_t v[12] = {cnt[0],
                                 cnt[1],
                                 c->panel[0].verify ? cnt[10] : cnt[4],
                                 c->panel[1].verify ? cnt[11] : cnt[5],
@@ -652,8 +654,10 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
                                 cnt[17],
                                 cnt[21],
                                 cnt[4],
-                                cnt[5]};
-        for (int i = 0; i < n_counts && i < 10; ++i) counts[i] = v[i];
+                                cnt[5],
+                                cnt[12],
+                                cnt[13]};
+        for (int i = 0; i < n_counts && i < 12; ++i) counts[i] = v[i];
     }
     if (flags) {
         int f = (int)cnt[3];

@@ -74,8 +74,8 @@ struct Ctx {
     size_t task_cap = 0;
     bool no_screen = false;              // DMX_NO_SCREEN=1: every window runs every adapter
     size_t n_counts = 0;
-    hipEvent_t ev[13] = {};   // [3r..3r+2] round r stages, [6+r] finalize, [8] start,
-                              // [9+2r] after filter, [10+2r] after verify
+    hipEvent_t ev[15] = {};   // [3r..3r+2] round r stages, [6+r] finalize, [8] start,
+                              // [9+2r] after filter, [10+2r] after verify, [13+r] after screen
     bool executed = false;
     ChopState* chop = nullptr;   // dmx_chop_* state, created by dmx_chop_set
 

@@ -361,6 +361,24 @@ __device__ __forceinline__ void flush_cands(const Sink& sink, const TaskView& tv
     }
 }
 
+// 16 bytes in four registers: byte q <- low byte of v (q a compile-time constant after
+// unrolling: one v_perm), and signed byte q for a run-time q (selects; a register array indexed
+// at run time would be demoted to LDS or scratch).
+struct Bytes16 {
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    __device__ __forceinline__ void put(int q, uint32_t v) {
+        const uint32_t sel = (0x03020100u & ~(0xFFu << (8 * (q & 3)))) | (4u << (8 * (q & 3)));
+        if (q < 4) w0 = __builtin_amdgcn_perm(v, w0, sel);
+        else if (q < 8) w1 = __builtin_amdgcn_perm(v, w1, sel);
+        else if (q < 12) w2 = __builtin_amdgcn_perm(v, w2, sel);
+        else w3 = __builtin_amdgcn_perm(v, w3, sel);
+    }
+    __device__ __forceinline__ int get(int q) const {
+        const uint32_t x = q < 8 ? (q < 4 ? w0 : w1) : (q < 12 ? w2 : w3);
+        return (int)(int8_t)(uint8_t)(x >> (8 * (q & 3)));
+    }
+};
+
 template <int HB, class Sink>
 __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink& sink,
                                                  const TaskView& tv, uint32_t item, int sub,
@@ -380,38 +398,53 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
     uint32_t seg = 0;
     uint64_t cm = 0, c0 = 0, c1 = 0, c2 = 0;
 
-#define DMX_CAND_STEP(q)                                                                  \
+    // One hit column j (D(m, j) = dv <= kk): the acceptance tests near column 0, the lower-bound
+    // key, and the column's cost bits in the current 64-column segment.
+    auto hit = [&](uint32_t j, int dv) __attribute__((always_inline)) {
+        bool ok = j >= jlo;
+        int L0 = m;
+        if (ok && (int)j < m + kk) {   // near column 0: the acceptance tables
+            ok = dv <= (int)pacc[min(m, (int)j + dv)];
+            L0 = min(m, (int)j - dv);
+            if (ok && !(L0 >= 0 && dv <= (int)acc[L0])) L0 = -1;
+        }
+        if (ok) {
+            // certainly accepted: aligned length >= L0 and acc is monotone (far from column 0,
+            // L0 = m and acc[m] = k >= d)
+            if (L0 >= 0) lbk = max(lbk, lb_key(L0 - 3 * dv, tv.o, dv));
+            if (!segset) {
+                segset = true;
+                seg = j;
+            }
+            const uint64_t bm = 1ull << (j - seg);
+            cm |= bm;
+            if (dv & 1) c0 |= bm;
+            if (dv & 2) c1 |= bm;
+            if (dv & 4) c2 |= bm;
+        }
+    };
+    // The 16 steps of a chunk are branch-free: each records the sign of D - kk - 1 (a hit bit,
+    // shifted in from the bottom: column q ends at bit 15 - q) and D's low byte; the hit columns
+    // of this lane are visited afterwards in column order.  (A per-column branch on D <= kk is
+    // taken by some lane of the wave in nearly every column.)
+    const int e0 = kk + 1;
+    int e = d - e0;                   // D - kk - 1: negative exactly at hit columns
+#define DMX_CAND_REC(q)                                                                   \
     {                                                                                     \
-        myers_step<HB>(eqv[q], pv, mv, d, hbit);                                          \
-        if (d <= kk) {                                                                    \
-            const uint32_t j = p0 + (q) + 1;                                              \
-            bool ok = j >= jlo;                                                           \
-            int L0 = m;                                                                   \
-            if (ok && (int)j < m + kk) {   /* near column 0: the acceptance tables */      \
-                ok = d <= (int)pacc[min(m, (int)j + d)];                                  \
-                L0 = min(m, (int)j - d);                                                  \
-                if (ok && !(L0 >= 0 && d <= (int)acc[L0])) L0 = -1;                       \
-            }                                                                             \
-            if (ok) {                                                                     \
-                /* certainly accepted: aligned length >= L0 and acc is monotone (far from \
-                   column 0, L0 = m and acc[m] = k >= d) */                               \
-                if (L0 >= 0) lbk = max(lbk, lb_key(L0 - 3 * d, tv.o, d));                       \
-                if (!segset) {                                                            \
-                    segset = true;                                                        \
-                    seg = j;                                                              \
-                }                                                                         \
-                const uint64_t bm = 1ull << (j - seg);                                    \
-                cm |= bm;                                                                 \
-                if (d & 1) c0 |= bm;                                                      \
-                if (d & 2) c1 |= bm;                                                      \
-                if (d & 4) c2 |= bm;                                                      \
-            }                                                                             \
-        }                                                                                 \
+        myers_step<HB>(eqv(q), pv, mv, e, hbit);                                          \
+        hits = __builtin_amdgcn_alignbit(hits, (uint32_t)e, 31);                          \
+        dq.put((q), (uint32_t)e);                                                         \
+    }
+#define DMX_CAND_VISIT(NQ)                                                                \
+    while (hits) {                                                                        \
+        const int q = (int)__clz(hits) - (32 - (NQ));                                     \
+        hits &= ~(0x80000000u >> __clz(hits));                                            \
+        hit(p0 + (uint32_t)q + 1u, dq.get(q) + e0);                                    \
     }
 #define DMX_CAND_EQ                                                                       \
-    uint64_t eqv[16];                                                                     \
-    _Pragma("unroll") for (int q = 0; q < 16; ++q)                                        \
-        eqv[q] = peq[(((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)) * kPeqStride];
+    const auto eqv = [&](int q) __attribute__((always_inline)) {                                                         \
+        return peq[(((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)) * kPeqStride];   \
+    };
 
     uint32_t p0 = js;
     uint32_t ncodes, nnb;             // next chunk, prefetched one chunk ahead
@@ -426,8 +459,11 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
             cm = c0 = c1 = c2 = 0;
         }
         DMX_CAND_EQ
+        uint32_t hits = 0;
+        Bytes16 dq;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) DMX_CAND_STEP(q)
+        for (int q = 0; q < 16; ++q) DMX_CAND_REC(q)
+        DMX_CAND_VISIT(16)
     }
     if (p0 < jhi) {
         const uint32_t codes = ncodes, nb = nnb;
@@ -438,11 +474,21 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
         }
         DMX_CAND_EQ
         const int cnt = (int)(jhi - p0);
+        uint32_t hits = 0;
+        Bytes16 dq;
 #pragma unroll
         for (int q = 0; q < 16; ++q)
-            if (q < cnt) DMX_CAND_STEP(q)
+            if (q < cnt) DMX_CAND_REC(q)
+        // cnt steps ran: column q's hit bit sits at bit cnt - 1 - q
+        while (hits) {
+            const int q = (int)__clz(hits) - (32 - cnt);
+            hits &= ~(0x80000000u >> __clz(hits));
+            hit(p0 + (uint32_t)q + 1u, dq.get(q) + e0);
+        }
     }
-#undef DMX_CAND_STEP
+    d = e + e0;
+#undef DMX_CAND_REC
+#undef DMX_CAND_VISIT
 #undef DMX_CAND_EQ
     // 3' adapters: last-column cells (adapter prefix aligned at the read end)
     uint64_t rows = 0;
@@ -2146,11 +2192,13 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         hipEventRecord(c->ev[10 + 2 * round], st);
         if (R.screen)
             hipLaunchKernelGGL(iscreen_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
+        hipEventRecord(c->ev[13 + round], st);
         if (band) hipLaunchKernelGGL(wscan_kernel<true>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(wscan_kernel<false>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
     } else if (grid > 0) {
         hipEventRecord(c->ev[9 + 2 * round], st);
         hipEventRecord(c->ev[10 + 2 * round], st);
+        hipEventRecord(c->ev[13 + round], st);
         if (band) hipLaunchKernelGGL(scan_kernel<true>, dim3(grid), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(scan_kernel<false>, dim3(grid), dim3(kScanBlock), 0, st, R);
     }

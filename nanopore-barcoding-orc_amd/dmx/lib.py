@@ -356,16 +356,18 @@ class Context:
         return buf.view(CAND_DTYPE if what in (DBG_CANDS0, DBG_CANDS1) else WINDOW_DTYPE)
 
     def stats(self):
-        ms = (ctypes.c_float * 11)()
-        cl = np.zeros(10, dtype=np.uint64)
+        ms = (ctypes.c_float * 15)()
+        cl = np.zeros(12, dtype=np.uint64)
         fl = ctypes.c_int()
-        self._check(self._L.dmx_stats(self._h, ms, 11, cl.ctypes.data, 10, ctypes.byref(fl)),
+        self._check(self._L.dmx_stats(self._h, ms, 15, cl.ctypes.data, 12, ctypes.byref(fl)),
                     "dmx_stats")
         names = ["scan0", "resolve0", "finalize0", "scan1", "resolve1", "finalize1", "total",
-                 "filter0", "verify0", "filter1", "verify1"]
+                 "filter0", "verify0", "filter1", "verify1", "screen0", "wscan0", "screen1",
+                 "wscan1"]
         return {"ms": dict(zip(names, list(ms))), "clusters": cl[:2].tolist(),
                 "windows": cl[2:4].tolist(), "resolved": cl[4:6].tolist(),
                 "traces": cl[6:8].tolist(), "windows_raw": cl[8:10].tolist(),
+                "tasks": cl[10:12].tolist(),
                 "flags": fl.value}
 
 

@@ -8,5 +8,5 @@ for l in "$@"; do
   tag=$(basename "$l" .so)
   if [ "$l" = default ]; then unset DMX_LIBDMX; else export DMX_LIBDMX=$PWD/$l; fi
   timeout -k 10 200 python3 bench.py --no-cpu-baseline > "$out/$tag.json" 2> "$out/$tag.err"
-  python3 -c "import json,sys; d=json.load(open('$out/$tag.json')); s=d['stage_ms_per_step']; print('$tag', d['value'], 'ms', d['ms_per_step'], 'scan0', s['scan0'], 'scan1', s['scan1'], 'f0', s['filter0'], 'f1', s['filter1'])"
+  python3 -c "import json,sys; d=json.load(open('$out/$tag.json')); s=d['stage_ms_per_step']; print('$tag', d['value'], 'ms', d['ms_per_step'], ' '.join(f'{k} {v}' for k, v in s.items() if k not in ('scan0', 'scan1', 'total')))"
 done

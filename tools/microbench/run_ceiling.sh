@@ -1,0 +1,29 @@
+#!/bin/bash
+# VALU issue ceiling on the GPU box (tools/microbench/myers_ilp.hip): independent v_bitop3 chains
+# and the 64-bit Myers step at 1..8 waves per SIMD, with the shader clock sampled before and after.
+# Usage: tools/microbench/run_ceiling.sh OUT.json
+set -e -o pipefail
+here=$(dirname "$0")
+out=$1
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o /tmp/myers_ilp "$here/myers_ilp.hip"
+clk0=$(timeout -k 5 30 rocm-smi --showclocks 2>/dev/null | grep -i "sclk" | head -2 | tr '\n' ' ' || true)
+res=$(timeout -k 10 120 /tmp/myers_ilp)
+clk1=$(timeout -k 5 30 rocm-smi --showclocks 2>/dev/null | grep -i "sclk" | head -2 | tr '\n' ' ' || true)
+python3 - "$out" "$clk0" "$clk1" <<PY
+import json, re, sys
+res = """$res"""
+lines = [l for l in res.splitlines() if l.strip()]
+m = re.search(r"bitop3 chain x4: ([0-9.]+) ms\s+([0-9.]+) T lane-ops/s", res)
+steps = [dict(chains=int(a), waves_per_simd=int(b), ms=float(c), g_lane_steps_per_s=float(d))
+         for a, b, c, d in re.findall(r"chains (\d+) waves/SIMD (\d+): ([0-9.]+) ms\s+([0-9.]+) G", res)]
+out = {"what": "VALU issue ceiling, gfx950 (MI355X): v_bitop3 dependency chains x4 per lane at "
+               "8192 x 256 threads; 64-bit Myers step (myers_step_hw) by chains per lane and waves "
+               "per SIMD", "source": "tools/microbench/myers_ilp.hip",
+       "bitop3_t_lane_ops_per_s": float(m.group(2)) if m else None,
+       "nominal_t_lane_ops_per_s": 256 * 4 * 32 * 2.4e9 / 1e12,
+       "myers_step": steps,
+       "best_g_lane_steps_per_s": max((s["g_lane_steps_per_s"] for s in steps), default=None),
+       "sclk_before": sys.argv[2], "sclk_after": sys.argv[3], "raw": lines}
+json.dump(out, open(sys.argv[1], "w"), indent=1)
+print(json.dumps({k: out[k] for k in ("bitop3_t_lane_ops_per_s", "best_g_lane_steps_per_s", "sclk_before")}))
+PY
