@@ -132,6 +132,36 @@ int ensure_pipeline(Ctx* c) {
     return DMX_OK;
 }
 
+// The pipeline counters (dmx_internal.h) with the sharded lists' totals (records kept, over
+// every shard) folded into their old slots: cnt[4 + r] windows, cnt[10 + r] verified windows,
+// cnt[12 + r] screen tasks, cnt[6 + 2r + l] candidates.  *ovf: flag bits of overflowed lists
+// (4 windows / tasks, 8 candidates).
+hipError_t read_counters(Ctx* c, uint32_t* cnt, int* ovf) {
+    hipError_t e = hipMemcpy(cnt, c->d_counters, 32 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    uint32_t sh[kShLists * kShards];
+    e = hipMemcpy(sh, c->d_shard, sizeof(sh), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    int o = 0;
+    for (int x = 0; x < kShLists; ++x) {
+        const bool cand = x >= kShCand;
+        const uint32_t scap = (uint32_t)((cand ? c->cand_cap : x >= kShTasks ? c->task_cap
+                                                                            : c->win_cap) /
+                                         kShards);
+        uint64_t t = 0;
+        for (int s = 0; s < kShards; ++s) {
+            const uint32_t v = sh[x * kShards + s];
+            t += std::min(v, scap);
+            if (v > scap) o |= cand ? 8 : 4;
+        }
+        const int slot = x < kShWin2 ? 4 + x : x < kShTasks ? 10 + (x - kShWin2)
+                       : x < kShCand ? 12 + (x - kShTasks) : 6 + (x - kShCand);
+        cnt[slot] = (uint32_t)t;
+    }
+    if (ovf) *ovf = o;
+    return hipSuccess;
+}
+
 int grow_cands(Ctx* c) {
     const size_t want = c->cand_cap * 2;
     int rc;
@@ -214,6 +244,7 @@ int dmx_open(int device, dmx_ctx** out) {
     for (auto& e : c->ev) hipEventCreate(&e);
     for (int r = 0; r < 2; ++r) hipMalloc((void**)&c->d_panel[r], sizeof(DevPanel));
     hipMalloc((void**)&c->d_counters, 32 * sizeof(uint32_t));
+    hipMalloc((void**)&c->d_shard, kShLists * kShards * sizeof(uint32_t));
     *out = c;
     return DMX_OK;
 }
@@ -226,7 +257,7 @@ void dmx_close(dmx_ctx* c) {
     comm_release(c);
     void* bufs[] = {c->d_seq_alloc, c->d_nmask_alloc,     c->d_offs,     c->d_lens,      c->d_res,
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
-                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_tasks, c->d_counters,
+                    c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_tasks, c->d_counters, c->d_shard,
                     c->d_counts,    c->d_panel[0],  c->d_panel[1]};
     for (void* b : bufs)
         if (b) hipFree(b);
@@ -552,6 +583,7 @@ int dmx_exec(dmx_ctx* c) {
     hipStream_t st = c->stream;
     CK(hipEventRecord(c->ev[8], st));
     CK(hipMemsetAsync(c->d_counters, 0, 32 * sizeof(uint32_t), st));
+    CK(hipMemsetAsync(c->d_shard, 0, kShLists * kShards * sizeof(uint32_t), st));
     CK(hipMemsetAsync(c->d_counts, 0, c->n_counts * sizeof(unsigned long long), st));
     // A panel whose accepted matches can score <= 0 keeps one winner per orientation:
     // ReverseComplementer compares the two orientations' best scores with "no match" = 0, so
@@ -636,7 +668,8 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
     hipEventElapsedTime(&t[6], c->ev[8], c->ev[6 + rounds - 1]);
     for (int i = 0; i < n_stage && i < 15; ++i) stage_ms[i] = t[i];
     uint32_t cnt[32];
-    CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
+    int list_ovf = 0;
+    CK(read_counters(c, cnt, &list_ovf));
     if (getenv("DMX_DEBUG_STATS"))
         fprintf(stderr,
                 "dmx stats: windows raw %u %u verified %u %u screened tasks %u %u "
@@ -662,11 +695,7 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
     if (flags) {
         int f = (int)cnt[3];
         if (cnt[0] > c->cl_cap || cnt[1] > c->cl_cap) f |= 1;
-        if (cnt[4] > c->win_cap || cnt[5] > c->win_cap) f |= 4;
-        if (cnt[10] > c->win_cap || cnt[11] > c->win_cap) f |= 4;
-        if (cnt[12] > c->task_cap || cnt[13] > c->task_cap) f |= 4;
-        for (int x = 6; x < 10; ++x)
-            if (cnt[x] > c->cand_cap) f |= 8;
+        f |= list_ovf;
         *flags = f;
     }
     return DMX_OK;
@@ -681,26 +710,35 @@ int dmx_debug_fetch(dmx_ctx* c, int what, int round, void* out, size_t cap_bytes
     CK(hipSetDevice(c->device));
     CK(hipStreamSynchronize(c->stream));
     uint32_t cnt[32];
-    CK(hipMemcpy(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
-    const void* src = nullptr;
-    size_t bytes = 0;
-    switch (what) {
-        case DMX_DBG_WINDOWS: src = c->d_win; bytes = std::min<size_t>(cnt[4 + round], c->win_cap) * sizeof(Window); break;
-        case DMX_DBG_VERIFIED: src = c->d_win2; bytes = std::min<size_t>(cnt[10 + round], c->win_cap) * sizeof(Window); break;
-        case DMX_DBG_TASKS: src = c->d_tasks; bytes = std::min<size_t>(cnt[12 + round], c->task_cap) * sizeof(Window); break;
-        case DMX_DBG_CANDS0: src = c->d_cand[round][0]; bytes = std::min<size_t>(cnt[6 + 2 * round], c->cand_cap) * sizeof(Cand); break;
-        case DMX_DBG_CANDS1: src = c->d_cand[round][1]; bytes = std::min<size_t>(cnt[7 + 2 * round], c->cand_cap) * sizeof(Cand); break;
-        case DMX_DBG_FLAGS: src = nullptr; bytes = 4; break;
-        default: return DMX_E_INVALID;
-    }
-    // windows / tasks of round 1 share buffers with round 0: only the last round's are resident
+    CK(read_counters(c, cnt, nullptr));
     if (what == DMX_DBG_FLAGS) {
         if (cap_bytes >= 4) std::memcpy(out, &cnt[3], 4);
         return 4;
     }
-    const size_t n = std::min(bytes, cap_bytes);
-    if (n) CK(hipMemcpy(out, src, n, hipMemcpyDeviceToHost));
-    return (int)std::min<size_t>(bytes, (size_t)1 << 30);
+    // every list is sharded: gather its shards (windows and tasks of round 1 share buffers with
+    // round 0: only the last executed round's are resident)
+    int slot;
+    const char* base;
+    size_t cap, rec;
+    switch (what) {
+        case DMX_DBG_WINDOWS: slot = kShWin + round; base = (const char*)c->d_win; cap = c->win_cap; rec = sizeof(Window); break;
+        case DMX_DBG_VERIFIED: slot = kShWin2 + round; base = (const char*)c->d_win2; cap = c->win_cap; rec = sizeof(Window); break;
+        case DMX_DBG_TASKS: slot = kShTasks + round; base = (const char*)c->d_tasks; cap = c->task_cap; rec = sizeof(Window); break;
+        case DMX_DBG_CANDS0: slot = kShCand + 2 * round; base = (const char*)c->d_cand[round][0]; cap = c->cand_cap; rec = sizeof(Cand); break;
+        case DMX_DBG_CANDS1: slot = kShCand + 2 * round + 1; base = (const char*)c->d_cand[round][1]; cap = c->cand_cap; rec = sizeof(Cand); break;
+        default: return DMX_E_INVALID;
+    }
+    uint32_t sh[kShards];
+    CK(hipMemcpy(sh, c->d_shard + slot * kShards, sizeof(sh), hipMemcpyDeviceToHost));
+    const size_t scap = cap / kShards;
+    size_t done = 0;
+    for (int s = 0; s < kShards; ++s) {
+        const size_t nb = std::min<size_t>(sh[s], scap) * rec;
+        const size_t take = out ? std::min(nb, cap_bytes > done ? cap_bytes - done : 0) : 0;
+        if (take) CK(hipMemcpy((char*)out + done, base + s * scap * rec, take, hipMemcpyDeviceToHost));
+        done += nb;
+    }
+    return (int)std::min<size_t>(done, (size_t)1 << 30);
 }
 
 int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,

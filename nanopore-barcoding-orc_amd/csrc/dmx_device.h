@@ -97,6 +97,11 @@ struct Window {
 static_assert(sizeof(Window) == 40, "Window layout");
 
 constexpr int kStageCap = 256;    // LDS staging of emitted records per block
+// Appendable lists are split into kShards shards, each with its own counter (a slot of
+// Ctx::d_shard) and a fixed capacity: one device-scope counter that every wave of the grid
+// appends through serialises them (measured: the window scan ran at the counter's atomic rate).
+constexpr int kShards = 16;
+enum ShardList { kShWin = 0, kShWin2 = 2, kShTasks = 4, kShCand = 6, kShLists = 10 };
 constexpr int kCandStageCap = 128; // per candidate list
 
 // Block-level staging of appended records: lanes append to LDS (LDS atomics), the block then

@@ -67,6 +67,7 @@ struct Ctx {
     size_t win_cap = 0;
     ItemView* d_items = nullptr;
     size_t item_cap = 0;
+    uint32_t* d_shard = nullptr;      // [kShLists][kShards] per-shard list counters (dmx_device.h)
     uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows, [6+2r..] candidates, [10+r] verified windows, [16+4r..] diag
     unsigned long long* d_counts = nullptr;
     unsigned long long* d_linked = nullptr;

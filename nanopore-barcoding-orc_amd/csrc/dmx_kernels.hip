@@ -35,20 +35,23 @@ struct RoundArgs {
     int32_t* origin;             // per slot
     int32_t* lb;                 // per slot: lower bound of the best accepted score (0 = none)
     Window* win;
-    uint32_t* win_count;
+    uint32_t* win_count;         // [kShards]: shard s at win + s * win_scap
     uint32_t win_cap;
+    uint32_t win_scap;
     Window* win2;                // verified windows (when the panel has a shared prefix)
-    uint32_t* win2_count;
+    uint32_t* win2_count;        // [kShards], per-shard capacity win_scap
     uint32_t* diag;              // [0] resolved clusters, [1] tracebacks
     int32_t band;                // 1: emit candidate cells (band kernels), 0: clusters (ring)
     Cand* cand[2];               // candidate lists: [0] cost <= 3 (band 7), [1] cost 4..7 (15)
     Outcome* cand_out[2];
-    uint32_t* cand_count;        // [2]
+    uint32_t* cand_count;        // [2][kShards]: list l, shard s at cand[l] + s * cand_scap
     uint32_t cand_cap;
+    uint32_t cand_scap;          // per-shard capacity
     int32_t screen;              // 1: the window scan runs the index screen's surviving pairs
     Window* tasks;               // index screen survivors: window pieces of one adapter each
-    uint32_t* task_count;
+    uint32_t* task_count;        // [kShards]: shard s at tasks + s * task_scap
     uint32_t task_cap;
+    uint32_t task_scap;
 };
 
 struct TaskView {
@@ -296,7 +299,45 @@ struct WaveStage {
     }
 };
 
-constexpr int kWaveCandCap = 64;
+// The shard a wave appends to (waves of a block spread over consecutive shards).
+__device__ __forceinline__ uint32_t wave_shard() {
+    return (blockIdx.x * (kScanBlock / 64) + (threadIdx.x >> 6)) & (uint32_t)(kShards - 1);
+}
+
+// Reader side of a sharded list: the block's prefix over the shards' (clamped) counts in LDS,
+// and the dense index -> record index map.  Every thread of the block calls load().
+struct ShardMap {
+    uint32_t* pre;   // LDS [kShards + 1]
+    uint32_t scap;
+    __device__ __forceinline__ void load(const uint32_t* counts, uint32_t shard_cap) {
+        scap = shard_cap;
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int k = 0; k < kShards; ++k) {
+                pre[k] = t;
+                t += min(counts[k], shard_cap);
+            }
+            pre[kShards] = t;
+        }
+        __syncthreads();
+    }
+    __device__ __forceinline__ uint32_t total() const { return pre[kShards]; }
+    __device__ __forceinline__ uint32_t phys(uint32_t t) const {
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t h = kShards / 2; h > 0; h >>= 1)
+            if (t >= pre[s + h]) s += h;
+        return s * scap + (t - pre[s]);
+    }
+};
+
+#ifndef DMX_WAVE_CAND_CAP
+#define DMX_WAVE_CAND_CAP 32   // rare: cells of earlier 64-column segments
+#endif
+#ifndef DMX_WAVE_CAND_FLUSH
+#define DMX_WAVE_CAND_FLUSH (DMX_WAVE_CAND_CAP / 2)
+#endif
+constexpr int kWaveCandCap = DMX_WAVE_CAND_CAP;
 constexpr int kWaveWinCap = 64;   // per-wave window / task staging (filter, verify, screen)
 
 struct WaveCandSink {
@@ -379,13 +420,78 @@ struct Bytes16 {
     }
 };
 
+// A task's candidate cells held in registers until the wave's next uniform point: its last
+// 64-column segment (cells with bits in `cells`, costs in three planes) and its 3' last-column
+// rows by list, all already filtered by the task's final lower-bound key.  Cells of earlier
+// segments (hit spans over 64 columns: rare) go through the staging sink as before.
+struct CandOut {
+    uint64_t cells = 0, c0 = 0, c1 = 0, c2 = 0;
+    uint64_t rows0 = 0, rows1 = 0;      // rows by list (cost <= 3 / > 3)
+    uint64_t pv = 0, mv = 0;            // column `len`: the rows' costs
+    uint32_t seg = 0;
+};
+
+// Exclusive prefix sum over the 64 lanes of the wave (every lane calls it), and the total.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+// Write every lane's held candidates: one prefix sum and one global atomic per list for the
+// whole wave (per-record or per-flush atomics on the two list counters serialise the scan).
+// Called by all lanes of the wave at a wave-uniform point; lanes without a task hold nothing.
+__device__ __forceinline__ void emit_cands(const RoundArgs& R, const CandOut& co,
+                                           const TaskView& tv, uint32_t item, int sub, int m) {
+    const uint32_t n1 = (uint32_t)(__popcll(co.cells & co.c2) + __popcll(co.rows1));
+    const uint32_t n0 = (uint32_t)(__popcll(co.cells & ~co.c2) + __popcll(co.rows0));
+    uint32_t tot;
+    const uint32_t pre = wave_excl_scan(n0 | (n1 << 16), tot);   // <= 64 x 128 per list
+    if (tot == 0) return;                                        // wave-uniform
+    const uint32_t sh = wave_shard();
+    uint32_t b0 = 0, b1 = 0;
+    if ((threadIdx.x & 63u) == 0) {
+        if (tot & 0xFFFFu) b0 = atomicAdd(R.cand_count + sh, tot & 0xFFFFu);
+        if (tot >> 16) b1 = atomicAdd(R.cand_count + kShards + sh, tot >> 16);
+    }
+    b0 = __builtin_amdgcn_readfirstlane(b0) + (pre & 0xFFFFu);
+    b1 = __builtin_amdgcn_readfirstlane(b1) + (pre >> 16);
+    const auto put = [&](int l, const Cand& cd) __attribute__((always_inline)) {
+        const uint32_t i = l ? b1++ : b0++;
+        if (i < R.cand_scap) R.cand[l][sh * R.cand_scap + i] = cd;
+        else atomicOr(R.flags, 8u);
+    };
+    uint64_t x = co.cells;
+    while (x) {
+        const int bit = __ffsll((unsigned long long)x) - 1;
+        x &= x - 1;
+        const int cost = (int)((co.c0 >> bit) & 1ull) | ((int)((co.c1 >> bit) & 1ull) << 1) |
+                         ((int)((co.c2 >> bit) & 1ull) << 2);
+        put(cost > 3, make_cand(tv, item, sub, m, cost, co.seg + (uint32_t)bit));
+    }
+    x = co.rows0 | co.rows1;
+    while (x) {
+        const int i = __ffsll((unsigned long long)x) - 1;
+        x &= x - 1;
+        const int cost = col_cost(co.pv, co.mv, i);
+        put(cost > 3, make_cand(tv, item, sub, i, cost, tv.len));
+    }
+}
+
 template <int HB, class Sink>
 __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink& sink,
                                                  const TaskView& tv, uint32_t item, int sub,
                                                  const uint64_t* peq, int A, const DevAdapter& ad,
                                                  const int8_t* acc, const int8_t* pacc,
                                                  uint32_t js, bool real, uint32_t jlo,
-                                                 uint32_t jhi, bool lastcol) {
+                                                 uint32_t jhi, bool lastcol,
+                                                 CandOut* out = nullptr) {
     const int m = ad.m;
     const int kk = ad.kk;   // <= 7 in band mode (three cost planes)
     const bool front = ad.where == kFront;
@@ -503,6 +609,34 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
             }
         }
     }
+    if (out) {   // hold the cells for the wave's direct emission (emit_cands)
+        uint64_t keep = 0, x = cm;
+        while (x) {
+            const int bit = __ffsll((unsigned long long)x) - 1;
+            x &= x - 1;
+            const int cost = (int)((c0 >> bit) & 1ull) | ((int)((c1 >> bit) & 1ull) << 1) |
+                             ((int)((c2 >> bit) & 1ull) << 2);
+            if (viable_lb(lbk, min(m, (int)(seg + (uint32_t)bit) + cost), tv.o, cost))
+                keep |= 1ull << bit;
+        }
+        out->cells = keep;
+        out->c0 = c0;
+        out->c1 = c1;
+        out->c2 = c2;
+        out->seg = seg;
+        out->pv = pv;
+        out->mv = mv;
+        out->rows0 = out->rows1 = 0;
+        while (rows) {
+            const int i = __ffsll((unsigned long long)rows) - 1;
+            rows &= rows - 1;
+            const int cost = col_cost(pv, mv, i);
+            if (!viable_lb(lbk, i, tv.o, cost)) continue;
+            if (cost <= 3) out->rows0 |= 1ull << i;
+            else out->rows1 |= 1ull << i;
+        }
+        return lbk;
+    }
     if (cm) flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
     while (rows) {                                // scan order: after every last-row cell
         const int i = __ffsll((unsigned long long)rows) - 1;
@@ -524,24 +658,28 @@ __device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const Sink& si
                                               const uint64_t* peq, int A, const DevAdapter& ad,
                                               const int8_t* acc, const int8_t* pacc,
                                               uint32_t js, bool real, uint32_t jlo,
-                                              uint32_t jhi, bool lastcol) {
+                                              uint32_t jhi, bool lastcol,
+                                              CandOut* out = nullptr) {
     if (ad.m > 32)
-        return scan_task_cand_hb<1, Sink>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real, jlo,
-                                    jhi, lastcol);
-    return scan_task_cand_hb<0, Sink>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real, jlo, jhi,
-                                lastcol);
+        return scan_task_cand_hb<1, Sink>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real,
+                                          jlo, jhi, lastcol, out);
+    return scan_task_cand_hb<0, Sink>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real, jlo,
+                                      jhi, lastcol, out);
 }
 
 #define DMX_CAND_STAGE                                                                    \
     __shared__ Cand s_cand[2][kCandStageCap];                                             \
     __shared__ uint32_t s_ccnt[2], s_cbase[2];                                            \
     if (threadIdx.x < 2) s_ccnt[threadIdx.x] = 0;                                         \
+    const uint32_t bsh = blockIdx.x & (uint32_t)(kShards - 1);                           \
     const CandSink sink{{Stage<Cand, kCandStageCap>{s_cand[0], &s_ccnt[0], &s_cbase[0],    \
-                                                    R.cand[0], R.cand_count, R.cand_cap,   \
+                                                    R.cand[0] + bsh * R.cand_scap,         \
+                                                    R.cand_count + bsh, R.cand_scap,       \
                                                     R.flags, 8u},                          \
                          Stage<Cand, kCandStageCap>{s_cand[1], &s_ccnt[1], &s_cbase[1],    \
-                                                    R.cand[1], R.cand_count + 1,           \
-                                                    R.cand_cap, R.flags, 8u}}};
+                                                    R.cand[1] + bsh * R.cand_scap,         \
+                                                    R.cand_count + kShards + bsh,          \
+                                                    R.cand_scap, R.flags, 8u}}};
 
 // Both kernels are templated on BAND; only the stage the instantiation uses takes LDS.
 #define DMX_STAGES                                                                        \
@@ -553,12 +691,15 @@ __device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const Sink& si
     __shared__ Cand s_cand[2][BAND ? kCandStageCap : 1];                                  \
     __shared__ uint32_t s_ccnt[2], s_cbase[2];                                            \
     if (threadIdx.x < 2) s_ccnt[threadIdx.x] = 0;                                         \
+    const uint32_t bsh = blockIdx.x & (uint32_t)(kShards - 1);                           \
     const CandSink sink{{Stage<Cand, kCandStageCap>{s_cand[0], &s_ccnt[0], &s_cbase[0],    \
-                                                    R.cand[0], R.cand_count, R.cand_cap,   \
+                                                    R.cand[0] + bsh * R.cand_scap,         \
+                                                    R.cand_count + bsh, R.cand_scap,       \
                                                     R.flags, 8u},                          \
                          Stage<Cand, kCandStageCap>{s_cand[1], &s_ccnt[1], &s_cbase[1],    \
-                                                    R.cand[1], R.cand_count + 1,           \
-                                                    R.cand_cap, R.flags, 8u}}};
+                                                    R.cand[1] + bsh * R.cand_scap,         \
+                                                    R.cand_count + kShards + bsh,          \
+                                                    R.cand_scap, R.flags, 8u}}};
 
 #define DMX_CLUSTER_STAGE                                                                 \
     __shared__ Cluster s_cl[kStageCap];                                                   \
@@ -902,8 +1043,9 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     __syncthreads();
     const uint32_t T0 = s_tot[0][kScanBlock - 1], T1 = s_tot[1][kScanBlock - 1];
     const uint32_t wv = threadIdx.x >> 6;   // windows staged per wave: no block barriers below
-    const WaveStage<Window, kWaveWinCap> st{s_win[wv], &s_wcnt[wv], R.win, R.win_count,
-                                            R.win_cap, R.flags, 4u};
+    const uint32_t wsh = wave_shard();
+    const WaveStage<Window, kWaveWinCap> st{s_win[wv], &s_wcnt[wv], R.win + wsh * R.win_scap,
+                                            R.win_count + wsh, R.win_scap, R.flags, 4u};
 
     const bool front = P->where == kFront;
     const uint32_t hbit = (uint32_t)(L - 1);
@@ -998,15 +1140,19 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
     const DevPanel* P = R.panel;
     if (threadIdx.x < 72) s_pf[threadIdx.x] = P->pf[threadIdx.x];
     if (threadIdx.x < 8) s_ppeq[threadIdx.x] = P->pre_peq[threadIdx.x];
-    __syncthreads();
-    const Stage<Window> st{s_w, &s_wc, &s_wb, R.win2, R.win2_count, R.win_cap, R.flags, 4u};
+    __shared__ uint32_t s_spre[kShards + 1];
+    ShardMap sm{s_spre, 0u};
+    sm.load(R.win_count, R.win_scap);                  // (its barrier covers the above)
+    const uint32_t bsh = blockIdx.x & (uint32_t)(kShards - 1);
+    const Stage<Window> st{s_w, &s_wc, &s_wb, R.win2 + bsh * R.win_scap, R.win2_count + bsh,
+                           R.win_scap, R.flags, 4u};
     const bool front = P->where == kFront;
     const int L = P->pre_len, kf = P->kf;
-    const uint32_t total = min(*R.win_count, R.win_cap);
+    const uint32_t total = sm.total();
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
         const uint32_t wi = base + threadIdx.x;
         if (wi < total) {
-            Window w = R.win[wi];
+            Window w = R.win[sm.phys(wi)];
             const int len = (int)w.len;
             const bool rows_free = (front && (int)w.j1 <= P->max_mk) || w.bmin == 255;
             // column ranges the prefix block must be evaluated on
@@ -1140,12 +1286,15 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
     for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
     if (threadIdx.x < kScanBlock / 64) s_tc[threadIdx.x] = 0;
     if (threadIdx.x == 0) s_nend = 0;
-    __syncthreads();
+    __shared__ uint32_t s_spre[kShards + 1];
+    ShardMap sm{s_spre, 0u};
+    sm.load(R.win2_count, R.win_scap);                 // (its barrier covers the above)
     const uint32_t wv = threadIdx.x >> 6;
-    const WaveStage<Window, kWaveWinCap> st{s_task[wv], &s_tc[wv], R.tasks, R.task_count,
-                                            R.task_cap, R.flags, 4u};
+    const uint32_t wsh = wave_shard();
+    const WaveStage<Window, kWaveWinCap> st{s_task[wv], &s_tc[wv], R.tasks + wsh * R.task_scap,
+                                            R.task_count + wsh, R.task_scap, R.flags, 4u};
     const Window* wl = R.win2;
-    const uint32_t nwin = min(*R.win2_count, R.win_cap);
+    const uint32_t nwin = sm.total();
     const uint32_t total = nwin * (uint32_t)A;    // host: win_cap * A < 2^32
     const bool front = P->where == kFront;
     const int jsplit = front ? P->jsplit : 0;
@@ -1157,7 +1306,7 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
         if (t < total) {
             const uint32_t wi = t / (uint32_t)A;
             const int a = (int)(t - wi * (uint32_t)A);
-            const Window w = wl[wi];
+            const Window w = wl[sm.phys(wi)];
             const DevAdapter& ad = P->ad[a];
             const int len = (int)w.len, j1 = (int)w.j1, j2 = (int)w.j2;
             const int l = (int)ad.m - pl - sl, kk = ad.kk;
@@ -1277,9 +1426,9 @@ template <bool BAND, class ClStage, class Sink>
 __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, int a, int A,
                                            const uint64_t* s_peq, const int8_t* s_acc,
                                            const int8_t* s_pacc, const ClStage& st,
-                                           const Sink& sink) {
-    const int sub = w.o * A + a;
-    TaskView tv;
+                                           const Sink& sink, CandOut& co, TaskView& tv,
+                                           int& sub) {
+    sub = w.o * A + a;
     tv.read = 0;
     tv.n = w.n;
     tv.strand = w.strand;
@@ -1296,7 +1445,7 @@ __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, 
     if constexpr (BAND)
         lb = scan_task_cand(R, sink, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
                             s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2,
-                            w.lastcol != 0);
+                            w.lastcol != 0, &co);
     else
         lb = scan_task(R, st, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
                        s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2, w.lastcol != 0);
@@ -1317,37 +1466,53 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     __shared__ uint32_t s_clcnt, s_clbase;
     __shared__ Cand s_wcand[BAND ? kScanBlock / 64 : 1][2][kWaveCandCap];
     __shared__ uint32_t s_wcn[kScanBlock / 64][2];
+#ifdef DMX_WSCAN_LDS_PAD   // A/B: occupancy cap through LDS
+    __shared__ uint32_t s_pad[DMX_WSCAN_LDS_PAD / 4];
+    if (threadIdx.x == 0) s_pad[R.n_items & 7] = 0;
+#endif
     if (threadIdx.x == 0) s_clcnt = 0;
     if (threadIdx.x < 2 * (kScanBlock / 64)) (&s_wcn[0][0])[threadIdx.x] = 0;
     const Stage<Cluster> st{s_cl, &s_clcnt, &s_clbase, R.cl, R.cl_count, R.cl_cap, R.flags, 1u};
     const uint32_t wv = BAND ? threadIdx.x >> 6 : 0u;
+    const uint32_t wsh = wave_shard();
     const WaveCandSink sink{{WaveStage<Cand, kWaveCandCap>{s_wcand[wv][0], &s_wcn[wv][0],
-                                                           R.cand[0], R.cand_count, R.cand_cap,
+                                                           R.cand[0] + wsh * R.cand_scap,
+                                                           R.cand_count + wsh, R.cand_scap,
                                                            R.flags, 8u},
                              WaveStage<Cand, kWaveCandCap>{s_wcand[wv][1], &s_wcn[wv][1],
-                                                           R.cand[1], R.cand_count + 1,
-                                                           R.cand_cap, R.flags, 8u}}};
+                                                           R.cand[1] + wsh * R.cand_scap,
+                                                           R.cand_count + kShards + wsh,
+                                                           R.cand_scap, R.flags, 8u}}};
     load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
-    __syncthreads();
+    __shared__ uint32_t s_spre[kShards + 1];
+    ShardMap sm{s_spre, 0u};
+    const Window* wl = R.panel->pre_len ? R.win2 : R.win;
+    if (R.screen) sm.load(R.task_count, R.task_scap);  // (its barrier covers the above)
+    else sm.load(R.panel->pre_len ? R.win2_count : R.win_count, R.win_scap);
 
     const int A = R.panel->n_adapters;
-    const Window* wl = R.panel->pre_len ? R.win2 : R.win;
-    const uint32_t* wc = R.panel->pre_len ? R.win2_count : R.win_count;
     if (R.screen) {   // the index screen's surviving (window piece, adapter) tasks
       const uint32_t stride = gridDim.x * blockDim.x;
       {
         const Window* tl = R.tasks;
-        const uint32_t nt = min(*R.task_count, R.task_cap);
+        const uint32_t nt = sm.total();
         for (uint32_t base = blockIdx.x * blockDim.x; base < nt; base += stride) {
             const uint32_t ti = base + threadIdx.x;
+            CandOut co;
+            TaskView tv{};
+            int sub = 0;
+            uint32_t item = 0;
             if (ti < nt) {
-                const Window w = tl[ti];
-                wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, st, sink);
+                const Window w = tl[sm.phys(ti)];
+                item = w.item;
+                wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, st, sink, co, tv,
+                                 sub);
             }
             if constexpr (BAND) {
+                emit_cands(R, co, tv, item, sub, R.panel->ad[tv.a].m);
                 __builtin_amdgcn_wave_barrier();
-                if (sink.st[0].count() > kWaveCandCap / 2) sink.st[0].flush();
-                if (sink.st[1].count() > kWaveCandCap / 2) sink.st[1].flush();
+                if (sink.st[0].count() > DMX_WAVE_CAND_FLUSH) sink.st[0].flush();
+                if (sink.st[1].count() > DMX_WAVE_CAND_FLUSH) sink.st[1].flush();
             } else {
                 if (stage_count(&s_clcnt) > kStageCap / 2) st.flush();
             }
@@ -1362,19 +1527,25 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
         }
         return;
     }
-    const uint64_t total = (uint64_t)min(*wc, R.win_cap) * (uint64_t)A;
+    const uint64_t total = (uint64_t)sm.total() * (uint64_t)A;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < total;
          base += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t t = base + threadIdx.x;
+        CandOut co;
+        TaskView tv{};
+        int sub = 0;
+        uint32_t item = 0;
         if (t < total) {
-            const Window w = wl[t / A];
+            const Window w = wl[sm.phys((uint32_t)(t / A))];
             const int a = (int)(t % A);
-            wscan_task<BAND>(R, w, a, A, s_peq, s_acc, s_pacc, st, sink);
+            item = w.item;
+            wscan_task<BAND>(R, w, a, A, s_peq, s_acc, s_pacc, st, sink, co, tv, sub);
         }
         if constexpr (BAND) {                        // wave-uniform: no block barrier
+            emit_cands(R, co, tv, item, sub, R.panel->ad[tv.a].m);
             __builtin_amdgcn_wave_barrier();
-            if (sink.st[0].count() > kWaveCandCap / 2) sink.st[0].flush();
-            if (sink.st[1].count() > kWaveCandCap / 2) sink.st[1].flush();
+            if (sink.st[0].count() > DMX_WAVE_CAND_FLUSH) sink.st[0].flush();
+            if (sink.st[1].count() > DMX_WAVE_CAND_FLUSH) sink.st[1].flush();
         } else {
             if (stage_count(&s_clcnt) > kStageCap / 2) st.flush();
         }
@@ -1743,14 +1914,17 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
         s_qe = 0;
         s_n = 0;
     }
-    __syncthreads();
-    const uint32_t total = min(R.cand_count[list], R.cand_cap);
+    __shared__ uint32_t s_spre[kShards + 1];
+    ShardMap sm{s_spre, 0u};
+    sm.load(R.cand_count + list * kShards, R.cand_scap);   // (its barrier covers the above)
+    const uint32_t total = sm.total();
     const Cand* cl = R.cand[list];
     Outcome* outs = R.cand_out[list];
     constexpr int H = W / 2;
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
-        const uint32_t ci = base + threadIdx.x;
-        if (ci < total) {
+        const uint32_t ti = base + threadIdx.x;
+        if (ti < total) {
+            const uint32_t ci = sm.phys(ti);
             const Cand c = cl[ci];
             const uint32_t slot = slot_of(R, c.item, c.sub);
             const int cost = c.cost, iend = c.iend;
@@ -1832,10 +2006,15 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
 }
 
 __global__ void select_cand_kernel(RoundArgs R) {
+    __shared__ uint32_t s_spre[kShards + 1];
     for (int list = 0; list < 2; ++list) {
-        const uint32_t total = min(R.cand_count[list], R.cand_cap);
-        for (uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x; ci < total;
-             ci += gridDim.x * blockDim.x) {
+        ShardMap sm{s_spre, 0u};
+        __syncthreads();   // the previous list's map is no longer read
+        sm.load(R.cand_count + list * kShards, R.cand_scap);
+        const uint32_t total = sm.total();
+        for (uint32_t ti = blockIdx.x * blockDim.x + threadIdx.x; ti < total;
+             ti += gridDim.x * blockDim.x) {
+            const uint32_t ci = sm.phys(ti);
             const Outcome o = R.cand_out[list][ci];
             if (o.key == ~0ull) continue;
             const Cand c = R.cand[list][ci];
@@ -2164,23 +2343,26 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     const uint32_t grid = (uint32_t)((R.n_items + rpb - 1) / rpb);
     R.diag = c->d_counters + 16 + 4 * round;
     R.win = c->d_win;
-    R.win_count = c->d_counters + 4 + round;
+    R.win_count = c->d_shard + (kShWin + round) * kShards;
     R.win2 = c->d_win2;
-    R.win2_count = c->d_counters + 10 + round;
+    R.win2_count = c->d_shard + (kShWin2 + round) * kShards;
     R.win_cap = (uint32_t)c->win_cap;
+    R.win_scap = (uint32_t)(c->win_cap / kShards);
     const bool band = c->band_ok[round] && !c->force_ring;
     R.band = band ? 1 : 0;
     for (int l = 0; l < 2; ++l) {
         R.cand[l] = c->d_cand[round][l];
         R.cand_out[l] = c->d_cand_out[round][l];
     }
-    R.cand_count = c->d_counters + 6 + 2 * round;
+    R.cand_count = c->d_shard + (kShCand + 2 * round) * kShards;
     R.cand_cap = (uint32_t)c->cand_cap;
+    R.cand_scap = (uint32_t)(c->cand_cap / kShards);
     R.screen = (hp.filter && hp.verify && hp.screen && !linked && !c->no_screen &&
                 (uint64_t)c->win_cap * (uint64_t)hp.n < (1ull << 32)) ? 1 : 0;
     R.tasks = c->d_tasks;
-    R.task_count = c->d_counters + 12 + round;
+    R.task_count = c->d_shard + (kShTasks + round) * kShards;
     R.task_cap = (uint32_t)c->task_cap;
+    R.task_scap = (uint32_t)(c->task_cap / kShards);
     hipEventRecord(c->ev[round * 3 + 0], st);
     if (hp.filter && !linked) {   // linked primers: short, no shared suffix block; plain scan
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
