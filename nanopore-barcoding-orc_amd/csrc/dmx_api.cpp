@@ -139,8 +139,8 @@ int ensure_pipeline(Ctx* c) {
 hipError_t read_counters(Ctx* c, uint32_t* cnt, int* ovf) {
     hipError_t e = hipMemcpy(cnt, c->d_counters, 32 * sizeof(uint32_t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return e;
-    uint32_t sh[kShLists * kShards];
-    e = hipMemcpy(sh, c->d_shard, sizeof(sh), hipMemcpyDeviceToHost);
+    std::vector<uint32_t> sh((size_t)kShLists * kShards * kShardStride);
+    e = hipMemcpy(sh.data(), c->d_shard, sh.size() * sizeof(uint32_t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return e;
     int o = 0;
     for (int x = 0; x < kShLists; ++x) {
@@ -150,7 +150,7 @@ hipError_t read_counters(Ctx* c, uint32_t* cnt, int* ovf) {
                                          kShards);
         uint64_t t = 0;
         for (int s = 0; s < kShards; ++s) {
-            const uint32_t v = sh[x * kShards + s];
+            const uint32_t v = sh[(size_t)(x * kShards + s) * kShardStride];
             t += std::min(v, scap);
             if (v > scap) o |= cand ? 8 : 4;
         }
@@ -244,7 +244,7 @@ int dmx_open(int device, dmx_ctx** out) {
     for (auto& e : c->ev) hipEventCreate(&e);
     for (int r = 0; r < 2; ++r) hipMalloc((void**)&c->d_panel[r], sizeof(DevPanel));
     hipMalloc((void**)&c->d_counters, 32 * sizeof(uint32_t));
-    hipMalloc((void**)&c->d_shard, kShLists * kShards * sizeof(uint32_t));
+    hipMalloc((void**)&c->d_shard, kShLists * kShards * kShardStride * sizeof(uint32_t));
     *out = c;
     return DMX_OK;
 }
@@ -583,7 +583,7 @@ int dmx_exec(dmx_ctx* c) {
     hipStream_t st = c->stream;
     CK(hipEventRecord(c->ev[8], st));
     CK(hipMemsetAsync(c->d_counters, 0, 32 * sizeof(uint32_t), st));
-    CK(hipMemsetAsync(c->d_shard, 0, kShLists * kShards * sizeof(uint32_t), st));
+    CK(hipMemsetAsync(c->d_shard, 0, kShLists * kShards * kShardStride * sizeof(uint32_t), st));
     CK(hipMemsetAsync(c->d_counts, 0, c->n_counts * sizeof(unsigned long long), st));
     // A panel whose accepted matches can score <= 0 keeps one winner per orientation:
     // ReverseComplementer compares the two orientations' best scores with "no match" = 0, so
@@ -728,12 +728,13 @@ int dmx_debug_fetch(dmx_ctx* c, int what, int round, void* out, size_t cap_bytes
         case DMX_DBG_CANDS1: slot = kShCand + 2 * round + 1; base = (const char*)c->d_cand[round][1]; cap = c->cand_cap; rec = sizeof(Cand); break;
         default: return DMX_E_INVALID;
     }
-    uint32_t sh[kShards];
-    CK(hipMemcpy(sh, c->d_shard + slot * kShards, sizeof(sh), hipMemcpyDeviceToHost));
+    uint32_t sh[kShards * kShardStride];
+    CK(hipMemcpy(sh, c->d_shard + slot * kShards * kShardStride, sizeof(sh),
+                 hipMemcpyDeviceToHost));
     const size_t scap = cap / kShards;
     size_t done = 0;
     for (int s = 0; s < kShards; ++s) {
-        const size_t nb = std::min<size_t>(sh[s], scap) * rec;
+        const size_t nb = std::min<size_t>(sh[s * kShardStride], scap) * rec;
         const size_t take = out ? std::min(nb, cap_bytes > done ? cap_bytes - done : 0) : 0;
         if (take) CK(hipMemcpy((char*)out + done, base + s * scap * rec, take, hipMemcpyDeviceToHost));
         done += nb;

@@ -100,7 +100,11 @@ constexpr int kStageCap = 256;    // LDS staging of emitted records per block
 // Appendable lists are split into kShards shards, each with its own counter (a slot of
 // Ctx::d_shard) and a fixed capacity: one device-scope counter that every wave of the grid
 // appends through serialises them (measured: the window scan ran at the counter's atomic rate).
-constexpr int kShards = 16;
+#ifndef DMX_SHARDS
+#define DMX_SHARDS 16
+#endif
+constexpr int kShards = DMX_SHARDS;
+constexpr int kShardStride = 32;   // u32 words between counters: one 128-B line each
 enum ShardList { kShWin = 0, kShWin2 = 2, kShTasks = 4, kShCand = 6, kShLists = 10 };
 constexpr int kCandStageCap = 128; // per candidate list
 

@@ -44,7 +44,7 @@ struct RoundArgs {
     int32_t band;                // 1: emit candidate cells (band kernels), 0: clusters (ring)
     Cand* cand[2];               // candidate lists: [0] cost <= 3 (band 7), [1] cost 4..7 (15)
     Outcome* cand_out[2];
-    uint32_t* cand_count;        // [2][kShards]: list l, shard s at cand[l] + s * cand_scap
+    uint32_t* cand_count;        // [2][kShards] x kShardStride: list l, shard s at cand[l] + s * cand_scap
     uint32_t cand_cap;
     uint32_t cand_scap;          // per-shard capacity
     int32_t screen;              // 1: the window scan runs the index screen's surviving pairs
@@ -315,7 +315,7 @@ struct ShardMap {
             uint32_t t = 0;
             for (int k = 0; k < kShards; ++k) {
                 pre[k] = t;
-                t += min(counts[k], shard_cap);
+                t += min(counts[k * kShardStride], shard_cap);
             }
             pre[kShards] = t;
         }
@@ -457,8 +457,8 @@ __device__ __forceinline__ void emit_cands(const RoundArgs& R, const CandOut& co
     const uint32_t sh = wave_shard();
     uint32_t b0 = 0, b1 = 0;
     if ((threadIdx.x & 63u) == 0) {
-        if (tot & 0xFFFFu) b0 = atomicAdd(R.cand_count + sh, tot & 0xFFFFu);
-        if (tot >> 16) b1 = atomicAdd(R.cand_count + kShards + sh, tot >> 16);
+        if (tot & 0xFFFFu) b0 = atomicAdd(R.cand_count + sh * kShardStride, tot & 0xFFFFu);
+        if (tot >> 16) b1 = atomicAdd(R.cand_count + (kShards + sh) * kShardStride, tot >> 16);
     }
     b0 = __builtin_amdgcn_readfirstlane(b0) + (pre & 0xFFFFu);
     b1 = __builtin_amdgcn_readfirstlane(b1) + (pre >> 16);
@@ -674,11 +674,13 @@ __device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const Sink& si
     const uint32_t bsh = blockIdx.x & (uint32_t)(kShards - 1);                           \
     const CandSink sink{{Stage<Cand, kCandStageCap>{s_cand[0], &s_ccnt[0], &s_cbase[0],    \
                                                     R.cand[0] + bsh * R.cand_scap,         \
-                                                    R.cand_count + bsh, R.cand_scap,       \
+                                                    R.cand_count + bsh * kShardStride,     \
+                                                    R.cand_scap,                           \
                                                     R.flags, 8u},                          \
                          Stage<Cand, kCandStageCap>{s_cand[1], &s_ccnt[1], &s_cbase[1],    \
                                                     R.cand[1] + bsh * R.cand_scap,         \
-                                                    R.cand_count + kShards + bsh,          \
+                                                    R.cand_count +                         \
+                                                        (kShards + bsh) * kShardStride,    \
                                                     R.cand_scap, R.flags, 8u}}};
 
 // Both kernels are templated on BAND; only the stage the instantiation uses takes LDS.
@@ -694,11 +696,13 @@ __device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const Sink& si
     const uint32_t bsh = blockIdx.x & (uint32_t)(kShards - 1);                           \
     const CandSink sink{{Stage<Cand, kCandStageCap>{s_cand[0], &s_ccnt[0], &s_cbase[0],    \
                                                     R.cand[0] + bsh * R.cand_scap,         \
-                                                    R.cand_count + bsh, R.cand_scap,       \
+                                                    R.cand_count + bsh * kShardStride,     \
+                                                    R.cand_scap,                           \
                                                     R.flags, 8u},                          \
                          Stage<Cand, kCandStageCap>{s_cand[1], &s_ccnt[1], &s_cbase[1],    \
                                                     R.cand[1] + bsh * R.cand_scap,         \
-                                                    R.cand_count + kShards + bsh,          \
+                                                    R.cand_count +                         \
+                                                        (kShards + bsh) * kShardStride,    \
                                                     R.cand_scap, R.flags, 8u}}};
 
 #define DMX_CLUSTER_STAGE                                                                 \
@@ -1045,7 +1049,8 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     const uint32_t wv = threadIdx.x >> 6;   // windows staged per wave: no block barriers below
     const uint32_t wsh = wave_shard();
     const WaveStage<Window, kWaveWinCap> st{s_win[wv], &s_wcnt[wv], R.win + wsh * R.win_scap,
-                                            R.win_count + wsh, R.win_scap, R.flags, 4u};
+                                            R.win_count + wsh * kShardStride, R.win_scap,
+                                            R.flags, 4u};
 
     const bool front = P->where == kFront;
     const uint32_t hbit = (uint32_t)(L - 1);
@@ -1144,7 +1149,8 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
     ShardMap sm{s_spre, 0u};
     sm.load(R.win_count, R.win_scap);                  // (its barrier covers the above)
     const uint32_t bsh = blockIdx.x & (uint32_t)(kShards - 1);
-    const Stage<Window> st{s_w, &s_wc, &s_wb, R.win2 + bsh * R.win_scap, R.win2_count + bsh,
+    const Stage<Window> st{s_w, &s_wc, &s_wb, R.win2 + bsh * R.win_scap,
+                           R.win2_count + bsh * kShardStride,
                            R.win_scap, R.flags, 4u};
     const bool front = P->where == kFront;
     const int L = P->pre_len, kf = P->kf;
@@ -1292,7 +1298,8 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t wsh = wave_shard();
     const WaveStage<Window, kWaveWinCap> st{s_task[wv], &s_tc[wv], R.tasks + wsh * R.task_scap,
-                                            R.task_count + wsh, R.task_scap, R.flags, 4u};
+                                            R.task_count + wsh * kShardStride, R.task_scap,
+                                            R.flags, 4u};
     const Window* wl = R.win2;
     const uint32_t nwin = sm.total();
     const uint32_t total = nwin * (uint32_t)A;    // host: win_cap * A < 2^32
@@ -1477,11 +1484,12 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     const uint32_t wsh = wave_shard();
     const WaveCandSink sink{{WaveStage<Cand, kWaveCandCap>{s_wcand[wv][0], &s_wcn[wv][0],
                                                            R.cand[0] + wsh * R.cand_scap,
-                                                           R.cand_count + wsh, R.cand_scap,
+                                                           R.cand_count + wsh * kShardStride,
+                                                           R.cand_scap,
                                                            R.flags, 8u},
                              WaveStage<Cand, kWaveCandCap>{s_wcand[wv][1], &s_wcn[wv][1],
                                                            R.cand[1] + wsh * R.cand_scap,
-                                                           R.cand_count + kShards + wsh,
+                                                           R.cand_count + (kShards + wsh) * kShardStride,
                                                            R.cand_scap, R.flags, 8u}}};
     load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
     __shared__ uint32_t s_spre[kShards + 1];
@@ -1916,7 +1924,7 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
     }
     __shared__ uint32_t s_spre[kShards + 1];
     ShardMap sm{s_spre, 0u};
-    sm.load(R.cand_count + list * kShards, R.cand_scap);   // (its barrier covers the above)
+    sm.load(R.cand_count + list * kShards * kShardStride, R.cand_scap);   // (barrier: above too)
     const uint32_t total = sm.total();
     const Cand* cl = R.cand[list];
     Outcome* outs = R.cand_out[list];
@@ -2010,7 +2018,7 @@ __global__ void select_cand_kernel(RoundArgs R) {
     for (int list = 0; list < 2; ++list) {
         ShardMap sm{s_spre, 0u};
         __syncthreads();   // the previous list's map is no longer read
-        sm.load(R.cand_count + list * kShards, R.cand_scap);
+        sm.load(R.cand_count + list * kShards * kShardStride, R.cand_scap);
         const uint32_t total = sm.total();
         for (uint32_t ti = blockIdx.x * blockDim.x + threadIdx.x; ti < total;
              ti += gridDim.x * blockDim.x) {
@@ -2343,9 +2351,9 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     const uint32_t grid = (uint32_t)((R.n_items + rpb - 1) / rpb);
     R.diag = c->d_counters + 16 + 4 * round;
     R.win = c->d_win;
-    R.win_count = c->d_shard + (kShWin + round) * kShards;
+    R.win_count = c->d_shard + (kShWin + round) * kShards * kShardStride;
     R.win2 = c->d_win2;
-    R.win2_count = c->d_shard + (kShWin2 + round) * kShards;
+    R.win2_count = c->d_shard + (kShWin2 + round) * kShards * kShardStride;
     R.win_cap = (uint32_t)c->win_cap;
     R.win_scap = (uint32_t)(c->win_cap / kShards);
     const bool band = c->band_ok[round] && !c->force_ring;
@@ -2354,13 +2362,13 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         R.cand[l] = c->d_cand[round][l];
         R.cand_out[l] = c->d_cand_out[round][l];
     }
-    R.cand_count = c->d_shard + (kShCand + 2 * round) * kShards;
+    R.cand_count = c->d_shard + (kShCand + 2 * round) * kShards * kShardStride;
     R.cand_cap = (uint32_t)c->cand_cap;
     R.cand_scap = (uint32_t)(c->cand_cap / kShards);
     R.screen = (hp.filter && hp.verify && hp.screen && !linked && !c->no_screen &&
                 (uint64_t)c->win_cap * (uint64_t)hp.n < (1ull << 32)) ? 1 : 0;
     R.tasks = c->d_tasks;
-    R.task_count = c->d_shard + (kShTasks + round) * kShards;
+    R.task_count = c->d_shard + (kShTasks + round) * kShards * kShardStride;
     R.task_cap = (uint32_t)c->task_cap;
     R.task_scap = (uint32_t)(c->task_cap / kShards);
     hipEventRecord(c->ev[round * 3 + 0], st);
