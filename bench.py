@@ -32,8 +32,20 @@ sys.path.insert(0, os.path.join(ROOT, "nanopore-barcoding-orc_amd"))
 METRIC = "Mreads/s two-round SP5×SP27 demux; % HBM roofline; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CUs x 4 SIMD32 x 2.4 GHz, 32-bit lane-ops
-VALU_CEILING = 48.5e12       # measured: v_bitop3 chains, full occupancy (tools/microbench)
-FILTER_OPS_PER_COLUMN = 30.7  # PMC: SQ_INSTS_VALU x 64 / filter columns (profiles/r1_pmc_*)
+VALU_CEILING_FILE = os.path.join(ROOT, "profiles", "r2_valu_ceiling.json")
+
+
+def _valu_ceiling() -> float:
+    """Measured VALU issue ceiling (tools/microbench/run_ceiling.sh -> profiles/)."""
+    try:
+        with open(VALU_CEILING_FILE) as fh:
+            return float(json.load(fh)["bitop3_t_lane_ops_per_s"]) * 1e12
+    except (OSError, ValueError, KeyError):
+        return 50.5e12
+
+
+VALU_CEILING = _valu_ceiling()   # independent v_bitop3 chains at full occupancy
+FILTER_OPS_PER_COLUMN = 30.9  # PMC: SQ_INSTS_VALU x 64 / filter columns (profiles/r2_pmc_*)
 CHOP_OPS_PER_COLUMN = 46.47   # PMC: same for chop_kernel (profiles/r1_pmc_summary_chop_c2_10M.txt)
 
 
@@ -59,6 +71,50 @@ def pmc_traffic(workload: str, reads: int):
     if key not in d:
         return None, None
     return d[key]["bytes_per_launch"], d[key]["source"]
+
+
+# the two-round pipeline's kernels and the live stage events that time them (per round)
+KERNEL_STAGES = (("dmx::filter_kernel", "filter"), ("dmx::verify_kernel", "verify"),
+                 ("dmx::iscreen_kernel", "screen"), ("dmx::wscan_kernel<true>", "wscan"),
+                 ("band_cand<7>+band_cand<15>+select_cand", "resolve"))
+PMC_NAMES = {"filter": ["filter_kernel"], "verify": ["verify_kernel"],
+             "screen": ["iscreen_kernel"], "wscan": ["wscan_kernel<true>"],
+             "resolve": ["band_cand_kernel<7>", "band_cand_kernel<15>", "select_cand_kernel"]}
+
+
+def kernel_table(workload: str, reads: int, stage: dict, K: int, step_ms: float):
+    """Per-kernel live time (HIP events around each stage of each round) with, where a committed
+    rocprofv3 PMC table exists for this exact workload (profiles/kernel_pmc.json, written by
+    tools/kernel_table_from_pmc.py), the VALU issue rate and HBM bytes of the same launches:
+    instructions and bytes per launch are properties of the workload, the time is this run's."""
+    pmc = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "kernel_pmc.json")) as fh:
+            pmc = json.load(fh).get(f"{workload}:{reads}")
+    except (OSError, ValueError):
+        pmc = None
+    out = {}
+    for name, st in KERNEL_STAGES:
+        ms = [stage[f"{st}{r}"] / K for r in (0, 1)]
+        ent = {"ms_per_step": round(sum(ms), 3), "ms_per_round": [round(x, 3) for x in ms],
+               "share_of_step": round(sum(ms) / step_ms, 4)}
+        if pmc is not None:
+            valu = hbm = 0.0
+            for kn in PMC_NAMES[st]:
+                for launch in pmc["kernels"].get(kn, []):
+                    valu += launch["valu_insts"]
+                    hbm += launch["hbm_bytes"]
+            if sum(ms) > 0 and valu > 0:
+                rate = valu * 64 / (sum(ms) / 1e3)
+                ent["valu_lane_ops_per_s"] = rate
+                ent["valu_frac_of_ceiling"] = round(rate / VALU_CEILING, 4)
+                ent["hbm_gb_per_s"] = round(hbm / (sum(ms) / 1e3) / 1e9, 1)
+                ent["hbm_frac"] = round(hbm / (sum(ms) / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+        out[name] = ent
+    if pmc is not None:
+        out["_source"] = (pmc["source"] + "; VALU ceiling " + os.path.relpath(VALU_CEILING_FILE,
+                                                                               ROOT))
+    return out
 
 
 def cpu_baseline(workload: str, threads: int, target_s: float = 12.0):
@@ -189,8 +245,10 @@ def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, 
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": round(alg_bytes),
                      "kernel": "dmx::filter_kernel", "avg_launch_ms": round(filt_ms, 3),
-                     "note": "the bit-vector filter is VALU-bound by construction "
-                             "(DESIGN.md §5): see 'valu' for its issue-rate fraction"},
+                     "share_of_step": round(2 * filt_ms / (elapsed / K * 1e3), 4),
+                     "note": "the dominant kernel (largest share of the step, see 'kernels'); "
+                             "a bit-vector scan, VALU-bound by construction (DESIGN.md §5): "
+                             "'valu' gives its issue rate against the measured ceiling"},
         "valu": {"filter_columns_per_s": col_rate,
                  "filter_lane_ops_per_column": FILTER_OPS_PER_COLUMN,
                  "filter_lane_ops_per_s": col_rate * FILTER_OPS_PER_COLUMN,
@@ -198,8 +256,9 @@ def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, 
                  "measured_ceiling_lane_ops_per_s": VALU_CEILING,
                  "nominal_peak_lane_ops_per_s": VALU_PEAK_TOPS * 1e12,
                  "source": "ops/column = SQ_INSTS_VALU x 64 / columns of the filter launch "
-                           "(profiles/r1_pmc_summary_c2x24_2M.txt); ceiling = independent "
-                           "v_bitop3 chains at full occupancy (tools/microbench/myers_ilp.hip)"},
+                           "(profiles/r2_pmc_summary_c2x24_10M.txt); ceiling = independent "
+                           "v_bitop3 chains at full occupancy (profiles/r2_valu_ceiling.json)"},
+        "kernels": kernel_table(args.workload, args.reads, stage, K, elapsed / K * 1e3),
         "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
         "clusters_per_step": (clusters / K).tolist(),
         "filter_windows_per_step": (windows / K).tolist(),
@@ -255,6 +314,8 @@ def main():
     ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-pcie", action="store_true",
+                    help="skip the PCIe-inclusive dmx_run after the timed region")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -308,6 +369,8 @@ def main():
         ctx.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC, 0.1)
         ctx.set_mode(lib.MODE_TWO_ROUND)
     ctx.load(packed)
+    # kept for the PCIe-inclusive run after the timed region (dmx_run from host memory)
+    host_batch = packed if not linked else None
     del packed
 
     def allreduce_counts():
@@ -372,6 +435,40 @@ def main():
     else:
         out = two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s,
                              clusters, windows, windows_raw, resolved, traces)
+    pcie = None
+    if host_batch is not None and not args.no_pcie:
+        # the boundary's host-memory path: upload, both rounds, download of every result, with
+        # copies overlapped with kernels (dmx_run's double-buffered chunks); not the headline
+        ctx.sync()
+        barrier_sync()
+        t1 = time.perf_counter()
+        ctx.run(host_batch)
+        ctx.sync()
+        barrier_sync()
+        pe = time.perf_counter() - t1
+        if dist is not None:
+            import torch
+            tt = torch.tensor([pe], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            pe = float(tt.item())
+        pcie = {"value": round(args.reads * world / pe / 1e6, 4), "unit": "Mreads/s",
+                "ms": round(pe * 1e3, 3),
+                "chunk_reads": int(os.environ.get("DMX_RUN_CHUNK", 1 << 21)),
+                # 2-bit codes, the data half of the 1-bit mask, offsets, lengths
+                "h2d_bytes_per_gpu": int(host_batch.seq2b.nbytes +
+                                         min(host_batch.nmask.nbytes,
+                                             host_batch.seq2b.nbytes // 2 + 8) +
+                                         host_batch.offsets.nbytes +
+                                         host_batch.lengths.nbytes),
+                "d2h_bytes_per_gpu": int(args.reads * 40),   # dmx_result
+                "note": "dmx_run from pageable host memory (one call, inputs not resident): "
+                        "uploads, both rounds, download of every per-read result; the next "
+                        "chunk's upload and the previous chunk's download overlap each chunk's "
+                        "kernels"}
+        del host_batch
+
+    if pcie is not None:
+        out["pcie_inclusive"] = pcie
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_threads)
     if rank == 0:

@@ -266,8 +266,12 @@ void dmx_close(dmx_ctx* c) {
             if (c->d_cand[r][l]) hipFree(c->d_cand[r][l]);
             if (c->d_cand_out[r][l]) hipFree(c->d_cand_out[r][l]);
         }
+    void* alt[] = {c->alt.seq_alloc, c->alt.nmask_alloc, c->alt.offs, c->alt.lens, c->alt.res};
+    for (void* b : alt)
+        if (b) hipFree(b);
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
+    if (c->cstream) hipStreamDestroy(c->cstream);
     hipStreamDestroy(c->stream);
     delete c;
 }
@@ -548,10 +552,14 @@ int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uin
         c->d_seq = c->d_seq_alloc + kGuardWords;
         c->d_nmask = c->d_nmask_alloc + kGuardWords;
         c->cap_words = n_words;
-    } else if (c->n_words > n_words) {   // stale tail of a longer batch: keep the guard zero
-        CK(hipMemsetAsync(c->d_seq + n_words, 0, (c->n_words - n_words) * 4, c->stream));
-        CK(hipMemsetAsync(c->d_nmask + n_words, 0, (c->n_words - n_words) * 4, c->stream));
     }
+    // the mask has 1 bit per nt: only its first half (of n_words words) carries data
+    const size_t nmw = std::min(n_words, (n_words + 1) / 2 + 2);
+    if (c->d_seq_alloc && c->n_words > n_words)   // stale tail of a longer batch: guard zero
+        CK(hipMemsetAsync(c->d_seq + n_words, 0, (c->n_words - n_words) * 4, c->stream));
+    if (c->d_nmask_alloc && c->n_words > nmw)
+        CK(hipMemsetAsync(c->d_nmask + nmw, 0, (std::min(c->n_words, c->cap_words) - nmw) * 4,
+                          c->stream));
     if (!c->d_offs || c->cap_reads < n_reads) {
         if ((rc = dev_alloc(c, &c->d_offs, n_reads))) return rc;
         if ((rc = dev_alloc(c, &c->d_lens, n_reads))) return rc;
@@ -560,13 +568,14 @@ int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uin
     c->n_reads = n_reads;
     c->n_words = n_words;
     CK(hipMemcpyAsync(c->d_seq, seq2b, n_words * 4, hipMemcpyHostToDevice, c->stream));
-    CK(hipMemcpyAsync(c->d_nmask, nmask, n_words * 4, hipMemcpyHostToDevice, c->stream));
+    CK(hipMemcpyAsync(c->d_nmask, nmask, nmw * 4, hipMemcpyHostToDevice, c->stream));
     if (n_reads) {
         CK(hipMemcpyAsync(c->d_offs, offsets, n_reads * 8, hipMemcpyHostToDevice, c->stream));
         CK(hipMemcpyAsync(c->d_lens, lens, n_reads * 4, hipMemcpyHostToDevice, c->stream));
     }
     CK(hipStreamSynchronize(c->stream));
     c->executed = false;
+    c->chunked = false;
     chop_invalidate(c);
     return DMX_OK;
 }
@@ -616,6 +625,10 @@ int dmx_fetch(dmx_ctx* c, dmx_result* out) {
     if (!c || (!out && c->n_reads)) return DMX_E_INVALID;
     if (!c->executed) {
         c->err = "dmx_fetch before dmx_exec";
+        return DMX_E_STATE;
+    }
+    if (c->chunked) {
+        c->err = "dmx_fetch after a chunked dmx_run (its results went to dmx_run's out)";
         return DMX_E_STATE;
     }
     CK(hipSetDevice(c->device));
@@ -742,8 +755,198 @@ int dmx_debug_fetch(dmx_ctx* c, int what, int round, void* out, size_t cap_bytes
     return (int)std::min<size_t>(done, (size_t)1 << 30);
 }
 
+namespace {
+
+// One chunk of a chunked dmx_run: reads [lo, hi) of the caller's dmx_pack batch, rebased.
+struct Chunk {
+    size_t lo, hi, w0, words;
+    std::vector<uint64_t> offs;
+};
+
+// The buffers of the resident batch (Ctx fields) <-> the second set.
+void swap_inputs(Ctx* c) {
+    std::swap(c->d_seq_alloc, c->alt.seq_alloc);
+    std::swap(c->d_nmask_alloc, c->alt.nmask_alloc);
+    std::swap(c->d_offs, c->alt.offs);
+    std::swap(c->d_lens, c->alt.lens);
+    std::swap(c->d_res, c->alt.res);
+    std::swap(c->cap_words, c->alt.cap_words);
+    std::swap(c->n_words, c->alt.n_words);
+    c->d_seq = c->d_seq_alloc + kGuardWords;
+    c->d_nmask = c->d_nmask_alloc + kGuardWords;
+}
+
+// Upload one chunk into the current set on the copy stream (host-blocking for pageable
+// memory, while the compute stream keeps running), zeroing a longer previous chunk's tail.
+int upload_chunk(Ctx* c, const Chunk& k, const uint32_t* seq2b, const uint32_t* nmask,
+                 const uint32_t* lens) {
+    hipStream_t s = c->cstream;
+    // the nmask words of a range (1 bit per nt: half as many); the rest of the buffer stays
+    // zero (the guard)
+    const auto mask_words = [](size_t w) { return std::min(w, (w + 1) / 2 + 2); };
+    const size_t nmw = mask_words(k.words), old_nmw = mask_words(c->n_words);
+    if (c->n_words > k.words)
+        CK(hipMemsetAsync(c->d_seq + k.words, 0, (c->n_words - k.words) * 4, s));
+    if (old_nmw > nmw) CK(hipMemsetAsync(c->d_nmask + nmw, 0, (old_nmw - nmw) * 4, s));
+    CK(hipMemcpyAsync(c->d_seq, seq2b + k.w0, k.words * 4, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(c->d_nmask, nmask + k.w0 / 2, nmw * 4, hipMemcpyHostToDevice, s));
+    const size_t n = k.hi - k.lo;
+    CK(hipMemcpyAsync(c->d_offs, k.offs.data(), n * 8, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(c->d_lens, lens + k.lo, n * 4, hipMemcpyHostToDevice, s));
+    CK(hipStreamSynchronize(s));
+    c->n_words = k.words;
+    return DMX_OK;
+}
+
+int alloc_set(Ctx* c, size_t words, size_t reads) {
+    int rc;
+    const size_t total = words + 2 * kGuardWords;
+    if ((rc = dev_alloc(c, &c->d_seq_alloc, total))) return rc;
+    if ((rc = dev_alloc(c, &c->d_nmask_alloc, total))) return rc;
+    CK(hipMemsetAsync(c->d_seq_alloc, 0, total * 4, c->stream));
+    CK(hipMemsetAsync(c->d_nmask_alloc, 0, total * 4, c->stream));
+    if ((rc = dev_alloc(c, &c->d_offs, reads))) return rc;
+    if ((rc = dev_alloc(c, &c->d_lens, reads))) return rc;
+    if ((rc = dev_alloc(c, &c->d_res, reads))) return rc;
+    c->d_seq = c->d_seq_alloc + kGuardWords;
+    c->d_nmask = c->d_nmask_alloc + kGuardWords;
+    c->cap_words = words;
+    c->n_words = 0;
+    CK(hipStreamSynchronize(c->stream));
+    return DMX_OK;
+}
+
+// dmx_run of a batch larger than one chunk: chunks of `per` reads alternate between two input
+// and result sets.  While chunk k's kernels run on the compute stream, the host uploads chunk
+// k+1 and downloads chunk k-1's results on the copy stream; per-bin counts are summed on the
+// host and left in d_counts for dmx_counts / dmx_allreduce_counts.  The batch must come from
+// dmx_pack (offsets on kPackAlign boundaries after DMX_PACK_PAD).
+int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
+                const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out,
+                size_t per) {
+    std::vector<Chunk> ch;
+    size_t maxw = 0, maxn = 0;
+    for (size_t lo = 0; lo < n_reads; lo += per) {
+        Chunk k;
+        k.lo = lo;
+        k.hi = std::min(n_reads, lo + per);
+        if (offsets[lo] < (uint64_t)DMX_PACK_PAD || offsets[lo] % kPackAlign) {
+            c->err = "dmx_run: offsets must come from dmx_pack";
+            return DMX_E_INVALID;
+        }
+        const uint64_t g0 = offsets[lo] - DMX_PACK_PAD;   // a 32-nt (nmask word) boundary
+        k.offs.resize(k.hi - lo);
+        uint64_t end = 0;
+        for (size_t r = lo; r < k.hi; ++r) {
+            k.offs[r - lo] = offsets[r] - g0;
+            end = std::max<uint64_t>(end, k.offs[r - lo] + lens[r]);
+        }
+        k.w0 = (size_t)(g0 / 16);
+        if (k.w0 >= n_words) {
+            c->err = "dmx_run: offsets beyond the packed buffer";
+            return DMX_E_INVALID;
+        }
+        k.words = std::min(n_words - k.w0, (size_t)((end + DMX_PACK_PAD + 31) / 32 * 2 + 4));
+        maxw = std::max(maxw, k.words);
+        maxn = std::max(maxn, k.hi - lo);
+        ch.push_back(std::move(k));
+    }
+    CK(hipSetDevice(c->device));
+    if (!c->cstream) CK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    int rc;
+    // both sets sized for the largest chunk (the resident set's read capacity is cap_reads,
+    // shared with the pipeline buffers; the second set's is alt.cap_reads)
+    if (c->cap_words < maxw || c->cap_reads < maxn || !c->d_offs || !c->d_res) {
+        if ((rc = alloc_set(c, maxw, maxn))) return rc;
+        c->cap_reads = maxn;
+    }
+    if (c->alt.cap_words < maxw || c->alt.cap_reads < maxn || !c->alt.offs || !c->alt.res) {
+        swap_inputs(c);
+        rc = alloc_set(c, maxw, maxn);
+        swap_inputs(c);
+        if (rc) return rc;
+        c->alt.cap_reads = maxn;
+    }
+    c->n_reads = maxn;
+    chop_invalidate(c);
+    c->chunked = false;
+    std::vector<uint64_t> total, part;
+    if ((rc = upload_chunk(c, ch[0], seq2b, nmask, lens))) return rc;
+    for (size_t i = 0; i < ch.size(); ++i) {
+        const size_t n = ch[i].hi - ch[i].lo;
+        c->n_reads = n;
+        int attempt = 0;
+        for (;; ++attempt) {
+            if ((rc = dmx_exec(c))) return rc;
+            // meanwhile: the next chunk into the other set, the previous chunk's results out
+            if (attempt == 0) {
+                swap_inputs(c);
+                if (i + 1 < ch.size() &&
+                    (rc = upload_chunk(c, ch[i + 1], seq2b, nmask, lens)))
+                    return rc;
+                if (i > 0) {
+                    const size_t pn = ch[i - 1].hi - ch[i - 1].lo;
+                    CK(hipMemcpyAsync(out + ch[i - 1].lo, c->d_res, pn * sizeof(dmx_result),
+                                      hipMemcpyDeviceToHost, c->cstream));
+                    CK(hipStreamSynchronize(c->cstream));
+                }
+                swap_inputs(c);
+            }
+            uint64_t cl[8];
+            int flags = 0;
+            float ms[7];
+            if ((rc = dmx_stats(c, ms, 7, cl, 8, &flags))) return rc;
+            if (flags & 2) {
+                c->err = "internal: traceback left the exact window (please report)";
+                return DMX_E_STATE;
+            }
+            if (!(flags & 13)) break;
+            if (attempt >= 7) {
+                c->err = "candidate cluster buffer overflow";
+                return DMX_E_NOMEM;
+            }
+            if ((flags & 1) && (rc = grow_clusters(c))) return rc;
+            if ((flags & 4) && (rc = grow_windows(c))) return rc;
+            if ((flags & 8) && (rc = grow_cands(c))) return rc;
+        }
+        part.assign(c->n_counts, 0);
+        CK(hipMemcpy(part.data(), c->d_counts, c->n_counts * 8, hipMemcpyDeviceToHost));
+        if (total.size() != part.size()) total.assign(part.size(), 0);
+        for (size_t x = 0; x < part.size(); ++x) total[x] += part[x];
+        swap_inputs(c);   // the next chunk (uploaded above) becomes the resident batch
+    }
+    // the last chunk's results sit in the other set now
+    swap_inputs(c);
+    {
+        const Chunk& k = ch.back();
+        CK(hipMemcpy(out + k.lo, c->d_res, (k.hi - k.lo) * sizeof(dmx_result),
+                     hipMemcpyDeviceToHost));
+    }
+    CK(hipMemcpy(c->d_counts, total.data(), total.size() * 8, hipMemcpyHostToDevice));
+    c->chunked = true;
+    return DMX_OK;
+}
+
+}  // namespace
+
 int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
             const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out) {
+    if (!c || (n_reads && (!seq2b || !nmask || !offsets || !lens || !out))) return DMX_E_INVALID;
+    size_t per = (size_t)1 << 21;   // reads per chunk of an overlapped run
+    if (const char* e = std::getenv("DMX_RUN_CHUNK")) per = (size_t)std::strtoull(e, nullptr, 10);
+    if (per > 0 && n_reads > per + per / 2) {
+        if (!c->panel[0].set || (c->mode != DMX_MODE_SINGLE && !c->panel[1].set)) {
+            c->err = "panels not set for this mode";
+            return DMX_E_STATE;
+        }
+        for (size_t r = 0; r < n_reads; ++r)
+            if (offsets[r] < 16 || (offsets[r] + lens[r] + 64) > (uint64_t)n_words * 16 ||
+                lens[r] >= (1u << 30)) {
+                c->err = "read offsets/lengths do not fit the packed buffer (use dmx_pack)";
+                return DMX_E_INVALID;
+            }
+        return run_chunked(c, seq2b, nmask, offsets, lens, n_words, n_reads, out, per);
+    }
     int rc = dmx_load(c, seq2b, nmask, offsets, lens, n_words, n_reads);
     if (rc) return rc;
     for (int attempt = 0; attempt < 8; ++attempt) {

@@ -46,6 +46,20 @@ struct Ctx {
     uint64_t* d_offs = nullptr;
     uint32_t* d_lens = nullptr;
 
+    // dmx_run of a large batch: chunks alternate between the buffers above and this second
+    // set (inputs + results), so the next chunk's upload and the previous chunk's download
+    // overlap the current chunk's kernels (dmx_api.cpp run_chunked)
+    struct InSet {
+        uint32_t* seq_alloc = nullptr;
+        uint32_t* nmask_alloc = nullptr;
+        uint64_t* offs = nullptr;
+        uint32_t* lens = nullptr;
+        dmx_result* res = nullptr;
+        size_t cap_words = 0, cap_reads = 0, n_words = 0;
+    } alt;
+    hipStream_t cstream = nullptr;      // copies of chunked runs
+    bool chunked = false;               // the last dmx_run was chunked: dmx_fetch is refused
+
     // pipeline state
     dmx_result* d_res = nullptr;
     unsigned long long* d_winner[2] = {nullptr, nullptr};
