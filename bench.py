@@ -61,7 +61,8 @@ def filter_algorithmic_bytes(lengths: np.ndarray, n_windows: int) -> float:
 def pmc_traffic(workload: str, reads: int):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary (FETCH_SIZE and
     WRITE_SIZE passes, corrected per MI355X_MICROARCH.md), if one exists for this workload."""
-    path = os.path.join(ROOT, "profiles", "filter_pmc_traffic.json")
+    path = os.environ.get("DMX_FILTER_TRAFFIC") or os.path.join(ROOT, "profiles",
+                                                                "filter_pmc_traffic.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
@@ -89,7 +90,8 @@ def kernel_table(workload: str, reads: int, stage: dict, K: int, step_ms: float)
     instructions and bytes per launch are properties of the workload, the time is this run's."""
     pmc = None
     try:
-        with open(os.path.join(ROOT, "profiles", "kernel_pmc.json")) as fh:
+        with open(os.environ.get("DMX_KERNEL_PMC") or
+                  os.path.join(ROOT, "profiles", "kernel_pmc.json")) as fh:
             pmc = json.load(fh).get(f"{workload}:{reads}")
     except (OSError, ValueError):
         pmc = None
