@@ -425,11 +425,16 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
                 !(c->no_filter);
     if (hp.filter) {
         dp.filter_len = flen;
+        // the block's rows in the top flen bits (last row = bit 31); the rows below match
+        // every code, N included, so they stay at cost 0 like row 0 (filter_kernel)
+        const int pad = 32 - flen;
+        for (int code = 0; code < 8; ++code)
+            dp.filter_peq[code] = pad > 0 ? (1u << pad) - 1u : 0u;
         const char* blk = seqs[0] + lens[0] - flen;
         for (int i = 0; i < flen; ++i) {
             const uint8_t mask = iupac_mask(blk[i]);
             for (int code = 0; code < 4; ++code)
-                if (mask & (1u << code)) dp.filter_peq[code] |= 1u << i;
+                if (mask & (1u << code)) dp.filter_peq[code] |= 1u << (pad + i);
         }
         int kf = -1, mk = 0;
         for (int L = 0; L < 72; ++L) dp.pf[L] = -1;

@@ -788,11 +788,36 @@ __device__ __forceinline__ uint32_t align32(uint32_t hi, uint32_t lo, uint32_t r
 
 struct SegState {
     uint32_t pv, mv;
-    int b;
+    int e;          // last-row cost b minus (kf_far + 1): negative exactly where b <= kf_far
     bool have;
     uint32_t w1, w2;
     int wb;
 };
+
+// Myers step of the filter block, stored in the TOP filter_len bits of the word (the rows
+// below are all-match padding that stays at cost 0, so they act as row 0): the last row is bit
+// 31, and the carries of the two horizontal shifts are its +1 / -1 (one v_add_co each, whose
+// carry the cost update consumes) instead of two bit-field extracts.
+__device__ __forceinline__ void myers_step_top(uint32_t eq, uint32_t& pv, uint32_t& mv, int& e) {
+    const uint32_t xv = eq | mv;
+    const uint32_t xh = (((eq & pv) + pv) ^ pv) | eq;
+    const uint32_t ph = mv | ~(xh | pv);
+    const uint32_t mh = pv & xh;
+    uint32_t cp, cm;
+    const uint32_t ph2 = __builtin_addc(ph, ph, 0u, &cp);
+    const uint32_t mh2 = __builtin_addc(mh, mh, 0u, &cm);
+    e += (int)cp - (int)cm;
+    pv = mh2 | ~(xv | ph2);
+    mv = ph2 & xv;
+}
+
+// 8 two-bit codes (16 bits) -> 8 nibbles holding code * 4 (an LDS byte offset into a u32
+// table): one v_perm spreads the two bytes, two shift-or-mask steps the codes.
+__device__ __forceinline__ uint32_t spread_codes(uint32_t codes, uint32_t sel) {
+    uint32_t x = __builtin_amdgcn_perm(0u, codes, sel);   // bytes -> bytes 0 and 2
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;                      // 4-bit halves -> bytes
+    return ((x << 2) | (x << 4)) & 0xCCCCCCCCu;             // 2-bit codes -> nibbles, * 4
+}
 
 // One 16-position chunk (view positions p0 .. p0+15) of a filter segment.  All 16 steps always
 // run (lanes of a wave stay in lockstep); columns past the segment end (q >= cnt) cannot hit.
@@ -804,38 +829,48 @@ struct SegState {
 template <bool CAREFUL>
 __device__ __forceinline__ void filter_chunk(uint32_t codes, uint32_t nb, uint32_t p0, int cnt,
                                              SegState& S, const uint32_t* s_fpeq,
-                                             const int8_t* s_thr, uint32_t hbit, int kf,
-                                             int kf_far, uint32_t gap, uint32_t hit_from,
+                                             const int8_t* s_thr, int kf_far, uint32_t gap,
+                                             uint32_t hit_from,
                                              const WaveStage<Window, kWaveWinCap>& st,
                                              uint32_t item, int o,
                                              const TaskView& tv) {
     uint32_t eq[16];
+    if (__builtin_amdgcn_ballot_w64(nb != 0u) == 0) {   // ACGT only (wave-uniform): byte offsets
+        const uint32_t lo = spread_codes(codes, 0x0c010c00u);
+        const uint32_t hi = spread_codes(codes, 0x0c030c02u);
+        const char* base = reinterpret_cast<const char*>(s_fpeq);
 #pragma unroll
-    for (int q = 0; q < 16; ++q)
-        eq[q] = s_fpeq[((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)];
+        for (int q = 0; q < 16; ++q)
+            eq[q] = *reinterpret_cast<const uint32_t*>(
+                base + __builtin_amdgcn_ubfe(q < 8 ? lo : hi, 4 * (q & 7), 4));
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            eq[q] = s_fpeq[((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)];
+    }
     uint4 tw = {0u, 0u, 0u, 0u};
     if constexpr (CAREFUL)   // 16 per-position thresholds (s_thr: 16-byte aligned rows)
         tw = *reinterpret_cast<const uint4*>(s_thr + (hit_from == 0 ? p0 : 240u));
-    uint32_t hits = 0;
-    int cb = 127;
+    uint32_t hits = 0;       // column q's hit bit is shifted in from the bottom: ends at 15 - q
+    int cm = 1 << 20;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        {
-            myers_step32(eq[q], S.pv, S.mv, S.b, hbit);
-            int t = kf_far;
-            if constexpr (CAREFUL) {
-                const uint32_t w = q < 4 ? tw.x : q < 8 ? tw.y : q < 12 ? tw.z : tw.w;
-                t = __builtin_amdgcn_sbfe((int)w, 8 * (q & 3), 8) |
-                    ((int)(p0 + (uint32_t)q - hit_from) >> 31);      // -1 in the warm-up
-            }
-            hits |= S.b <= t ? (1u << q) : 0u;
-            cb = min(cb, S.b);
+        myers_step_top(eq[q], S.pv, S.mv, S.e);
+        int sgn = S.e;       // < 0 exactly at a hit column
+        if constexpr (CAREFUL) {
+            const uint32_t w = q < 4 ? tw.x : q < 8 ? tw.y : q < 12 ? tw.z : tw.w;
+            const int t = __builtin_amdgcn_sbfe((int)w, 8 * (q & 3), 8) |
+                          ((int)(p0 + (uint32_t)q - hit_from) >> 31);   // -1 in the warm-up
+            sgn = S.e + kf_far - t;
         }
+        hits = __builtin_amdgcn_alignbit(hits, (uint32_t)sgn, 31);
+        cm = min(cm, S.e);
     }
-    hits &= cnt >= 16 ? 0xFFFFu : (cnt > 0 ? (1u << cnt) - 1u : 0u);
+    hits &= cnt >= 16 ? 0xFFFFu : (cnt > 0 ? (0xFFFFu << (16 - cnt)) & 0xFFFFu : 0u);
+    const int cb = cm + kf_far + 1;   // the chunk's minimum b: a lower bound of every hit's b
     while (hits) {
-        const int q = __ffs(hits) - 1;
-        hits &= hits - 1;
+        const int q = (int)__clz(hits) - 16;
+        hits &= ~(0x80000000u >> __clz(hits));
         const uint32_t j = p0 + (uint32_t)q + 1;
         if (S.have && j - S.w2 <= gap) {
             S.w2 = j;
@@ -905,8 +940,7 @@ __device__ __forceinline__ void seg_extract(SegBlocks& B, uint32_t vc[4], uint32
 __device__ __forceinline__ void filter_segment(const RoundArgs& R, const TaskView& tv,
                                                uint32_t P0, uint32_t P1, SegState& S,
                                                const uint32_t* s_fpeq, const int8_t* s_thr,
-                                               uint32_t hbit, int kf, int kf_far, uint32_t gap,
-                                               uint32_t hit_from,
+                                               int kf_far, uint32_t gap, uint32_t hit_from,
                                                const WaveStage<Window, kWaveWinCap>& st,
                                                uint32_t item, int o) {
     const bool rev = tv.strand != 0;
@@ -943,11 +977,11 @@ __device__ __forceinline__ void filter_segment(const RoundArgs& R, const TaskVie
             const uint32_t pc = p0 + 16u * (uint32_t)c;
             const int cnt = (int)P1 - (int)pc;
             if (careful)
-                filter_chunk<true>(vc[0], vn[0], pc, cnt, S, s_fpeq, s_thr, hbit, kf, kf_far, gap,
+                filter_chunk<true>(vc[0], vn[0], pc, cnt, S, s_fpeq, s_thr, kf_far, gap,
                                    hit_from, st, item, o, tv);
             else
-                filter_chunk<false>(vc[0], vn[0], pc, cnt, S, s_fpeq, s_thr, hbit, kf, kf_far,
-                                    gap, hit_from, st, item, o, tv);
+                filter_chunk<false>(vc[0], vn[0], pc, cnt, S, s_fpeq, s_thr, kf_far, gap,
+                                    hit_from, st, item, o, tv);
             vc[0] = vc[1];
             vc[1] = vc[2];
             vc[2] = vc[3];
@@ -1053,9 +1087,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                                             R.flags, 4u};
 
     const bool front = P->where == kFront;
-    const uint32_t hbit = (uint32_t)(L - 1);
     const int kf_far = min(kf, (int)s_pf[71]);
     const uint32_t gap = (uint32_t)P->max_mk;
+    // the block's rows sit in the top L bits (filter_peq, host side): rows start at cost i
+    const uint32_t pv_rows = L >= 32 ? ~0u : ~0u << (32 - L);
 
     // With both orientations of every item (--rc) the two strand groups have equal segment
     // counts; then the block's two halves walk them in step (half 0: strand-0 segment tt, half
@@ -1098,14 +1133,13 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             const uint32_t P1 = min(tv.len, seg0 + SEG);
             SegState S;
             const bool fresh = k == 0;                 // view start: the panel's own column 0
-            S.pv = (fresh && front) ? 0u : ~0u;
+            S.pv = (fresh && front) ? 0u : pv_rows;
             S.mv = 0u;
-            S.b = (fresh && front) ? 0 : L;
+            S.e = ((fresh && front) ? 0 : L) - (kf_far + 1);
             S.have = false;
             S.w1 = S.w2 = 0;
             S.wb = 255;
-            filter_segment(R, tv, P0, P1, S, s_fpeq, s_thr, hbit, kf, kf_far, gap, seg0, st, item,
-                           o);
+            filter_segment(R, tv, P0, P1, S, s_fpeq, s_thr, kf_far, gap, seg0, st, item, o);
             const uint32_t len = tv.len;
             if (!front && P1 == len) {
                 // 3' panels: the last column (adapter prefix off the read end) is always checked
