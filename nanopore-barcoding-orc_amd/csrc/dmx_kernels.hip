@@ -105,6 +105,7 @@ __device__ __forceinline__ uint32_t slot_of(const RoundArgs& R, uint32_t item, i
 // consecutive adapters; windows sharing a wave read other codes' rows, shifted by 24 banks
 // (a power-of-two stride put every code's copy of adapter a in the same bank).
 constexpr int kPeqStride = kMaxAdapters + 24;
+constexpr int kIpeqStride = 9;   // index screen: words per adapter (4 codes + bank padding)
 
 __device__ __forceinline__ void load_panel_lds(const DevPanel* P, uint64_t* s_peq, int8_t* s_acc,
                                                int8_t* s_pacc) {
@@ -1310,18 +1311,23 @@ __device__ __forceinline__ Window make_task(Window w, uint32_t jlo, uint32_t jhi
 }
 
 __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
-    __shared__ uint32_t s_ipeq[8 * kPeqStride];     // code-major: [c][a], bit r = row pre_len + r
+    // adapter-major [a][kIpeqStride], codes 0..3: I_a's rows in the top l_a bits (row pre_len + r
+    // at bit 32 - l_a + r), all-match padding below (myers_step_top); 9 words per adapter keep
+    // the 24 lanes of one window (same code) on distinct banks
+    __shared__ uint32_t s_ipeq[kMaxAdapters * kIpeqStride];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
     __shared__ Window s_task[kScanBlock / 64][kWaveWinCap];   // per-wave task staging
     __shared__ uint32_t s_tc[kScanBlock / 64], s_nend;
     const DevPanel* P = R.panel;
     const int A = P->n_adapters;
     const int pl = P->pre_len, sl = P->filter_len, kf = P->kf;
-    for (int x = threadIdx.x; x < 8 * A; x += blockDim.x) {
-        const int c = x / A, a = x % A;
+    for (int x = threadIdx.x; x < 4 * A; x += blockDim.x) {
+        const int c = x & 3, a = x >> 2;
         const int l = (int)P->ad[a].m - pl - sl;
-        const uint64_t v = c < 4 ? (P->ad[a].peq[c] >> pl) : 0ull;
-        s_ipeq[c * kPeqStride + a] = (uint32_t)(l >= 32 ? v : (v & ((1ull << l) - 1ull)));
+        const uint64_t v = P->ad[a].peq[c] >> pl;
+        s_ipeq[a * kIpeqStride + c] =
+            l >= 32 ? (uint32_t)v
+                    : ((uint32_t)(v & ((1ull << l) - 1ull)) << (32 - l)) | ((1u << (32 - l)) - 1u);
     }
     for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
     if (threadIdx.x < kScanBlock / 64) s_tc[threadIdx.x] = 0;
@@ -1392,9 +1398,9 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
                 const int nch = (xe - x1 + 15) >> 4;
                 const int jb = xe - 16 * nch;
                 const int xrh = min(xr_hi, len);
-                const uint32_t* ip = s_ipeq + a;
-                const uint32_t hbit = (uint32_t)(l - 1);
-                uint32_t pv = ~0u, mv = 0u;
+                const char* ip = reinterpret_cast<const char*>(s_ipeq + a * kIpeqStride);
+                const uint32_t rows_m = l >= 32 ? ~0u : ~0u << (32 - l);   // I_a's rows
+                uint32_t pv = rows_m, mv = 0u;
                 int d = l;
                 TaskView tv;
                 tv.read = 0;
@@ -1421,26 +1427,41 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
                     const int tk = max(inR ? thr : -1, inE ? thr_e : -1);
                     const int qlo = min(inR ? xr_lo : (1 << 30), inE ? xe_lo : (1 << 30)) - p0 - 1;
                     uint32_t eq[16];
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) eq[q] = ip[((codes >> (2 * q)) & 3u) * kPeqStride];
-                    if (__builtin_amdgcn_ballot_w64(nb != 0u)) {   // a non-ACGT byte: no match
+                    {
+                        const uint32_t lo = spread_codes(codes, 0x0c010c00u);
+                        const uint32_t hi = spread_codes(codes, 0x0c030c02u);
 #pragma unroll
                         for (int q = 0; q < 16; ++q)
-                            eq[q] &= ~(uint32_t)__builtin_amdgcn_sbfe((int)nb, q, 1);
+                            eq[q] = *reinterpret_cast<const uint32_t*>(
+                                ip + __builtin_amdgcn_ubfe(q < 8 ? lo : hi, 4 * (q & 7), 4));
+                    }
+                    if (__builtin_amdgcn_ballot_w64(nb != 0u)) {   // non-ACGT: no match in I_a
+#pragma unroll
+                        for (int q = 0; q < 16; ++q)
+                            eq[q] &= ~((uint32_t)__builtin_amdgcn_sbfe((int)nb, q, 1) & rows_m);
                     }
                     int cm = 127;
+                    if (__builtin_amdgcn_ballot_w64(qlo > 0) == 0) {   // every column counts
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) {
-                        myers_step32(eq[q], pv, mv, d, hbit);
-                        cm = min(cm, q >= qlo ? d : 127);
+                        for (int q = 0; q < 16; ++q) {
+                            myers_step_top(eq[q], pv, mv, d);
+                            cm = min(cm, d);
+                        }
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 16; ++q) {
+                            myers_step_top(eq[q], pv, mv, d);
+                            cm = min(cm, q >= qlo ? d : 127);
+                        }
                     }
                     pass = cm <= tk;
                     by_end = !inR;
                 }
                 if (lastc && !pass) {   // partial I_a at the read end: cells (pl + r, len)
                     int dd = 0;
+                    const int sh = 32 - l;   // row pre_len + r at bit sh + r - 1
                     for (int r = 1; r < l && !pass; ++r) {
-                        dd += (int)((pv >> (r - 1)) & 1u) - (int)((mv >> (r - 1)) & 1u);
+                        dd += (int)((pv >> (sh + r - 1)) & 1u) - (int)((mv >> (sh + r - 1)) & 1u);
                         pass = dPn + dd <= (int)s_acc[72 * a + pl + r];
                     }
                 }
