@@ -487,7 +487,12 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
     c->panel[round] = hp;
     c->ring_small[round] = hp.ring_small;
     c->band_ok[round] = true;
-    for (int a = 0; a < n; ++a) c->band_ok[round] &= hp.ad[a].kk <= 7;
+    int kkmax = 0;
+    for (int a = 0; a < n; ++a) {
+        c->band_ok[round] &= hp.ad[a].kk <= 7;
+        kkmax = std::max(kkmax, (int)hp.ad[a].kk);
+    }
+    c->band_wide[round] = kkmax > 5;   // list 1 (costs 4..kk): 11 diagonals cover kk <= 5
     for (int a = 0; a < n; ++a) dp.ad[a] = hp.ad[a];
     CK(hipSetDevice(c->device));
     CK(hipMemcpy(c->d_panel[round], &dp, sizeof(dp), hipMemcpyHostToDevice));

@@ -67,6 +67,7 @@ struct Ctx {
     int32_t* d_lb[2] = {nullptr, nullptr};
     bool ring_small[2] = {true, true};
     bool band_ok[2] = {true, true};
+    bool band_wide[2] = {true, true};      // some adapter has kk 6..7: list 1 needs 15 diagonals
     bool orient_slot[2] = {false, false};   // per round: one winner slot per (item, orientation)   // every adapter has kk <= 7: banded resolve
     bool force_ring = false;          // DMX_RESOLVE=ring (A/B testing)
     size_t slot_cap = 0;

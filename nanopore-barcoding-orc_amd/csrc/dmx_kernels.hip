@@ -2450,7 +2450,10 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     hipEventRecord(c->ev[round * 3 + 1], st);
     if (band) {
         hipLaunchKernelGGL(band_cand_kernel<7>, dim3(256 * 8), dim3(256), 0, st, R, 0);
-        hipLaunchKernelGGL(band_cand_kernel<15>, dim3(256 * 4), dim3(256), 0, st, R, 1);
+        if (c->band_wide[round])
+            hipLaunchKernelGGL(band_cand_kernel<15>, dim3(256 * 4), dim3(256), 0, st, R, 1);
+        else   // every cost in list 1 is <= 5: a band of 2 * 5 + 1 diagonals is exact
+            hipLaunchKernelGGL(band_cand_kernel<11>, dim3(256 * 4), dim3(256), 0, st, R, 1);
         hipLaunchKernelGGL(select_cand_kernel, dim3(1024), dim3(256), 0, st, R);
         hipEventRecord(c->ev[round * 3 + 2], st);
         return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
