@@ -73,8 +73,43 @@ def _unsupported(msg: str):
     raise SystemExit(2)
 
 
-def run(argv=None) -> int:
+_T_IMPORT = time.perf_counter()
+
+
+def _since_exec() -> float:
+    """Seconds since this process started (Linux /proc, 10 ms resolution; -1 elsewhere)."""
+    try:
+        with open("/proc/self/stat") as fh:
+            start = int(fh.read().rsplit(")", 1)[1].split()[19])
+        with open("/proc/uptime") as fh:
+            up = float(fh.read().split()[0])
+        return up - start / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, IndexError):
+        return -1.0
+
+
+_EXEC_TO_IMPORT = _since_exec()
+
+
+def _phase(name: str, marks: list):
+    """DMX_PROFILE_CLI=1: phase timestamps of this call (seconds since the module import)."""
+    if marks is not None:
+        marks.append((name, time.perf_counter() - _T_IMPORT))
+
+
+_CTX_CACHE: dict = {}   # devices -> contexts kept by the resident server (dmx/daemon.py)
+
+
+def close_cached_contexts():
+    for ctxs in _CTX_CACHE.values():
+        for c in ctxs:
+            c.close()
+    _CTX_CACHE.clear()
+
+
+def run(argv=None, keep_contexts: bool = False) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
+    marks = [] if os.environ.get("DMX_PROFILE_CLI") == "1" else None
     args = build_parser().parse_args(argv)
     if args.action != "trim":
         _unsupported("only --action=trim is implemented")
@@ -96,10 +131,19 @@ def run(argv=None) -> int:
     if linked and args.rc:
         _unsupported("--rc with linked adapters is not implemented")
 
+    _phase("args", marks)
     devices = _devices(args)
-    ctxs = lib.open_group(devices)
+    if keep_contexts:   # the server's contexts (panels and mode are set again below)
+        key = tuple(devices)
+        if key not in _CTX_CACHE:
+            _CTX_CACHE[key] = lib.open_group(devices)
+        ctxs = _CTX_CACHE[key]
+    else:
+        ctxs = lib.open_group(devices)
+    _phase("open", marks)
     for ctx in ctxs:
         _configure(ctx, ads, linked, args)
+    _phase("panel", marks)
     level = 1 if args.zlevel1 else args.compression_level
 
     demux = "{name}" in args.output
@@ -121,20 +165,34 @@ def run(argv=None) -> int:
     a1 = len(ads) if linked else 0
     totals = np.zeros((len(ads) + 1, a1 + 1), dtype=np.int64)
     sink = nio.Sink(paths, fasta_out, level, threads=args.cores)
+    _phase("sink", marks)
+    tw = [0.0, 0.0, 0.0]   # read wait, GPU, plan + write enqueue
     try:
         with nio.Reader(args.input, args.batch_mb << 20, threads=args.cores) as reader:
+            _phase("reader", marks)
+            t = time.perf_counter()
             for batch in reader:
+                tw[0] += time.perf_counter() - t
                 try:
                     if len(batch):
+                        t = time.perf_counter()
                         res, cnt = lib.run_batch(ctxs, batch.packed)
+                        tw[1] += time.perf_counter() - t
+                        t = time.perf_counter()
                         totals += lib.bin_totals(cnt, len(ads), len(ads) if linked else 0)
                         plan = _plan(res, ads, linked, demux, unmatched_to, batch.lens, stats,
                                      batch.packed)
                         sink.write(batch, *plan)
+                        tw[2] += time.perf_counter() - t
                 finally:
                     batch.free()
+                t = time.perf_counter()
+        _phase("loop", marks)
     finally:
         sink.close()
+    _phase("drain", marks)
+    if marks is not None:
+        marks.extend([("read_wait", tw[0]), ("gpu", tw[1]), ("plan_write", tw[2])])
     # per-adapter totals: the devices' bin counts (summed over GPUs by RCCL) must agree with the
     # per-read results the outputs were written from
     dev = np.diagonal(totals[1:, 1:]) if linked else totals[1:, 0]
@@ -149,8 +207,13 @@ def run(argv=None) -> int:
         print(f"Command line parameters: {' '.join(argv)}")
         print(f"Finished in {time.perf_counter() - t0:.3f} s on {len(ctxs)} GPU(s)\n")
         stats.summary(error_rate=args.error_rate)
-    for ctx in ctxs:
-        ctx.close()
+    if not keep_contexts:
+        for ctx in ctxs:
+            ctx.close()
+    _phase("close", marks)
+    if marks is not None:
+        print("dmx cli phases: " + " ".join(f"{k}={v:.3f}" for k, v in marks) +
+              f" exec_to_import={_EXEC_TO_IMPORT:.2f}", file=sys.stderr)
     return 0
 
 

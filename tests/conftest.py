@@ -8,6 +8,8 @@ PKG = os.path.join(ROOT, "nanopore-barcoding-orc_amd")
 for p in (ROOT, PKG, os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
+# drop-in calls run in their own process unless a test asks for the resident server
+os.environ.setdefault("DMX_DAEMON", "0")
 
 
 def pytest_configure(config):

@@ -16,7 +16,10 @@ from helpers import (CLI, LOOP, amplicon_reads, oracle_linked, oracle_round, ran
 pytestmark = pytest.mark.gpu
 
 
-def test_02_cutadapt_loop_dropin(tmp_path):
+@pytest.mark.parametrize("server", ["0", "1"])
+def test_02_cutadapt_loop_dropin(tmp_path, server):
+    """The unchanged script's 13 calls, each in its own process (server "0") or through the
+    resident server bin/cutadapt starts (dmx/daemon.py, "1"): identical files either way."""
     d = synth.generate("c2", n=3000, seed=12)
     seqs = synth.to_strings(d)
     rng = np.random.default_rng(3)
@@ -30,7 +33,8 @@ def test_02_cutadapt_loop_dropin(tmp_path):
     out = tmp_path / "demuxed"
     (out / "SP5").mkdir(parents=True)
     (out / "SP27").mkdir()
-    env = dict(os.environ)
+    env = dict(os.environ, DMX_DAEMON=server, DMX_DAEMON_IDLE="5",
+               DMX_DAEMON_SOCK=str(tmp_path / "dmx.sock"))
     # round 1 (02_cutadapt_loop.sh:64-72)
     subprocess.run([CLI, "--action=trim", "-e", "0.1", "-j", "4", "--rc",
                     "-g", f"file:{panel.SP5_FASTA}", "-o", f"{out}/SP5/{{name}}_{ds}.fastq.gz",

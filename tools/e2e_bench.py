@@ -149,23 +149,39 @@ def main():
         os.makedirs(f"{out}/SP27", exist_ok=True)
         cli = os.path.join(PKG, "bin", "cutadapt")
         j = str(a.threads)
+        # the drop-in's default: calls served by the resident server (dmx/daemon.py); set
+        # DMX_DAEMON=0 to time one process per call
+        penv = dict(env, DMX_PROFILE_CLI="1")
+        per_call = []
+
+        def call(cmd):
+            t1 = time.perf_counter()
+            p = subprocess.run(cmd, check=True, env=penv, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, text=True)
+            prof = [ln for ln in p.stderr.splitlines() if ln.startswith("dmx cli phases")]
+            per_call.append({"s": round(time.perf_counter() - t1, 3),
+                             "phases": prof[-1][len("dmx cli phases: "):] if prof else ""})
+
         t = time.perf_counter()
-        subprocess.run([cli, "--action=trim", "-e", "0.1", "-j", j, "--rc",
-                        "-g", f"file:{panel.SP5_FASTA}", "-o", f"{out}/SP5/{{name}}_e2e.fastq.gz",
-                        gz, f"--json={out}/SP5/cutadapt_SP5_e2e.json"], check=True, env=env,
-                       stdout=subprocess.DEVNULL)
+        call([cli, "--action=trim", "-e", "0.1", "-j", j, "--rc",
+              "-g", f"file:{panel.SP5_FASTA}", "-o", f"{out}/SP5/{{name}}_e2e.fastq.gz",
+              gz, f"--json={out}/SP5/cutadapt_SP5_e2e.json"])
         ids = sorted(os.path.basename(f)[:-len("_e2e.fastq.gz")]
                      for f in glob.glob(f"{out}/SP5/*_e2e.fastq.gz") if "unknown" not in f)
         for ident in ids:
-            subprocess.run([cli, "--action=trim", "-e", "0.1", "-j", j, "--rc",
-                            "-a", f"file:{panel.SP27RC_FASTA}",
-                            "-o", f"{out}/SP27/{{name}}_{ident}_e2e.fastq.gz",
-                            f"{out}/SP5/{ident}_e2e.fastq.gz",
-                            f"--json={out}/SP27/{ident}_e2e.json"], check=True, env=env,
-                           stdout=subprocess.DEVNULL)
+            call([cli, "--action=trim", "-e", "0.1", "-j", j, "--rc",
+                  "-a", f"file:{panel.SP27RC_FASTA}",
+                  "-o", f"{out}/SP27/{{name}}_{ident}_e2e.fastq.gz",
+                  f"{out}/SP5/{ident}_e2e.fastq.gz",
+                  f"--json={out}/SP27/{ident}_e2e.json"])
         cs = time.perf_counter() - t
         res["calls_s"] = round(cs, 3)
         res["calls_reads_per_s"] = round(a.reads / cs, 1)
+        res["calls_per_call"] = per_call
+        res["calls_server"] = penv.get("DMX_DAEMON", "1") != "0"
+        t1 = time.perf_counter()
+        subprocess.run([sys.executable, "-c", "import numpy"], check=True)
+        res["python_numpy_start_s"] = round(time.perf_counter() - t1, 3)
     print(json.dumps(res))
 
 
