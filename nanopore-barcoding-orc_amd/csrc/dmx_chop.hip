@@ -9,10 +9,12 @@
 // here: the semantics are the build's restatement (checkers oracle/chop_oracle.c
 // and oracle/chopper.py), parity unpinned.  Per read:
 //   hits      every label (each primer of the -b FASTA and its reverse complement; IUPAC codes,
-//             N = any base; a read N matches anything) is searched in HW (infix) mode: D(j) =
-//             least edit distance of the label ending at read column j.  Each maximal run of
-//             columns with D <= k = int(cutoff * m) gives one hit: the run's first column of
-//             least D (stop) and the start of the shortest optimal alignment ending there;
+//             N = any base; a read N matches anything) is searched like one edlib HW / TASK_LOC
+//             call with k = int(cutoff * m) (edlib 1.3.x edlibAlign): D(j) = least edit distance
+//             of the label ending at read column j, best = min over the read of D(j); when
+//             best <= k every column with D(j) == best is a hit (edlib's end locations) whose
+//             start is that of the LONGEST optimal alignment ending there (edlib's reverse SHW
+//             alignment, last position);
 //   segments  the read's hits sorted by (start, stop, label) are paired greedily left to right:
 //             consecutive hits (a, b) whose labels form a configuration rule (-c, e.g.
 //             "+:SP5,-SP27|-:SP27,-SP5") delimit one segment on the rule's strand and are both
@@ -26,19 +28,22 @@
 //                 words.  A lane runs the 64-bit Myers/Hyyro step of the demux scans (labels
 //                 <= 64 nt) from m + k columns before its segment — exact for every D <= k from
 //                 the segment's first column on, as an alignment of cost <= k spans <= m + k
-//                 columns — follows
-//                 runs of D <= k (a run crossing the segment end is followed to its end) and
-//                 appends the runs that start inside its segment to an LDS hit list (one LDS
-//                 atomic each).  After a barrier one lane per hit finds its start (an anchored
-//                 Myers scan of the reverse-complement label over the reverse-complement view,
-//                 <= m + k columns); the block groups its hits by read (counting scatter), one
+//                 columns — keeps, per run of D <= k inside its segment, the columns at the
+//                 run's minimum (first column + a 64-bit offset mask), and at the run's end
+//                 appends them to an LDS hit list unless a lower D was already seen for the
+//                 (read, label): by this lane, or by any lane through the block's LDS minimum
+//                 (atomicMin).  After a barrier the hits above the (read, label) minimum are
+//                 dropped and one lane per hit finds its start (an anchored Myers scan of the
+//                 reverse-complement label over the reverse-complement view, m + best
+//                 columns); the block groups its hits by read (counting scatter), one
 //                 lane per read insertion-sorts its few hits and pairs them, and the block
 //                 reserves its ranges of the global hit and segment lists with one atomic each.
 //   chop_blkscan_kernel, chop_order_kernel
 //                 move every block's ranges into read order (block order = read order), so the
 //                 host receives read-ordered hits and segments without a sort.
 // A block whose hits overflow its LDS list (reads with hundreds of primer hits) is redone alone
-// by chop_big_kernel: hit lists in global memory sized by the exact count the LDS pass measured,
+// by chop_big_kernel: hit lists in global memory sized by the count the LDS pass measured
+// without the cross-lane pruning (which depends on timing; the redo prunes within lanes only),
 // counting scatter by read, parallel rank sort per read; a staging overflow re-runs with larger
 // buffers.
 #include <hip/hip_runtime.h>
@@ -102,28 +107,58 @@ struct ChopOrderArgs {
     dmx_chop_seg* segs;
 };
 
-__device__ __forceinline__ void chop_push(uint32_t* s_nh, dmx_chop_hit* s_hit, uint32_t cap,
-                                          uint32_t read, int lab, int dist, uint32_t stop) {
-    const uint32_t i = atomicAdd(s_nh, 1u);   // keeps counting past cap: the exact hit count
-    if (i < cap) {
+// Where a scan lane appends its hits.  nall == nullptr (chop_big_kernel): every hit that passes
+// the lane's own minimum is stored (a count the LDS pass measured exactly); otherwise hits are
+// stored only if no lower D is known for the (read, label) yet, and nall counts them all.
+struct ChopSink {
+    uint32_t* nh;          // stored hits (keeps counting past cap)
+    uint32_t* nall;        // hits before the cross-lane pruning, or nullptr
+    dmx_chop_hit* list;
+    uint32_t cap;
+    uint32_t* smin;        // the block's least D per (read, label): [read - r0][label]
+    uint32_t r0;
+};
+
+__device__ __forceinline__ void chop_push(const ChopSink& S, uint32_t read, int lab, int dist,
+                                          uint32_t stop) {
+    const uint32_t i = atomicAdd(S.nh, 1u);
+    if (i < S.cap) {
         dmx_chop_hit h;
         h.read = read;
         h.label = (int16_t)lab;
         h.dist = (int16_t)dist;
         h.start = -1;
         h.stop = (int32_t)stop;
-        s_hit[i] = h;
+        S.list[i] = h;
+    }
+}
+
+// The columns at one run's minimum: bstop and bstop + every set bit of `more`.
+__device__ __forceinline__ void chop_flush(const ChopSink& S, uint32_t read, int lab, int best,
+                                           uint32_t bstop, uint64_t more, int& lmin) {
+    if (best > lmin) return;
+    lmin = best;
+    uint32_t* smin = S.smin + (read - S.r0) * (uint32_t)kChopMaxLabels + (uint32_t)lab;
+    bool store = true;
+    if (S.nall) {
+        atomicAdd(S.nall, 1u + (uint32_t)__popcll(more));
+        store = (uint32_t)best <= *smin;
+    }
+    atomicMin(smin, (uint32_t)best);
+    if (!store) return;
+    chop_push(S, read, lab, best, bstop);
+    while (more) {
+        chop_push(S, read, lab, best, bstop + (uint32_t)__builtin_ctzll(more));
+        more &= more - 1ull;
     }
 }
 
 // One (segment, label) task: D(j) over the owned columns (s0, s0 + kChopSeg] of the read.
-// s_nh / s_hit: the block's hit counter and list (LDS, or global memory in chop_big_kernel).
 // HB: the last row's bit is in the low (0) or high (1) 32-bit half for every label, or -1
 // (mixed: selected per step).
 template <int HB>
 __device__ __forceinline__ void chop_scan(const ChopArgs& A, const ChopLabel& L, int lab,
-                                          uint32_t read, uint32_t si, uint32_t* s_nh,
-                                          dmx_chop_hit* s_hit, uint32_t cap) {
+                                          uint32_t read, uint32_t si, const ChopSink& S) {
     const uint32_t n = A.lens[read];
     const uint64_t off = A.offs[read];
     const int m = L.m, k = L.k;
@@ -133,19 +168,20 @@ __device__ __forceinline__ void chop_scan(const ChopArgs& A, const ChopLabel& L,
     // warm-up: starting at ws, the scan's D(m, j) is the true value whenever an optimal
     // alignment starts at or after ws, and never below it.  An alignment of cost c <= k spans
     // at most m + c columns, so from column ws + m + k on every D <= k is exact and every
-    // D > k stays > k: run membership and run minima are exact from column s0 on, which
-    // decides run ownership.
+    // D > k stays > k: D(j) is exact wherever it matters for j > s0.  Runs crossing a segment
+    // boundary are split; each piece reports its own minimum columns, a superset of the
+    // columns at the (read, label) minimum, which the block keeps.
     const uint32_t wu = (uint32_t)(m + k);
     const uint32_t ws = s0 > wu ? s0 - wu : 0u;
-    uint64_t pv = ~0ull, mv = 0ull;
+    uint64_t pv = ~0ull, mv = 0ull, more = 0ull;
     int d = m;
-    bool run = false, owned = false;
-    int best = 0;
+    bool run = false;
+    int best = 0, lmin = k;
     uint32_t bstop = 0;
-    for (uint32_t p = ws; p < n; p += 16) {
+    for (uint32_t p = ws; p < send; p += 16) {
         uint32_t codes, nb;
         fetch16(A.seq, A.nmask, off, n, 0u, 0u, p, codes, nb);
-        const uint32_t cnt = min(16u, n - p);
+        const uint32_t cnt = min(16u, send - p);
         uint64_t eqv[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q)
@@ -165,31 +201,36 @@ __device__ __forceinline__ void chop_scan(const ChopArgs& A, const ChopLabel& L,
                 if ((uint32_t)q < cnt) {
                     myers_step<HB>(eqv[q], pv, mv, d, hbit);
                     const uint32_t j = p + (uint32_t)q + 1u;
-                    if (d <= k) {
-                        if (!run) {
+                    if (d <= k && j > s0) {
+                        if (!run || d < best) {
                             run = true;
-                            owned = j > s0 && j <= s1;
                             best = d;
                             bstop = j;
-                        } else if (d < best) {
-                            best = d;
-                            bstop = j;
+                            more = 0ull;
+                        } else if (d == best) {
+                            if (j - bstop < 64u) {
+                                more |= 1ull << (j - bstop);
+                            } else {   // a long run: report these columns, keep collecting
+                                chop_flush(S, read, lab, best, bstop, more, lmin);
+                                bstop = j;
+                                more = 0ull;
+                            }
                         }
                     } else if (run) {
                         run = false;
-                        if (owned) chop_push(s_nh, s_hit, cap, read, lab, best, bstop);
+                        chop_flush(S, read, lab, best, bstop, more, lmin);
                     }
                 }
             }
         }
-        if (p + 16u >= send && !run) return;
     }
-    if (run && owned) chop_push(s_nh, s_hit, cap, read, lab, best, bstop);
+    if (run) chop_flush(S, read, lab, best, bstop, more, lmin);
 }
 
-// Start of the shortest optimal alignment ending at `stop`: the reverse-complement label R
-// (label ^ 1) anchored at reverse-complement view position n - stop (row 0 = t: the text is not
-// free at the anchor), first t with D'(m, t) == best.  min over t of D'(m, t) is `best`.
+// Start of the longest optimal alignment ending at `stop` (edlib: the last position of the
+// reverse SHW alignment): the reverse-complement label R (label ^ 1) anchored at
+// reverse-complement view position n - stop (row 0 = t: the text is not free at the anchor),
+// last t <= m + best with D'(m, t) == best.  min over t of D'(m, t) is `best`.
 __device__ int chop_start(const ChopArgs& A, const ChopLabel& R, uint32_t read, int best,
                           uint32_t stop) {
     const uint32_t n = A.lens[read];
@@ -199,6 +240,7 @@ __device__ int chop_start(const ChopArgs& A, const ChopLabel& R, uint32_t read, 
     uint64_t pv = ~0ull, mv = 0ull;
     int d = m;
     const uint32_t tmax = min(stop, (uint32_t)(m + best));
+    int start = -1;
     for (uint32_t t0 = 0; t0 < tmax; t0 += 16) {
         uint32_t codes, nb;
         fetch16(A.seq, A.nmask, off, n, 1u, 0u, n - stop + t0, codes, nb);
@@ -214,10 +256,10 @@ __device__ int chop_start(const ChopArgs& A, const ChopLabel& R, uint32_t read, 
             mh <<= 1;
             pv = mh | ~(xv | ph);
             mv = ph & xv;
-            if (d == best) return (int)(stop - (t0 + q + 1u));
+            if (d == best) start = (int)(stop - (t0 + q + 1u));
         }
     }
-    return -1;   // unreachable
+    return start;
 }
 
 __device__ __forceinline__ bool hit_less(const dmx_chop_hit& a, const dmx_chop_hit& b) {
@@ -336,43 +378,54 @@ __global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
     __shared__ uint32_t s_cnt[kChopReads], s_sc[kChopReads];
     __shared__ dmx_chop_hit s_hit[kChopHitCap];
     __shared__ dmx_chop_hit s_srt[kChopHitCap];
-    __shared__ uint32_t s_nh, s_base[2];
+    __shared__ uint32_t s_nh, s_nall, s_base[2];
+    // least D per (read, label) during the scans and the filter; s_srt is written only after
+    static_assert(kChopReads * kChopMaxLabels * 4 <= sizeof(dmx_chop_hit) * kChopHitCap, "s_min");
+    uint32_t* s_min = reinterpret_cast<uint32_t*>(s_srt);
     chop_load_panel(A.panel, s_lab, s_rule, s_rstrand);
     const int NL = A.panel->n_labels;
     const bool keep = A.panel->keep != 0;
     const uint32_t r0 = blockIdx.x * kChopReads;
     const uint32_t nr = min(kChopReads, A.n_reads - r0);
-    if (threadIdx.x == 0) s_nh = 0u;
+    if (threadIdx.x == 0) s_nh = s_nall = 0u;
+    for (uint32_t i = threadIdx.x; i < kChopReads * kChopMaxLabels; i += blockDim.x)
+        s_min[i] = ~0u;
     chop_segment_prefix(A, r0, nr, s_cnt, s_pre);
 
     // 1. scans: (segment, label) tasks, labels fastest
+    const ChopSink S{&s_nh, &s_nall, s_hit, kChopHitCap, s_min, r0};
     const uint32_t total = s_pre[nr] * (uint32_t)NL;
     for (uint32_t task = threadIdx.x; task < total; task += blockDim.x) {
         const uint32_t sg = task / (uint32_t)NL;
         const int lab = (int)(task - sg * (uint32_t)NL);
         const uint32_t t = chop_last_le(s_pre, nr, sg);
-        chop_scan<HB>(A, s_lab[lab], lab, r0 + t, sg - s_pre[t], &s_nh, s_hit, kChopHitCap);
+        chop_scan<HB>(A, s_lab[lab], lab, r0 + t, sg - s_pre[t], S);
     }
     __syncthreads();
-    const uint32_t nh = s_nh;
-    if (nh > kChopHitCap) {   // block-uniform: redone by chop_big_kernel with the exact count
+    const uint32_t ns = s_nh;
+    if (ns > kChopHitCap) {   // block-uniform: redone by chop_big_kernel with the exact count
         if (threadIdx.x == 0) {
             atomicOr(&A.ctr[2], 1ull);
             const unsigned long long i = atomicAdd(&A.ctr[3], 1ull);
             if (i < A.ovf_cap) {
                 A.ovf[2 * i] = blockIdx.x;
-                A.ovf[2 * i + 1] = nh;
+                A.ovf[2 * i + 1] = s_nall;
             }
         }
         return;
     }
 
-    // 2. starts; group by read (counting scatter)
-    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x) {
+    // 2. drop hits above their (read, label) minimum; starts; group by read (counting scatter)
+    for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
         dmx_chop_hit h = s_hit[i];
+        const uint32_t t = h.read - r0;
+        if ((uint32_t)h.dist > s_min[t * kChopMaxLabels + (uint32_t)h.label]) {
+            s_hit[i].read = ~0u;
+            continue;
+        }
         h.start = chop_start(A, s_lab[h.label ^ 1], h.read, h.dist, (uint32_t)h.stop);
         s_hit[i] = h;
-        atomicAdd(&s_cnt[h.read - r0], 1u);
+        atomicAdd(&s_cnt[t], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -385,12 +438,14 @@ __global__ __launch_bounds__(kChopBlock) void chop_kernel(ChopArgs A) {
         s_off[nr] = acc;
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x) {
+    for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
         const dmx_chop_hit h = s_hit[i];
+        if (h.read == ~0u) continue;
         const uint32_t t = h.read - r0;
         s_srt[s_off[t] + atomicAdd(&s_cnt[t], 1u)] = h;
     }
     __syncthreads();
+    const uint32_t nh = s_off[nr];
 
     // 3. one lane per read: insertion-sort its few hits by (start, stop, label)
     if (threadIdx.x < nr) {
@@ -426,7 +481,10 @@ __global__ __launch_bounds__(kChopBlock) void chop_big_kernel(ChopArgs A, const 
     __shared__ int8_t s_rstrand[kChopMaxRules];
     __shared__ uint32_t s_pre[kChopReads + 1], s_off[kChopReads + 1], s_soff[kChopReads + 1];
     __shared__ uint32_t s_cnt[kChopReads], s_sc[kChopReads];
+    __shared__ uint32_t s_min[kChopReads * kChopMaxLabels];
     __shared__ uint32_t s_base[2];
+    for (uint32_t i = threadIdx.x; i < kChopReads * kChopMaxLabels; i += blockDim.x)
+        s_min[i] = ~0u;
     chop_load_panel(A.panel, s_lab, s_rule, s_rstrand);
     const int NL = A.panel->n_labels;
     const bool keep = A.panel->keep != 0;
@@ -438,20 +496,26 @@ __global__ __launch_bounds__(kChopBlock) void chop_big_kernel(ChopArgs A, const 
     dmx_chop_hit* T = temp + base[blockIdx.x];
     uint32_t* cnt = counter + blockIdx.x;
     chop_segment_prefix(A, r0, nr, s_cnt, s_pre);
+    const ChopSink S{cnt, nullptr, H, cap, s_min, r0};
     const uint32_t total = s_pre[nr] * (uint32_t)NL;
     for (uint32_t task = threadIdx.x; task < total; task += blockDim.x) {
         const uint32_t sg = task / (uint32_t)NL;
         const int lab = (int)(task - sg * (uint32_t)NL);
         const uint32_t t = chop_last_le(s_pre, nr, sg);
-        chop_scan<-1>(A, s_lab[lab], lab, r0 + t, sg - s_pre[t], cnt, H, cap);
+        chop_scan<-1>(A, s_lab[lab], lab, r0 + t, sg - s_pre[t], S);
     }
     __syncthreads();
-    const uint32_t nh = min(atomicAdd(cnt, 0u), cap);
-    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x) {
+    const uint32_t ns = min(atomicAdd(cnt, 0u), cap);
+    for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
         dmx_chop_hit h = H[i];
+        const uint32_t t = h.read - r0;
+        if ((uint32_t)h.dist > s_min[t * kChopMaxLabels + (uint32_t)h.label]) {
+            H[i].read = ~0u;
+            continue;
+        }
         h.start = chop_start(A, s_lab[h.label ^ 1], h.read, h.dist, (uint32_t)h.stop);
         H[i] = h;
-        atomicAdd(&s_cnt[h.read - r0], 1u);
+        atomicAdd(&s_cnt[t], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -464,12 +528,14 @@ __global__ __launch_bounds__(kChopBlock) void chop_big_kernel(ChopArgs A, const 
         s_off[nr] = acc;
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x) {
+    for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
         const dmx_chop_hit h = H[i];
+        if (h.read == ~0u) continue;
         const uint32_t t = h.read - r0;
         T[s_off[t] + atomicAdd(&s_cnt[t], 1u)] = h;
     }
     __syncthreads();
+    const uint32_t nh = s_off[nr];
     for (uint32_t t = 0; t < nr; ++t) {   // block-uniform
         const uint32_t o = s_off[t], c = s_off[t + 1] - o;
         for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {

@@ -6,15 +6,20 @@
  * semantics below are the build's definition, restated from edlib's documented
  * HW ("infix") mode; oracle/chopper.py carries the segmentation / classification half.
  *
- * For one label (a primer, or its reverse complement) P of length m and one read R of length n:
+ * For one label (a primer, or its reverse complement) P of length m and one read R of length n,
+ * one edlib call `edlibAlign(P, R, HW, TASK_LOC, k)` (edlib 1.3.x, edlib.cpp edlibAlign: the HW
+ * end locations, then one reverse SHW alignment per end location for its start):
  *   match(P[i], R[j])  = R[j] not in ACGT (N matches anything, edlib additionalEqualities
  *                        style), or R[j] in IUPAC(P[i])                (reads upper-cased)
  *   D(j), 1 <= j <= n  = min over s <= j of unit-cost editdist(P, R[s:j))   (HW / infix)
  *   k                  = (int)(cutoff * m)
- *   hits               = maximal runs of consecutive j with D(j) <= k; per run:
- *                        stop = first j of the run with the run's minimal D, dist = D(stop),
- *                        start = the largest s with editdist(P, R[s:stop)) == dist
- *                        (edlib's start search: the shortest optimal alignment ending at stop)
+ *   best               = min over j of D(j) (edlib's editDistance); no hits when best > k
+ *   hits               = every stop j with D(j) == best (edlib's endLocations, ascending), each
+ *                        with dist = best and start = the SMALLEST s with
+ *                        editdist(P, R[s:stop)) == best: edlib takes the last position of the
+ *                        reverse SHW alignment ("taking last location as start ensures that
+ *                        alignment will not start with insertions if it can start with
+ *                        mismatches instead"), i.e. the longest optimal alignment ending there
  * Computed with the textbook O(m n) column DP (no bit vectors), independently of the HIP
  * kernel's Myers scan and warm-up segmentation.  orc_chop_batch runs it over a batch on
  * pthreads (the bench's CPU baseline).
@@ -62,52 +67,53 @@ int orc_chop_hits(const char* pat, int m, double cutoff, const uint8_t* read, in
         }
     }
     const int k = (int)(cutoff * m);
+    int* D = malloc(sizeof(int) * ((size_t)n + 1));
     for (int i = 0; i <= m; ++i) col[i] = i;
-    int nh = 0, run = 0, best = 0, bstop = 0;
-    for (int j = 1; j <= n + 1; ++j) {
-        int d = m + 1;   /* j == n + 1: sentinel closing an open run */
-        if (j <= n) {
-            const int rb = base_bit(read[j - 1]);
-            int diag = col[0];   /* D(0, j-1) = 0: free start */
-            col[0] = 0;
-            for (int i = 1; i <= m; ++i) {
-                const int up = col[i - 1] + 1, left = col[i] + 1;
-                const int dg = diag + (eqc(pm[i - 1], rb) ? 0 : 1);
-                diag = col[i];
-                int v = dg < up ? dg : up;
-                col[i] = v < left ? v : left;
-            }
-            d = col[m];
+    int best = m + 1;
+    D[0] = m;
+    for (int j = 1; j <= n; ++j) {
+        const int rb = base_bit(read[j - 1]);
+        int diag = col[0];   /* D(0, j-1) = 0: free start */
+        col[0] = 0;
+        for (int i = 1; i <= m; ++i) {
+            const int up = col[i - 1] + 1, left = col[i] + 1;
+            const int dg = diag + (eqc(pm[i - 1], rb) ? 0 : 1);
+            diag = col[i];
+            int v = dg < up ? dg : up;
+            col[i] = v < left ? v : left;
         }
-        if (d <= k) {
-            if (!run) { run = 1; best = d; bstop = j; }
-            else if (d < best) { best = d; bstop = j; }
-        } else if (run) {
-            run = 0;
-            /* start: G(i, t) = editdist(P[m-i:], R[stop-t:stop)); first t with G(m, t) == best */
-            int start = -1;
-            for (int i = 0; i <= m; ++i) g[i] = i;
-            for (int t = 1; t <= bstop && start < 0; ++t) {
-                const int rb = base_bit(read[bstop - t]);
-                int diag = g[0];
-                g[0] = t;
-                for (int i = 1; i <= m; ++i) {
-                    const int up = g[i - 1] + 1, left = g[i] + 1;
-                    const int dg = diag + (eqc(pm[m - i], rb) ? 0 : 1);
-                    diag = g[i];
-                    int v = dg < up ? dg : up;
-                    g[i] = v < left ? v : left;
-                }
-                if (g[m] == best) start = bstop - t;
-            }
-            if (nh < cap) {
-                out[3 * nh] = bstop;
-                out[3 * nh + 1] = start;
-                out[3 * nh + 2] = best;
-            }
-            ++nh;
-        }
+        D[j] = col[m];
+        if (D[j] < best) best = D[j];
     }
+    int nh = 0;
+    for (int j = 1; j <= n && best <= k; ++j) {
+        if (D[j] != best) continue;
+        /* start: G(i, t) = editdist(P[m-i:], R[stop-t:stop)); last t <= m + best with
+         * G(m, t) == best (an alignment of cost best spans at most m + best columns) */
+        int start = -1;
+        for (int i = 0; i <= m; ++i) g[i] = i;
+        const int tmax = j < m + best ? j : m + best;
+        for (int t = 1; t <= tmax; ++t) {
+            const int rb = base_bit(read[j - t]);
+            int diag = g[0];
+            g[0] = t;
+            for (int i = 1; i <= m; ++i) {
+                const int up = g[i - 1] + 1, left = g[i] + 1;
+                const int dg = diag + (eqc(pm[m - i], rb) ? 0 : 1);
+                diag = g[i];
+                int v = dg < up ? dg : up;
+                g[i] = v < left ? v : left;
+            }
+            if (g[m] == best) start = j - t;
+        }
+        if (nh < cap) {
+            out[3 * nh] = j;
+            out[3 * nh + 1] = start;
+            out[3 * nh + 2] = best;
+        }
+        ++nh;
+    }
+    free(D);
     free(pm); free(col); free(g);
     return nh;
 }

@@ -11,11 +11,13 @@ options:
 
   labels    primer p of the -b FASTA (file order; name = first header word) is label 2p
             ("NAME"), its reverse complement label 2p+1 ("-NAME", the config's notation)
-  hits      per label: every maximal run of read columns j with D(j) <= int(cutoff * m), D(j)
-            = least edit distance of the label ending at column j (IUPAC codes; a read N
-            matches anything); hit = the run's first column of least D (stop) and the start of
-            the shortest optimal alignment ending there — oracle/chop_oracle.c (plain O(mn) DP)
-            or `hits_py` (pure Python, tiny cases)
+  hits      per label, one edlib HW / TASK_LOC call with k = int(cutoff * m) (edlib 1.3.x,
+            edlib.cpp edlibAlign): D(j) = least edit distance of the label ending at read column
+            j (IUPAC codes; a read N matches anything); best = min over j of D(j); no hits when
+            best > k, else one hit per stop j with D(j) == best (edlib's end locations), its
+            start the smallest s with editdist(label, read[s:j)) == best (edlib takes the last
+            position of its reverse SHW alignment: the longest optimal alignment) —
+            oracle/chop_oracle.c (plain O(mn) DP) or `hits_py` (pure Python, tiny cases)
   segments  a read's hits sorted by (start, stop, label) are paired greedily left to right by
             the config rules (M13_config_for_pychopper.txt:1 "+:SP5,-SP27|-:SP27,-SP5"); span
             [a.start, b.stop) with -p (keep primers), else [a.stop, b.start) (empty if they
@@ -134,19 +136,15 @@ def hits_py(pat: str, read: str, cutoff: float):
                            col[i] + 1))
         col = cur
         D.append(col[m])
-    out, j = [], 1
-    while j <= n:
-        if D[j] > k:
-            j += 1
-            continue
-        e = j
-        while e < n and D[e + 1] <= k:
-            e += 1
-        best = min(D[j:e + 1])
-        stop = D.index(best, j, e + 1)
-        start = next(s for s in range(stop, -1, -1) if _global(pat, R[s:stop]) == best)
-        out.append((start, stop, best))
-        j = e + 1
+    best = min(D[1:], default=m + 1)
+    if best > k:
+        return []
+    out = []
+    for stop in range(1, n + 1):
+        if D[stop] == best:
+            start = min(s for s in range(max(0, stop - m - best), stop + 1)
+                        if _global(pat, R[s:stop]) == best)
+            out.append((start, stop, best))
     return out
 
 

@@ -214,14 +214,23 @@ def test_chop_random_primer_panels(ctx):
 
 @pytest.mark.gpu
 def test_chop_reads_beyond_the_lds_hit_list(ctx):
-    """Long reads with thousands of hits (6-nt primers, one error allowed) overflow the 64-read
-    block's 512-entry LDS hit list: chop_big_kernel redoes those blocks with global hit lists;
-    the other blocks take the normal path."""
+    """Long tandem repeats of a primer (thousands of end locations at the least distance, 6-nt
+    primers, one error allowed) overflow the 64-read block's 512-entry LDS hit list:
+    chop_big_kernel redoes those blocks with global hit lists; the other blocks take the normal
+    path."""
     rng = np.random.default_rng(41)
     primers = [(f"P{i}", "".join(rng.choice(list("ACGT"), size=6))) for i in range(8)]
     rules = [(0, 3, 0), (2, 1, 1), (4, 5, 0), (7, 6, 1)]
-    seqs = ["".join(rng.choice(list("ACGT"), size=int(rng.integers(4000, 9000))))
-            if i % 3 == 0 else "".join(rng.choice(list("ACGT"), size=int(rng.integers(0, 300))))
+
+    def tandem(i):
+        unit = primers[i % 8][1] + "".join(rng.choice(list("ACGT"), size=int(rng.integers(0, 3))))
+        s = list(unit * (int(rng.integers(4000, 9000)) // len(unit)))
+        for p in rng.integers(0, len(s), size=len(s) // 200):
+            s[p] = "ACGT"[int(rng.integers(4))]
+        return "".join(s)
+
+    seqs = [tandem(i) if i % 3 == 0
+            else "".join(rng.choice(list("ACGT"), size=int(rng.integers(0, 300))))
             for i in range(40)]
     for keep in (True, False):
         nseg, nhit, H, S = _gpu(ctx, seqs, primers, rules, 0.2, keep)
