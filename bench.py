@@ -45,8 +45,26 @@ def _valu_ceiling() -> float:
 
 
 VALU_CEILING = _valu_ceiling()   # independent v_bitop3 chains at full occupancy
-FILTER_OPS_PER_COLUMN = 30.9  # PMC: SQ_INSTS_VALU x 64 / filter columns (profiles/r2_pmc_*)
-CHOP_OPS_PER_COLUMN = 46.47   # PMC: same for chop_kernel (profiles/r1_pmc_summary_chop_c2_10M.txt)
+
+
+def pmc_table(workload: str, reads: int):
+    """The committed rocprofv3 PMC table of this exact workload (profiles/kernel_pmc.json,
+    tools/kernel_table_from_pmc.py over tools/pmc_passes.sh), or None."""
+    try:
+        with open(os.environ.get("DMX_KERNEL_PMC") or
+                  os.path.join(ROOT, "profiles", "kernel_pmc.json")) as fh:
+            return json.load(fh).get(f"{workload}:{reads}")
+    except (OSError, ValueError):
+        return None
+
+
+def pmc_valu_insts(workload: str, reads: int, kernel: str, last_only: bool = False):
+    """SQ_INSTS_VALU of the kernel's launches in one PMC'd step (all launches, or the last)."""
+    pmc = pmc_table(workload, reads)
+    launches = (pmc or {}).get("kernels", {}).get(kernel, [])
+    if not launches:
+        return None
+    return launches[-1]["valu_insts"] if last_only else sum(e["valu_insts"] for e in launches)
 
 
 def filter_algorithmic_bytes(lengths: np.ndarray, n_windows: int) -> float:
@@ -77,10 +95,11 @@ def pmc_traffic(workload: str, reads: int):
 # the two-round pipeline's kernels and the live stage events that time them (per round)
 KERNEL_STAGES = (("dmx::filter_kernel", "filter"), ("dmx::verify_kernel", "verify"),
                  ("dmx::iscreen_kernel", "screen"), ("dmx::wscan_kernel<true>", "wscan"),
-                 ("band_cand<7>+band_cand<15>+select_cand", "resolve"))
+                 ("band_cand<7>+band_cand<11|15>+select_cand", "resolve"))
 PMC_NAMES = {"filter": ["filter_kernel"], "verify": ["verify_kernel"],
              "screen": ["iscreen_kernel"], "wscan": ["wscan_kernel<true>"],
-             "resolve": ["band_cand_kernel<7>", "band_cand_kernel<15>", "select_cand_kernel"]}
+             "resolve": ["band_cand_kernel<7>", "band_cand_kernel<11>", "band_cand_kernel<15>",
+                         "select_cand_kernel"]}
 
 
 def kernel_table(workload: str, reads: int, stage: dict, K: int, step_ms: float):
@@ -88,13 +107,7 @@ def kernel_table(workload: str, reads: int, stage: dict, K: int, step_ms: float)
     rocprofv3 PMC table exists for this exact workload (profiles/kernel_pmc.json, written by
     tools/kernel_table_from_pmc.py), the VALU issue rate and HBM bytes of the same launches:
     instructions and bytes per launch are properties of the workload, the time is this run's."""
-    pmc = None
-    try:
-        with open(os.environ.get("DMX_KERNEL_PMC") or
-                  os.path.join(ROOT, "profiles", "kernel_pmc.json")) as fh:
-            pmc = json.load(fh).get(f"{workload}:{reads}")
-    except (OSError, ValueError):
-        pmc = None
+    pmc = pmc_table(workload, reads)
     out = {}
     for name, st in KERNEL_STAGES:
         ms = [stage[f"{st}{r}"] / K for r in (0, 1)]
@@ -182,6 +195,8 @@ def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutof
     extra = np.maximum(np.ceil(L / 512) - 1, 0)
     cols = sum(float(np.sum(L + extra * (m + int(cutoff * m)))) for m in label_lens)
     traffic, traffic_src = pmc_traffic("chop", args.reads)
+    vi = pmc_valu_insts("chop", args.reads, "chop_kernel", last_only=True)
+    ops_col = vi * 64 / cols if vi else None
     return {
         "metric": "Mreads/s pychopper-style reorientation (01_pychopper.sh: -m edlib -p, "
                   "M13 SP5/SP27 primers)",
@@ -201,13 +216,13 @@ def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutof
                      "kernel": "dmx::chop_kernel", "avg_launch_ms": round(kern_ms, 3),
                      "note": "VALU-bound bit-vector scan (DESIGN.md §8d)"},
         "valu": {"columns_per_s": cols / (kern_ms / 1e3),
-                 "lane_ops_per_column": CHOP_OPS_PER_COLUMN,
-                 "lane_ops_per_s": cols / (kern_ms / 1e3) * CHOP_OPS_PER_COLUMN,
-                 "frac_of_measured_ceiling": cols / (kern_ms / 1e3) * CHOP_OPS_PER_COLUMN
-                 / VALU_CEILING,
+                 "lane_ops_per_column": ops_col,
+                 "lane_ops_per_s": cols / (kern_ms / 1e3) * ops_col if ops_col else None,
+                 "frac_of_measured_ceiling": (cols / (kern_ms / 1e3) * ops_col / VALU_CEILING
+                                              if ops_col else None),
                  "measured_ceiling_lane_ops_per_s": VALU_CEILING,
-                 "source": "ops/column = SQ_INSTS_VALU x 64 / Myers columns of the timed launch "
-                           "(cutoff 0.15, profiles/r1_pmc_summary_chop_c2_10M.txt)"},
+                 "source": "ops/column = SQ_INSTS_VALU x 64 of the PMC'd timed launch "
+                           "(profiles/kernel_pmc.json 'chop:<reads>') / its Myers columns"},
         "stage_ms_per_step": {k: round(v / K, 3) for k, v in ms.items()},
         "hits_per_read": round(n_hits / max(1, len(L)), 4),
         "segments_per_read": round(n_segs / max(1, len(L)), 4),
@@ -232,6 +247,8 @@ def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, 
     A0, A1 = ctx.panel_sizes
     cols = float(lengths.sum()) * 2 + float(len2.sum()) * 2     # filter columns, both strands
     col_rate = cols / ((stage["filter0"] + stage["filter1"]) / K / 1e3)
+    vi = pmc_valu_insts(args.workload, args.reads, "filter_kernel")
+    ops_col = vi * 64 / cols if vi else None
     return {
         "metric": METRIC, "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
         "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
@@ -252,13 +269,14 @@ def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, 
                              "a bit-vector scan, VALU-bound by construction (DESIGN.md §5): "
                              "'valu' gives its issue rate against the measured ceiling"},
         "valu": {"filter_columns_per_s": col_rate,
-                 "filter_lane_ops_per_column": FILTER_OPS_PER_COLUMN,
-                 "filter_lane_ops_per_s": col_rate * FILTER_OPS_PER_COLUMN,
-                 "frac_of_measured_ceiling": col_rate * FILTER_OPS_PER_COLUMN / VALU_CEILING,
+                 "filter_lane_ops_per_column": ops_col,
+                 "filter_lane_ops_per_s": col_rate * ops_col if ops_col else None,
+                 "frac_of_measured_ceiling": (col_rate * ops_col / VALU_CEILING
+                                              if ops_col else None),
                  "measured_ceiling_lane_ops_per_s": VALU_CEILING,
                  "nominal_peak_lane_ops_per_s": VALU_PEAK_TOPS * 1e12,
-                 "source": "ops/column = SQ_INSTS_VALU x 64 / columns of the filter launch "
-                           "(profiles/r2_pmc_summary_c2x24_10M.txt); ceiling = independent "
+                 "source": "ops/column = SQ_INSTS_VALU x 64 of both PMC'd filter launches "
+                           "(profiles/kernel_pmc.json) / their columns; ceiling = independent "
                            "v_bitop3 chains at full occupancy (profiles/r2_valu_ceiling.json)"},
         "kernels": kernel_table(args.workload, args.reads, stage, K, elapsed / K * 1e3),
         "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},

@@ -205,9 +205,10 @@ int dmx_locate(dmx_ctx* ctx, const char* const* patterns, const int* plens, int 
  * restated in DESIGN.md §8d, parity unpinned).  Runs on the batch made resident by dmx_load.
  * Labels: primer p (file order) is label 2p, its reverse complement label 2p+1 (pychopper's
  * "-NAME").  IUPAC codes in primers (N = any base); a read N matches anything.
- * Hits: per label, each maximal run of read columns whose least infix edit distance is
- * <= k = (int)(cutoff * m) gives one hit: the run's first column of least distance (stop) and
- * the start of the shortest optimal alignment ending there.
+ * Hits: per label, as one edlib HW / EDLIB_TASK_LOC call with k = (int)(cutoff * m): when the
+ * least infix edit distance over the read, best, is <= k, every read column whose least
+ * distance equals best is a hit (stop), with the start of the longest optimal alignment
+ * ending there (edlib's reverse SHW alignment, last position).
  * Segments: a read's hits sorted by (start, stop, label) are paired greedily left to right;
  * consecutive hits (a, b) with a rule (rule_left[r], rule_right[r]) form a segment on strand
  * rule_strand[r] (0 '+', 1 '-'; the first rule of a pair wins) spanning [a.start, b.stop) with
