@@ -50,6 +50,11 @@ typedef struct dmx_reader dmx_reader;
 typedef struct dmx_sink dmx_sink;
 
 int dmx_io_abi_version(void);
+/* One gzip member of src[0, n) in the writers' format (RFC 1952 with a "DX" size subfield;
+ * level 1 = Huffman-only DEFLATE, other levels zlib): written to out (cap bytes, at least
+ * 2 n + 4096), its length to *out_len.  0 on success, negative if cap is too small. */
+int dmx_io_gzip(const uint8_t* src, size_t n, int level, uint8_t* out, size_t cap,
+                size_t* out_len);
 
 /* path: a file (gzip detected by its magic bytes) or "-" for stdin. */
 int dmx_reader_open(const char* path, size_t batch_bytes, int threads, dmx_reader** out);

@@ -1031,6 +1031,17 @@ bool gzip_member(const uint8_t* src, size_t n, int level, Bytes& out) {
 
 }  // namespace
 
+extern "C" int dmx_io_gzip(const uint8_t* src, size_t n, int level, uint8_t* out, size_t cap,
+                           size_t* out_len) {
+    if ((!src && n) || !out || !out_len || level < 0 || level > 9) return -1;
+    Bytes m;
+    if (!gzip_member(src, n, level, m)) return -1;
+    if (m.size() > cap) return -2;
+    memcpy(out, m.data(), m.size());
+    *out_len = m.size();
+    return 0;
+}
+
 struct dmx_sink {
     std::vector<Out> outs;
     bool fasta_out = false;

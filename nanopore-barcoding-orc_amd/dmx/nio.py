@@ -20,7 +20,7 @@ IO_PATH = os.path.join(HERE, "libdmx_io.so")
 IO_EXPORTS = ["dmx_io_abi_version", "dmx_reader_open", "dmx_reader_next", "dmx_reader_error",
               "dmx_reader_close", "dmx_batch_free", "dmx_sink_open", "dmx_sink_write",
               "dmx_sink_close", "dmx_sink_error", "dmx_sink_free", "dmx_sink_write_rows",
-              "dmx_batch_mean_qual"]
+              "dmx_batch_mean_qual", "dmx_io_gzip"]
 
 
 class _CBatch(ctypes.Structure):
@@ -63,10 +63,23 @@ def load() -> ctypes.CDLL:
     L.dmx_sink_error.restype = ctypes.c_char_p
     L.dmx_sink_free.argtypes = [P]
     L.dmx_sink_free.restype = None
+    L.dmx_io_gzip.argtypes = [ctypes.c_char_p, c_size, c_int, P, c_size, P]
     if L.dmx_io_abi_version() != 1:
         raise DmxError("libdmx_io ABI mismatch")
     _io = L
     return L
+
+
+def gzip_member(data: bytes, level: int = 1) -> bytes:
+    """One gzip member of `data` in the writers' format (dmx_io_gzip)."""
+    L = load()
+    cap = 2 * len(data) + 4096
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    if L.dmx_io_gzip(data, len(data), int(level), ctypes.addressof(out), cap,
+                     ctypes.addressof(n)) != 0:
+        raise DmxError("dmx_io_gzip failed")
+    return out.raw[:n.value]
 
 
 def _view(ptr, n, dtype):

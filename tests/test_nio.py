@@ -222,3 +222,31 @@ def test_sized_member_crc_mismatch_is_an_error(tmp_path):
     (tmp_path / "bad.fq.gz").write_bytes(bytes(blob))
     with pytest.raises(ValueError):
         _read_all(tmp_path / "bad.fq.gz")
+
+
+def test_huffman_gzip_members_inflate_with_zlib():
+    """The writers' level-1 members (csrc/dmx_deflate.h: dynamic-Huffman blocks, no LZ77) are
+    standard gzip: Python's zlib inflates them byte-exact, over block boundaries (256 KB),
+    constant input, every byte value, one very rare byte (code lengths past 15 bits are
+    flattened), empty input, and real FASTQ text; the reader inflates them too."""
+    import gzip
+    import zlib
+    rng = np.random.default_rng(5)
+    skew = rng.choice(256, size=600_000, p=np.r_[[0.5], np.full(255, 0.5 / 255)]).astype(np.uint8)
+    rare = np.full(1 << 20, 65, np.uint8)
+    rare[::3] = 67
+    rare[12345] = 7                      # probability 1e-6: depth > 15 before flattening
+    fib = np.repeat(np.arange(24, dtype=np.uint8),
+                    [int(1.6 ** i) + 1 for i in range(24)])   # Fibonacci-like frequencies
+    cases = [b"", b"A", b"AAAA" * 1000, bytes(range(256)) * 3000, skew.tobytes(),
+             rare.tobytes(), rng.permutation(fib).tobytes(),
+             rng.integers(0, 256, size=(1 << 20) + 17, dtype=np.uint8).tobytes(),
+             b"@r1 x\nACGTN\n+\nIIII#\n" * 50_000]
+    for data in cases:
+        for level in (1, 6):
+            m = nio.gzip_member(data, level)
+            assert gzip.decompress(m) == data
+            assert zlib.decompress(m, 31) == data
+    fq = b"".join(b"@r%d\n%s\n+\n%s\n" % (i, b"ACGT" * (i % 50 + 1), b"I" * (4 * (i % 50 + 1)))
+                  for i in range(20000))
+    assert len(nio.gzip_member(fq, 1)) < 0.45 * len(fq)
