@@ -169,22 +169,29 @@ inline void huff_block(BitWriter& bw, const uint8_t* src, size_t n, bool final) 
 
     uint32_t tab[256];
     for (int s = 0; s < 256; ++s) tab[s] = (uint32_t)code[s] | ((uint32_t)len[s] << 16);
+    // branch-free packing: three codes (<= 45 bits) on top of <= 7 pending bits, then store 8
+    // bytes and advance by the whole bytes written (the output keeps 8 bytes of slack)
     uint64_t buf = bw.buf;
     int nb = bw.n;
     uint8_t* p = bw.p;
+    while (nb >= 8) {
+        *p++ = (uint8_t)buf;
+        buf >>= 8;
+        nb -= 8;
+    }
     i = 0;
-    for (; i + 2 <= n; i += 2) {   // two codes (<= 30 bits) per flush check: nb stays < 64
-        const uint32_t e0 = tab[src[i]], e1 = tab[src[i + 1]];
-        buf |= (uint64_t)(e0 & 0xFFFFu) << nb;
-        nb += (int)(e0 >> 16);
-        buf |= (uint64_t)(e1 & 0xFFFFu) << nb;
-        nb += (int)(e1 >> 16);
-        if (nb >= 32) {
-            std::memcpy(p, &buf, 4);
-            p += 4;
-            buf >>= 32;
-            nb -= 32;
-        }
+    for (; i + 3 <= n; i += 3) {
+        // the three codes are joined off the bit-position dependency chain
+        const uint32_t e0 = tab[src[i]], e1 = tab[src[i + 1]], e2 = tab[src[i + 2]];
+        const int l0 = (int)(e0 >> 16), l01 = l0 + (int)(e1 >> 16);
+        const uint64_t v = (uint64_t)(e0 & 0xFFFFu) | ((uint64_t)(e1 & 0xFFFFu) << l0) |
+                           ((uint64_t)(e2 & 0xFFFFu) << l01);
+        buf |= v << nb;
+        nb += l01 + (int)(e2 >> 16);
+        std::memcpy(p, &buf, 8);
+        p += nb >> 3;
+        buf >>= nb & ~7;
+        nb &= 7;
     }
     bw.buf = buf;
     bw.n = nb;

@@ -449,12 +449,65 @@ struct MemberGzSource : Source {
 // ------------------------------------------------------------------------------------------
 // batches
 
+// Process-wide cache of large buffers.  glibc serves allocations above 32 MiB by mmap and unmaps
+// them on free, so every batch (and every CLI call of the resident server) faulted its ~256 MB
+// of text and packed words in again, page by page, from the threads that fill them.  Batches
+// hand their big buffers back here and the next batch takes them, pages still mapped.
+template <class V>
+struct BigPool {
+    static constexpr size_t kMinBytes = 32u << 20;
+    static constexpr size_t kKeep = 8;
+    std::mutex mu;
+    std::vector<V> keep;
+    // v (empty) gets a pooled buffer of capacity >= n elements, if there is one
+    void take(V& v, size_t n) {
+        std::lock_guard<std::mutex> g(mu);
+        int bi = -1;
+        for (int i = 0; i < (int)keep.size(); ++i)
+            if (keep[i].capacity() >= n && (bi < 0 || keep[i].capacity() < keep[bi].capacity()))
+                bi = i;
+        if (bi < 0) return;
+        v.swap(keep[bi]);
+        keep.erase(keep.begin() + bi);
+        v.clear();
+    }
+    void give(V& v) {
+        if (v.capacity() * sizeof(typename V::value_type) < kMinBytes) return;
+        std::lock_guard<std::mutex> g(mu);
+        if (keep.size() < kKeep) {
+            keep.emplace_back();
+            keep.back().swap(v);
+        }
+    }
+    // v grows to n elements (contents kept), from the pool when it has to reallocate
+    void grow(V& v, size_t n) {
+        if (v.capacity() >= n) return;
+        V nv;
+        take(nv, n);
+        if (nv.capacity() < n) {
+            v.reserve(n);
+            return;
+        }
+        nv.assign(v.begin(), v.end());
+        v.swap(nv);
+        give(nv);
+    }
+};
+BigPool<Bytes> g_bytes_pool;
+BigPool<Words> g_words_pool;
+
 struct Batch : dmx_batch {
     std::atomic<int> refs{1};
     Bytes text_v, seqtext_v;
     std::vector<uint64_t> head_v, seq_v, qual_v, offs_v;
     std::vector<uint32_t> lens_v;
     Words seq2b_v, nmask_v;
+    ~Batch() {
+        g_bytes_pool.give(text_v);
+        g_bytes_pool.give(seqtext_v);
+        g_words_pool.give(seq2b_v);
+        g_words_pool.give(nmask_v);
+    }
     void publish() {
         text = text_v.data();
         head = head_v.data();
@@ -519,6 +572,8 @@ void pack_batch(Batch* b, int nth) {
     }
     b->total_nt = total;
     const size_t words = pack_words(total, n);
+    g_words_pool.grow(b->seq2b_v, words);
+    g_words_pool.grow(b->nmask_v, words);
     b->seq2b_v.resize(words);
     b->nmask_v.resize(words);
     // zero the head pad and everything after the last read (reads tile [kPad, g) exactly)
@@ -689,7 +744,7 @@ bool dmx_reader::next_batch(Batch** out, std::string& e) {
     double t0 = kIoDebug ? now_s() : 0, t1 = 0, t2 = 0;
     for (;;) {
         // fill
-        if (buf.capacity() < target + 64) buf.reserve(target + 64);
+        g_bytes_pool.grow(buf, target + 64);
         while (!src_eof && buf.size() < target) {
             const size_t old = buf.size();
             const size_t want = std::min<size_t>(target - old, src->chunk_hint());
