@@ -1236,10 +1236,22 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
                     if (end_lo <= 0) dmin_end = L;
                     if (near_lo <= 0) dmin_near = L;
                 }
+                // two 16-column chunks in flight: the next chunk's gather is issued before this
+                // chunk's steps (one lane per window: the loads are scattered, latency-bound)
+                uint32_t c_nx = 0, n_nx = 0, c_nx2 = 0, n_nx2 = 0;
+                if (js < hi)
+                    fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, (uint32_t)js, c_nx,
+                            n_nx);
+                if (js + 16 < hi)
+                    fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start,
+                            (uint32_t)(js + 16), c_nx2, n_nx2);
                 for (int p0 = js; p0 < hi; p0 += 16) {
-                    uint32_t codes, nb;
-                    fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, (uint32_t)p0, codes,
-                            nb);
+                    const uint32_t codes = c_nx, nb = n_nx;
+                    c_nx = c_nx2;
+                    n_nx = n_nx2;
+                    if (p0 + 32 < hi)
+                        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start,
+                                (uint32_t)(p0 + 32), c_nx2, n_nx2);
                     const int cnt = min(16, hi - p0);
                     for (int q = 0; q < cnt; ++q) {
                         const uint32_t code = ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
