@@ -14,24 +14,30 @@ Protocol: request = u32 length + JSON {"argv", "cwd", "env"}; reply = frames u8 
 + payload, tags b"o" (stdout bytes), b"e" (stderr bytes), b"x" (exit status as text)."""
 from __future__ import annotations
 
-import hashlib
 import json
 import os
 import socket
 import struct
 import sys
 import tempfile
+import zlib
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def socket_path() -> str:
-    """One server per user and checkout (a different tree never answers for this one)."""
+    """One server per user and checkout (a different tree never answers for this one); the
+    same rule as the client's (bin/cutadapt _sock_path)."""
     env = os.environ.get("DMX_DAEMON_SOCK")
     if env:
         return env
-    tag = hashlib.sha1(PKG.encode()).hexdigest()[:12]
-    return os.path.join(tempfile.gettempdir(), f"dmx-{os.getuid()}-{tag}.sock")
+    tmp = "/tmp"
+    for k in ("TMPDIR", "TEMP", "TMP"):
+        d = os.environ.get(k)
+        if d and os.path.isdir(d):
+            tmp = d
+            break
+    return os.path.join(tmp, f"dmx-{os.getuid()}-{zlib.crc32(PKG.encode()):08x}.sock")
 
 
 def _recv_exact(conn, n: int) -> bytes:
