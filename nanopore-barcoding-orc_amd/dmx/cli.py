@@ -63,7 +63,7 @@ def build_parser():
                    action="store_true")
     p.add_argument("--match-read-wildcards", action="store_true")
     p.add_argument("--device", type=int, default=None)
-    p.add_argument("--batch-mb", type=int, default=256)
+    p.add_argument("--batch-mb", type=int, default=None)
     p.add_argument("input")
     return p
 
@@ -168,7 +168,7 @@ def run(argv=None, keep_contexts: bool = False) -> int:
     _phase("sink", marks)
     tw = [0.0, 0.0, 0.0]   # read wait, GPU, plan + write enqueue
     try:
-        with nio.Reader(args.input, args.batch_mb << 20, threads=args.cores) as reader:
+        with nio.Reader(args.input, _batch_bytes(args), threads=args.cores) as reader:
             _phase("reader", marks)
             t = time.perf_counter()
             for batch in reader:
@@ -215,6 +215,23 @@ def run(argv=None, keep_contexts: bool = False) -> int:
         print("dmx cli phases: " + " ".join(f"{k}={v:.3f}" for k, v in marks) +
               f" exec_to_import={_EXEC_TO_IMPORT:.2f}", file=sys.stderr)
     return 0
+
+
+def _batch_bytes(args) -> int:
+    """Reader batch size: --batch-mb / DMX_BATCH_MB, else about a quarter of the input (32..256
+    MB), so that a round-2 call's ~200 MB bin is read, demultiplexed and written as a pipeline
+    of batches (reading batch i+1 while batch i is written) instead of one batch in series.
+    Large inputs keep 256 MB batches (fewer per-batch thread fan-outs)."""
+    mb = args.batch_mb or int(os.environ.get("DMX_BATCH_MB", "0") or 0)
+    if mb > 0:
+        return mb << 20
+    try:
+        size = os.path.getsize(args.input)
+    except OSError:
+        return 256 << 20
+    if args.input.endswith(".gz"):
+        size *= 2                     # FASTQ deflates to about half
+    return int(min(256 << 20, max(32 << 20, size // 4)))
 
 
 def _devices(args) -> list:

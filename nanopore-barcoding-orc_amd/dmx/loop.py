@@ -56,7 +56,7 @@ def build_parser():
     p.add_argument("--no-cleanup", action="store_true",
                    help="keep the unknown and SP27_009..012 outputs (:107-119 delete them)")
     p.add_argument("--compression-level", type=int, default=1)
-    p.add_argument("--batch-mb", type=int, default=256)
+    p.add_argument("--batch-mb", type=int, default=int(os.environ.get("DMX_BATCH_MB", "256")))
     p.add_argument("--device", type=int, default=None)
     return p
 
