@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -86,17 +87,84 @@ int clamp_threads(int t) {
 }
 
 // Run f(t) for t in [0, nth) on nth threads (the calling thread takes t = 0).
+// Persistent workers for parallel(): the reader and the writer fan out to -j threads several
+// times per batch (inflate, newline scan, parse, pack, render, compress), and with batches of a
+// few tens of MB (a round-2 call's bin) thread creation per fan-out became a visible cost.
+// Workers claim the indices of a fan-out from a shared counter; the caller claims too and then
+// waits for the indices the workers took, so concurrent fan-outs (reader and writer threads)
+// never wait on each other's queue position.
+struct WorkPool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    std::vector<std::thread> workers;
+    bool stop = false;
+    ~WorkPool() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : workers) t.join();
+    }
+    void loop() {
+        for (;;) {
+            std::function<void()> job;
+            {
+                std::unique_lock<std::mutex> l(mu);
+                cv.wait(l, [&] { return stop || !q.empty(); });
+                if (q.empty()) return;
+                job = std::move(q.front());
+                q.pop_front();
+            }
+            job();
+        }
+    }
+    void submit(int n, const std::function<void()>& job) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            while ((int)workers.size() < std::min(n, 255)) workers.emplace_back([this] { loop(); });
+            for (int i = 0; i < n; ++i) q.push_back(job);
+        }
+        if (n == 1) cv.notify_one();
+        else cv.notify_all();
+    }
+};
+WorkPool& work_pool() {
+    static WorkPool* p = new WorkPool();   // never destroyed: workers may outlive static dtors
+    return *p;
+}
+
 template <typename F>
 void parallel(int nth, F&& f) {
     if (nth <= 1) {
         f(0);
         return;
     }
-    std::vector<std::thread> th;
-    th.reserve(nth - 1);
-    for (int t = 1; t < nth; ++t) th.emplace_back([&f, t] { f(t); });
+    struct Group {
+        std::atomic<int> next{1};
+        int n = 0;
+        std::mutex m;
+        std::condition_variable cv;
+        int done = 0;
+        std::function<void(int)>* fn = nullptr;
+        void run_claimed() {   // claim and run indices until none is left
+            for (int t; (t = next.fetch_add(1)) < n;) {
+                (*fn)(t);
+                std::lock_guard<std::mutex> g(m);
+                if (++done == n - 1) cv.notify_all();
+            }
+        }
+    };
+    std::function<void(int)> fn = [&f](int t) { f(t); };
+    auto g = std::make_shared<Group>();
+    g->n = nth;
+    g->fn = &fn;
+    work_pool().submit(nth - 1, [g] { g->run_claimed(); });
     f(0);
-    for (auto& x : th) x.join();
+    g->run_claimed();
+    std::unique_lock<std::mutex> l(g->m);
+    g->cv.wait(l, [&] { return g->done == nth - 1; });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1017,7 +1085,7 @@ inline uint8_t* put_u32(uint8_t* p, uint32_t v) {
     return p;
 }
 
-constexpr size_t kMemberMax = 4u << 20;   // uncompressed bytes per gzip member
+constexpr size_t kMemberMax = 1u << 20;   // uncompressed bytes per gzip member
 
 inline void put32(uint8_t* p, uint32_t v) {
     p[0] = (uint8_t)v;
