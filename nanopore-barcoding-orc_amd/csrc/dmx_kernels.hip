@@ -868,6 +868,10 @@ __device__ __forceinline__ void filter_chunk(uint32_t codes, uint32_t nb, uint32
         cm = min(cm, S.e);
     }
     hits &= cnt >= 16 ? 0xFFFFu : (cnt > 0 ? (0xFFFFu << (16 - cnt)) & 0xFFFFu : 0u);
+    if constexpr (!CAREFUL) {   // warm-up columns (j <= hit_from) of a later segment never hit
+        const int nw = (int)hit_from - (int)p0;
+        hits &= nw >= 16 ? 0u : (nw <= 0 ? 0xFFFFu : (0xFFFFu >> nw));
+    }
     const int cb = cm + kf_far + 1;   // the chunk's minimum b: a lower bound of every hit's b
     while (hits) {
         const int q = (int)__clz(hits) - 16;
@@ -973,7 +977,10 @@ __device__ __forceinline__ void filter_segment(const RoundArgs& R, const TaskVie
         uint32_t vc[4], vn[4];
         if (rev) seg_extract<1>(B, vc, vn);
         else seg_extract<0>(B, vc, vn);
-        const bool careful = p0 == P0;                 // uniform: every lane's first 64
+        // per-column thresholds only near the view start (segment 0, grouped first in the
+        // block's task order, so the branch is wave-uniform but for one wave); later segments
+        // have threshold kf_far everywhere and mask their warm-up columns
+        const bool careful = p0 == P0 && hit_from == 0;
         for (int c = 0; c < 4; ++c) {
             const uint32_t pc = p0 + 16u * (uint32_t)c;
             const int cnt = (int)P1 - (int)pc;
@@ -1002,8 +1009,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     __shared__ __attribute__((aligned(16))) int8_t s_thr[kScanBlock];
     __shared__ Window s_win[kScanBlock / 64][kWaveWinCap];   // per-wave window staging
     __shared__ uint32_t s_wcnt[kScanBlock / 64];
-    __shared__ uint32_t s_pre[2][kSegViewsPerBlock];   // per strand: segments before view v
-    __shared__ uint32_t s_tot[2][kScanBlock];
+    // per strand: first segments (segment 0) and later segments before view v; the block's
+    // task order per strand is every view's segment 0, then every view's later segments
+    __shared__ uint32_t s_pre[2][kSegViewsPerBlock], s_prl[2][kSegViewsPerBlock];
+    __shared__ uint32_t s_tot[2][kScanBlock], s_totl[2][kScanBlock];
     const DevPanel* P = R.panel;
     const int no = P->n_orient;
     const uint32_t n_items = R.items ? *R.n_items_dev : R.n_items;
@@ -1035,7 +1044,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     constexpr int VPT = kSegViewsPerBlock / kScanBlock;   // 4 views per thread
     uint32_t cnt[VPT];
     int grp[VPT];
-    uint32_t sum0 = 0, sum1 = 0;
+    uint32_t sum0 = 0, sum1 = 0, suml0 = 0, suml1 = 0;
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {
         const uint32_t vl = threadIdx.x * VPT + e;
@@ -1049,38 +1058,60 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             cnt[e] = tv.len ? (tv.len + SEG - 1) / SEG : (P->where == kFront ? 0u : 1u);
             grp[e] = (int)tv.strand;
         }
-        if (grp[e]) sum1 += cnt[e];
-        else sum0 += cnt[e];
+        const uint32_t f = cnt[e] ? 1u : 0u, l = cnt[e] - f;
+        if (grp[e]) {
+            sum1 += f;
+            suml1 += l;
+        } else {
+            sum0 += f;
+            suml0 += l;
+        }
     }
     s_tot[0][threadIdx.x] = sum0;
     s_tot[1][threadIdx.x] = sum1;
+    s_totl[0][threadIdx.x] = suml0;
+    s_totl[1][threadIdx.x] = suml1;
     __syncthreads();
-    for (uint32_t d = 1; d < kScanBlock; d <<= 1) {   // inclusive Hillis-Steele scan
-        uint32_t x0 = 0, x1 = 0;
+    for (uint32_t d = 1; d < kScanBlock; d <<= 1) {   // inclusive Hillis-Steele scans
+        uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
         if (threadIdx.x >= d) {
             x0 = s_tot[0][threadIdx.x - d];
             x1 = s_tot[1][threadIdx.x - d];
+            y0 = s_totl[0][threadIdx.x - d];
+            y1 = s_totl[1][threadIdx.x - d];
         }
         __syncthreads();
         s_tot[0][threadIdx.x] += x0;
         s_tot[1][threadIdx.x] += x1;
+        s_totl[0][threadIdx.x] += y0;
+        s_totl[1][threadIdx.x] += y1;
         __syncthreads();
     }
     {
         uint32_t r0 = s_tot[0][threadIdx.x] - sum0, r1 = s_tot[1][threadIdx.x] - sum1;
+        uint32_t q0 = s_totl[0][threadIdx.x] - suml0, q1 = s_totl[1][threadIdx.x] - suml1;
 #pragma unroll
         for (int e = 0; e < VPT; ++e) {
             const uint32_t vl = threadIdx.x * VPT + e;
             if (vl < kSegViewsPerBlock) {
                 s_pre[0][vl] = r0;
                 s_pre[1][vl] = r1;
+                s_prl[0][vl] = q0;
+                s_prl[1][vl] = q1;
             }
-            if (grp[e]) r1 += cnt[e];
-            else r0 += cnt[e];
+            const uint32_t f = cnt[e] ? 1u : 0u, l = cnt[e] - f;
+            if (grp[e]) {
+                r1 += f;
+                q1 += l;
+            } else {
+                r0 += f;
+                q0 += l;
+            }
         }
     }
     __syncthreads();
-    const uint32_t T0 = s_tot[0][kScanBlock - 1], T1 = s_tot[1][kScanBlock - 1];
+    const uint32_t F0 = s_tot[0][kScanBlock - 1], F1 = s_tot[1][kScanBlock - 1];
+    const uint32_t T0 = F0 + s_totl[0][kScanBlock - 1], T1 = F1 + s_totl[1][kScanBlock - 1];
     const uint32_t wv = threadIdx.x >> 6;   // windows staged per wave: no block barriers below
     const uint32_t wsh = wave_shard();
     const WaveStage<Window, kWaveWinCap> st{s_win[wv], &s_wcnt[wv], R.win + wsh * R.win_scap,
@@ -1098,7 +1129,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     // 1: strand-1 segment tt), so both strands of the same reads are loaded together and the
     // second load of each byte hits in L2 (strand-major order re-read it from the fabric:
     // 1.8x the algorithmic bytes).  The strand branch stays wave-uniform.
-    const bool paired = T1 == T0 && T0 > 0;
+    const bool paired = T1 == T0 && F1 == F0 && T0 > 0;
     const uint32_t step = paired ? (uint32_t)kScanBlock / 2 : (uint32_t)kScanBlock;
     const uint32_t total = paired ? T0 : T0 + T1;
     for (uint32_t tb = 0; tb < total; tb += step) {
@@ -1116,15 +1147,21 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             tt = g ? t - T0 : t;
         }
         if (valid) {
-            // the last view whose segment prefix is <= tt (views of the other strand add 0)
+            // tasks [0, F_g): segment 0 of the views in order; then the later segments,
+            // view-major.  The view is the last one whose prefix is <= the index (views of the
+            // other strand, and views without such segments, add 0).
+            const uint32_t Fg = g ? F1 : F0;
+            const bool first = tt < Fg;
+            const uint32_t x = first ? tt : tt - Fg;
+            const uint32_t* pre = first ? s_pre[g] : s_prl[g];
             uint32_t lo = 0, hi = nv;                  // answer in [lo, hi)
             while (hi - lo > 1) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (s_pre[g][mid] <= tt) lo = mid;
+                if (pre[mid] <= x) lo = mid;
                 else hi = mid;
             }
             const uint32_t v = vbeg + lo;
-            const uint32_t k = tt - s_pre[g][lo];
+            const uint32_t k = first ? 0u : 1u + (x - pre[lo]);
             const uint32_t item = v / (uint32_t)no;
             const int o = (int)(v % (uint32_t)no);
             TaskView tv;
