@@ -1009,9 +1009,12 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     __shared__ __attribute__((aligned(16))) int8_t s_thr[kScanBlock];
     __shared__ Window s_win[kScanBlock / 64][kWaveWinCap];   // per-wave window staging
     __shared__ uint32_t s_wcnt[kScanBlock / 64];
-    // per strand: first segments (segment 0) and later segments before view v; the block's
-    // task order per strand is every view's segment 0, then every view's later segments
+    // Block task order per strand: every view's segment 0; then the middle segments (neither
+    // first nor last), view-major; then the views' last segments grouped by their number of
+    // 64-position steps (1..4), so the waves of short tails finish early.  s_pre / s_prl: first
+    // / middle segments before view v; s_lastv: the views of the last-segment region in order.
     __shared__ uint32_t s_pre[2][kSegViewsPerBlock], s_prl[2][kSegViewsPerBlock];
+    __shared__ uint16_t s_lastv[2][kSegViewsPerBlock];
     __shared__ uint32_t s_tot[2][kScanBlock], s_totl[2][kScanBlock];
     const DevPanel* P = R.panel;
     const int no = P->n_orient;
@@ -1042,13 +1045,14 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
 
     // segment counts per view, grouped by strand; block-wide exclusive scan
     constexpr int VPT = kSegViewsPerBlock / kScanBlock;   // 4 views per thread
-    uint32_t cnt[VPT];
+    uint32_t cnt[VPT], bk[VPT];
     int grp[VPT];
     uint32_t sum0 = 0, sum1 = 0, suml0 = 0, suml1 = 0;
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {
         const uint32_t vl = threadIdx.x * VPT + e;
         cnt[e] = 0;
+        bk[e] = 0;
         grp[e] = 0;
         if (vl < nv) {
             const uint32_t v = vbeg + vl;
@@ -1057,8 +1061,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             // an empty view of a 3' panel still gets its last-column window (one segment)
             cnt[e] = tv.len ? (tv.len + SEG - 1) / SEG : (P->where == kFront ? 0u : 1u);
             grp[e] = (int)tv.strand;
+            if (cnt[e] >= 2)   // last segment: positions [seg0 - W, len), in 64-position steps
+                bk[e] = (tv.len - (cnt[e] - 1u) * SEG + W + 63u) / 64u;
         }
-        const uint32_t f = cnt[e] ? 1u : 0u, l = cnt[e] - f;
+        const uint32_t f = cnt[e] ? 1u : 0u, l = cnt[e] >= 2 ? cnt[e] - 2u : 0u;
         if (grp[e]) {
             sum1 += f;
             suml1 += l;
@@ -1099,7 +1105,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                 s_prl[0][vl] = q0;
                 s_prl[1][vl] = q1;
             }
-            const uint32_t f = cnt[e] ? 1u : 0u, l = cnt[e] - f;
+            const uint32_t f = cnt[e] ? 1u : 0u, l = cnt[e] >= 2 ? cnt[e] - 2u : 0u;
             if (grp[e]) {
                 r1 += f;
                 q1 += l;
@@ -1111,7 +1117,67 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     }
     __syncthreads();
     const uint32_t F0 = s_tot[0][kScanBlock - 1], F1 = s_tot[1][kScanBlock - 1];
-    const uint32_t T0 = F0 + s_totl[0][kScanBlock - 1], T1 = F1 + s_totl[1][kScanBlock - 1];
+    const uint32_t M0 = s_totl[0][kScanBlock - 1], M1 = s_totl[1][kScanBlock - 1];
+    __syncthreads();
+    // last segments per (strand, step bucket): 16-bit fields, buckets 1|2 in s_tot, 3|4 in
+    // s_totl (a block has <= 1024 views, so no field overflows)
+    uint32_t bl[2] = {0u, 0u}, bh[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < VPT; ++e) {
+        if (!bk[e]) continue;
+        const uint32_t one = 1u << (16u * ((bk[e] - 1u) & 1u));
+        if (bk[e] <= 2) bl[grp[e]] += one;
+        else bh[grp[e]] += one;
+    }
+    s_tot[0][threadIdx.x] = bl[0];
+    s_tot[1][threadIdx.x] = bl[1];
+    s_totl[0][threadIdx.x] = bh[0];
+    s_totl[1][threadIdx.x] = bh[1];
+    __syncthreads();
+    for (uint32_t d = 1; d < kScanBlock; d <<= 1) {
+        uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
+        if (threadIdx.x >= d) {
+            x0 = s_tot[0][threadIdx.x - d];
+            x1 = s_tot[1][threadIdx.x - d];
+            y0 = s_totl[0][threadIdx.x - d];
+            y1 = s_totl[1][threadIdx.x - d];
+        }
+        __syncthreads();
+        s_tot[0][threadIdx.x] += x0;
+        s_tot[1][threadIdx.x] += x1;
+        s_totl[0][threadIdx.x] += y0;
+        s_totl[1][threadIdx.x] += y1;
+        __syncthreads();
+    }
+    uint32_t LB[2][5];   // region base of each step bucket, LB[g][4] = the region's size
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        const uint32_t lo = s_tot[g][kScanBlock - 1], hi = s_totl[g][kScanBlock - 1];
+        LB[g][0] = 0;
+        LB[g][1] = lo & 0xFFFFu;
+        LB[g][2] = LB[g][1] + (lo >> 16);
+        LB[g][3] = LB[g][2] + (hi & 0xFFFFu);
+        LB[g][4] = LB[g][3] + (hi >> 16);
+    }
+    {
+        uint32_t xl[2], xh[2];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            xl[g] = s_tot[g][threadIdx.x] - bl[g];
+            xh[g] = s_totl[g][threadIdx.x] - bh[g];
+        }
+#pragma unroll
+        for (int e = 0; e < VPT; ++e) {
+            if (!bk[e]) continue;
+            const int g = grp[e];
+            const uint32_t b = bk[e] - 1u, sh = 16u * (b & 1u);
+            uint32_t& x = b < 2 ? xl[g] : xh[g];
+            s_lastv[g][LB[g][b] + ((x >> sh) & 0xFFFFu)] = (uint16_t)(threadIdx.x * VPT + e);
+            x += 1u << sh;
+        }
+    }
+    __syncthreads();
+    const uint32_t T0 = F0 + M0 + LB[0][4], T1 = F1 + M1 + LB[1][4];
     const uint32_t wv = threadIdx.x >> 6;   // windows staged per wave: no block barriers below
     const uint32_t wsh = wave_shard();
     const WaveStage<Window, kWaveWinCap> st{s_win[wv], &s_wcnt[wv], R.win + wsh * R.win_scap,
@@ -1129,7 +1195,8 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     // 1: strand-1 segment tt), so both strands of the same reads are loaded together and the
     // second load of each byte hits in L2 (strand-major order re-read it from the fabric:
     // 1.8x the algorithmic bytes).  The strand branch stays wave-uniform.
-    const bool paired = T1 == T0 && F1 == F0 && T0 > 0;
+    const bool paired = T1 == T0 && F1 == F0 && M1 == M0 && LB[0][1] == LB[1][1] &&
+                        LB[0][2] == LB[1][2] && LB[0][3] == LB[1][3] && T0 > 0;
     const uint32_t step = paired ? (uint32_t)kScanBlock / 2 : (uint32_t)kScanBlock;
     const uint32_t total = paired ? T0 : T0 + T1;
     for (uint32_t tb = 0; tb < total; tb += step) {
@@ -1150,22 +1217,29 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             // tasks [0, F_g): segment 0 of the views in order; then the later segments,
             // view-major.  The view is the last one whose prefix is <= the index (views of the
             // other strand, and views without such segments, add 0).
-            const uint32_t Fg = g ? F1 : F0;
-            const bool first = tt < Fg;
-            const uint32_t x = first ? tt : tt - Fg;
-            const uint32_t* pre = first ? s_pre[g] : s_prl[g];
-            uint32_t lo = 0, hi = nv;                  // answer in [lo, hi)
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (pre[mid] <= x) lo = mid;
-                else hi = mid;
+            const uint32_t Fg = g ? F1 : F0, Mg = g ? M1 : M0;
+            uint32_t lo = 0, k;
+            if (tt >= Fg + Mg) {                       // last segments, by step bucket
+                lo = s_lastv[g][tt - Fg - Mg];
+                k = 0xFFFFFFFFu;                       // (set from the view's length below)
+            } else {
+                const bool first = tt < Fg;
+                const uint32_t x = first ? tt : tt - Fg;
+                const uint32_t* pre = first ? s_pre[g] : s_prl[g];
+                uint32_t hi = nv;                      // answer in [lo, hi)
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (pre[mid] <= x) lo = mid;
+                    else hi = mid;
+                }
+                k = first ? 0u : 1u + (x - pre[lo]);
             }
             const uint32_t v = vbeg + lo;
-            const uint32_t k = first ? 0u : 1u + (x - pre[lo]);
             const uint32_t item = v / (uint32_t)no;
             const int o = (int)(v % (uint32_t)no);
             TaskView tv;
             task_view(R, item, o * A, A, tv);
+            if (k == 0xFFFFFFFFu) k = (tv.len + SEG - 1) / SEG - 1u;
             const uint32_t seg0 = k * SEG;
             const uint32_t P0 = k ? seg0 - W : 0u;
             const uint32_t P1 = min(tv.len, seg0 + SEG);
