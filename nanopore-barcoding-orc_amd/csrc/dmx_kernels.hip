@@ -762,7 +762,10 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
 // segment boundary.  Segments are ordered strand 0 first, then strand 1, so the strand branch is
 // wave-uniform except in one wave per block.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kSegViewsPerBlock = 1024;
+#ifndef DMX_SEG_VIEWS
+#define DMX_SEG_VIEWS 1024
+#endif
+constexpr uint32_t kSegViewsPerBlock = DMX_SEG_VIEWS;   // views per filter block (>= 256)
 constexpr int kSegSpan = 256;                 // view positions loaded per segment (S + W)
 
 __device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskView& tv,
@@ -1044,7 +1047,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     }
 
     // segment counts per view, grouped by strand; block-wide exclusive scan
-    constexpr int VPT = kSegViewsPerBlock / kScanBlock;   // 4 views per thread
+    constexpr int VPT = kSegViewsPerBlock / kScanBlock;   // views per thread
     uint32_t cnt[VPT], bk[VPT];
     int grp[VPT];
     uint32_t sum0 = 0, sum1 = 0, suml0 = 0, suml1 = 0;
