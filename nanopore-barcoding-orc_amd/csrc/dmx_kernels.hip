@@ -763,7 +763,7 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
 // wave-uniform except in one wave per block.
 // ---------------------------------------------------------------------------------------------
 #ifndef DMX_SEG_VIEWS
-#define DMX_SEG_VIEWS 1024
+#define DMX_SEG_VIEWS 512
 #endif
 constexpr uint32_t kSegViewsPerBlock = DMX_SEG_VIEWS;   // views per filter block (>= 256)
 constexpr int kSegSpan = 256;                 // view positions loaded per segment (S + W)
