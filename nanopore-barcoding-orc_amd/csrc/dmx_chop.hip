@@ -60,7 +60,10 @@ namespace dmx {
 
 constexpr int kChopMaxLabels = 2 * DMX_CHOP_MAX_PRIMERS;
 constexpr int kChopMaxRules = DMX_CHOP_MAX_RULES;
-constexpr uint32_t kChopSeg = 512;       // columns owned by one scan lane
+#ifndef DMX_CHOP_SEG
+#define DMX_CHOP_SEG 512
+#endif
+constexpr uint32_t kChopSeg = DMX_CHOP_SEG;   // columns owned by one scan lane
 constexpr int kChopBlock = 256;
 constexpr uint32_t kChopReads = 64;      // reads per block (first launch)
 constexpr uint32_t kChopHitCap = 512;    // LDS hit list per block
