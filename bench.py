@@ -7,8 +7,13 @@ of one resident batch of synthetic reads — the work of scripts/02_cutadapt_loo
 Workload (default, BASELINE.json configs[1]): 10M synthetic ONT reads per GPU, lognormal
 length mean 1.2 kb, synthetic 24 x 24 M13 panel, -e 0.1, --rc.
 
-Multi-GPU (torchrun): one process per GPU, reads sharded by contiguous range (rank r processes
-reads [r*N, (r+1)*N) of one seeded generation: weak scaling), one RCCL all-reduce of the
+Multi-GPU: one process per GPU, started by torchrun (the driver) or, for `--gpus N` without
+WORLD_SIZE, by this script itself (N child processes spawned before anything touches the GPU;
+never an exec).  `--gpus` must equal WORLD_SIZE when both are given.  Reads are sharded by
+contiguous range: by default every rank processes `--reads` reads (rank r takes reads
+[r*N, (r+1)*N) of one seeded generation: weak scaling); with `--reads-total T` the T reads of
+one generation are split over the ranks balanced on the sum of read lengths (BASELINE
+configs[2], "10M reads sharded across 8 GPUs": strong scaling).  One RCCL all-reduce of the
 per-bin counts per step inside libdmx (dmx_allreduce_counts on the library's stream; the only
 exchange the path has).  torch.distributed (gloo) is the control plane only: it hands rank 0's
 RCCL id to the other ranks, and carries the barrier and the max-over-ranks time.  At N=1 the
@@ -28,6 +33,66 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "nanopore-barcoding-orc_amd"))
+
+
+def host_cores() -> tuple[int, str]:
+    """Physical host cores this process may use: min(physical cores of the CPUs in its affinity
+    set, the affinity set, the cgroup CPU quota); with how each was found."""
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = list(range(os.cpu_count() or 1))
+    phys = set()
+    try:   # (package, core) of every allowed logical CPU
+        for cpu in aff:
+            base = f"/sys/devices/system/cpu/cpu{cpu}/topology/"
+            with open(base + "physical_package_id") as a, open(base + "core_id") as b:
+                phys.add((a.read().strip(), b.read().strip()))
+    except OSError:
+        phys = set()
+    quota = None
+    try:   # cgroup v2 cpu.max: "<quota> <period>" or "max <period>"
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    cands = [len(aff)] + ([len(phys)] if phys else []) + ([quota] if quota else [])
+    n = max(1, min(cands))
+    how = (f"{len(aff)} logical CPUs in the affinity set, "
+           f"{len(phys) if phys else 'unknown'} physical cores among them, "
+           f"cgroup quota {quota if quota else 'none'}")
+    return n, how
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* as torchrun sets them) before this process touches the GPU, wait for
+    them, and return the worst exit status.  Rank 0 prints the JSON line."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+                if codes[i] not in (None, 0):   # one rank failed: the others would hang
+                    for q in procs:
+                        if q.poll() is None:
+                            q.send_signal(signal.SIGTERM)
+        time.sleep(0.1)
+    return max((abs(c) for c in codes), default=0)
 
 METRIC = "Mreads/s two-round SP5×SP27 demux; % HBM roofline; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -132,9 +197,9 @@ def kernel_table(workload: str, reads: int, stage: dict, K: int, step_ms: float)
     return out
 
 
-def cpu_baseline(workload: str, threads: int, target_s: float = 12.0):
+def cpu_baseline(workload: str, threads: int, cores_how: str, target_s: float = 12.0):
     """Oracle (CPU restatement of cutadapt 4.9, C, pthreads) on a bounded sample of the same
-    workload.  rank 0, N=1 only."""
+    workload, one thread per physical host core available.  rank 0, N=1 only."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: timed CPU baseline only
     from dmx import synth
@@ -154,12 +219,12 @@ def cpu_baseline(workload: str, threads: int, target_s: float = 12.0):
     what = "linked -g F...R, no --rc" if linked else "two rounds, --rc"
     return {"value": n / dt / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "port",
             "sample": f"{n} reads of workload {workload} (seed 98), {what}, -e 0.1, "
-                      f"{dt:.1f} s wall on {threads} host threads (oracle/cutadapt_oracle.c, "
-                      "a C restatement of cutadapt 4.9's Ukkonen-banded DP; cutadapt itself is "
-                      "not installed)"}
+                      f"{dt:.1f} s wall on {threads} host threads, one per physical core "
+                      f"available ({cores_how}) (oracle/cutadapt_oracle.c, a C restatement of "
+                      "cutadapt 4.9's Ukkonen-banded DP; cutadapt itself is not installed)"}
 
 
-def chop_cpu_baseline(threads: int, cutoff: float, target_s: float = 12.0):
+def chop_cpu_baseline(threads: int, cores_how: str, cutoff: float, target_s: float = 12.0):
     """Oracle primer-hit search (oracle/chop_oracle.c, plain O(mn) DP on pthreads) on a bounded
     sample of the chop workload.  rank 0, N=1 only."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -179,8 +244,15 @@ def chop_cpu_baseline(threads: int, cutoff: float, target_s: float = 12.0):
     return {"value": n / dt / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "port",
             "sample": f"{n} reads of config 2 (seed 98): hits of SP5, SP27 and their reverse "
                       f"complements at cutoff {cutoff}, {dt:.1f} s wall on {threads} host threads "
-                      "(oracle/chop_oracle.c, a plain-DP restatement; pychopper / edlib are not "
-                      "installed)"}
+                      f"({cores_how}) (oracle/chop_oracle.c, a plain-DP restatement; pychopper / "
+                      "edlib are not installed)"}
+
+
+def reads_desc(args, what: str) -> str:
+    if args.scaling == "strong":
+        return (f"{args.total_reads} {what} in total, split over {len(args.shards)} GPU(s) by "
+                "sum of read lengths")
+    return f"{args.shards[0]} {what} per GPU"
 
 
 def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutoff, gen_s,
@@ -202,13 +274,14 @@ def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutof
                   "M13 SP5/SP27 primers)",
         "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
         "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u64",
         "data": "synthetic",
-        "config": {"workload": f"chop: {args.reads} synthetic ONT reads per GPU (config 2 "
+        "config": {"workload": f"chop: {reads_desc(args, 'synthetic ONT reads')} (config 2 "
                                "generator, both orientations), primers "
                                "M13_seqs_for_pychopper.fa, layout +:SP5,-SP27|-:SP27,-SP5, "
                                "-p, inputs resident in HBM",
-                   "cutoff": cutoff, "reads_per_gpu": args.reads, "parallelism": f"dp{world}"},
+                   "cutoff": cutoff, "reads_per_gpu": args.shards, "reads_total": args.total_reads,
+                   "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_source": traffic_src,
@@ -252,12 +325,13 @@ def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, 
     return {
         "metric": METRIC, "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
         "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u64",
         "data": "synthetic",
-        "config": {"workload": f"{args.workload}: {args.reads} synthetic ONT reads per GPU "
+        "config": {"workload": f"{args.workload}: {reads_desc(args, 'synthetic ONT reads')} "
                                "(SURVEY.md §8d), two-round SP5 x SP27 demux, -e 0.1 --rc, "
                                "inputs resident in HBM",
-                   "panel": f"{A0}x{A1}", "reads_per_gpu": args.reads,
+                   "panel": f"{A0}x{A1}", "reads_per_gpu": args.shards,
+                   "reads_total": args.total_reads,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
@@ -304,12 +378,13 @@ def linked_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen
         "metric": "Mreads/s linked-primer trimming (config 5, cutadapt -g F...R per pair)",
         "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
         "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u64",
         "data": "synthetic",
-        "config": {"workload": f"c5: {args.reads} synthetic COI consensuses per GPU (SURVEY.md "
+        "config": {"workload": f"c5: {reads_desc(args, 'synthetic COI consensuses')} (SURVEY.md "
                                "§8d config 5), linked COI_primers.fa pairs, -e 0.1, no --rc, "
                                "inputs resident in HBM",
-                   "pairs": A0, "reads_per_gpu": args.reads, "parallelism": f"dp{world}"},
+                   "pairs": A0, "reads_per_gpu": args.shards, "reads_total": args.total_reads,
+                   "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
                      "algorithmic_bytes_per_launch": round(alg_bytes),
@@ -323,7 +398,9 @@ def linked_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="number of ranks (one per GPU); default WORLD_SIZE or 1.  Without a "
+                         "launcher, N > 1 starts N rank processes itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="c2x24",
@@ -331,14 +408,29 @@ def main():
                     help="c5 = config 5, linked COI primers (-g F...R) on consensus FASTA; "
                          "chop = pychopper-style reorientation (01_pychopper.sh) of config 2's "
                          "reads")
-    ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU")
+    ap.add_argument("--reads", type=int, default=10_000_000,
+                    help="reads per GPU (weak scaling)")
+    ap.add_argument("--reads-total", type=int, default=None,
+                    help="strong scaling: this many reads in total, split over the ranks in "
+                         "contiguous ranges balanced on the sum of read lengths (BASELINE "
+                         "configs[2]: --reads-total 10000000 on 8 GPUs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="threads of the CPU baseline; default one per physical host core "
+                         "available to this process")
     ap.add_argument("--no-pcie", action="store_true",
                     help="skip the PCIe-inclusive dmx_run after the timed region")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))   # nothing has touched the GPU in this process
+    world = int(env_world or 1)
+    if args.gpus is not None and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher must start "
+                 "one process per GPU (torchrun --nproc-per-node N), or run without a launcher")
+    if args.gpus is not None and args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -360,8 +452,20 @@ def main():
     gen_threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
     t0 = time.perf_counter()
     chop_mode = args.workload == "chop"
-    d = synth.generate("c2" if chop_mode else args.workload, n=args.reads,
-                       first=rank * args.reads, threads=gen_threads)
+    gen_cfg = "c2" if chop_mode else args.workload
+    if args.reads_total is not None:   # strong scaling: one generation split over the ranks
+        bounds = synth.shard_bounds(gen_cfg, args.reads_total, world)
+        first, n_local = bounds[rank], bounds[rank + 1] - bounds[rank]
+        args.shards = [bounds[r + 1] - bounds[r] for r in range(world)]
+        args.total_reads = args.reads_total
+        args.scaling = "strong"
+    else:                              # weak scaling: args.reads per rank
+        first, n_local = rank * args.reads, args.reads
+        args.shards = [args.reads] * world
+        args.total_reads = args.reads * world
+        args.scaling = "weak"
+    args.reads = n_local               # this rank's reads (PMC tables are keyed by it)
+    d = synth.generate(gen_cfg, n=n_local, first=first, threads=gen_threads)
     packed = lib.pack(d["blob"], d["offsets"], d["lengths"])
     tune = None
     if chop_mode:   # the CLI's autotune sample: the first 10000 reads
@@ -448,8 +552,7 @@ def main():
         elapsed = float(tt.item())
 
     K = args.steps
-    total_reads = args.reads * world * K
-    value = total_reads / elapsed / 1e6
+    value = args.total_reads * K / elapsed / 1e6
     if linked:
         out = linked_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s)
     else:
@@ -471,7 +574,7 @@ def main():
             tt = torch.tensor([pe], dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             pe = float(tt.item())
-        pcie = {"value": round(args.reads * world / pe / 1e6, 4), "unit": "Mreads/s",
+        pcie = {"value": round(args.total_reads / pe / 1e6, 4), "unit": "Mreads/s",
                 "ms": round(pe * 1e3, 3),
                 "chunk_reads": int(os.environ.get("DMX_RUN_CHUNK", 1 << 21)),
                 # 2-bit codes, the data half of the 1-bit mask, offsets, lengths
@@ -490,7 +593,10 @@ def main():
     if pcie is not None:
         out["pcie_inclusive"] = pcie
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_threads)
+        cores, how = host_cores()
+        if args.cpu_threads:
+            cores, how = args.cpu_threads, f"--cpu-threads {args.cpu_threads}; detected: {how}"
+        out["cpu_baseline"] = cpu_baseline(args.workload, cores, how)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
@@ -538,11 +644,14 @@ def chop_main(args, ctx, packed, tune, lengths, gen_s, world, rank, dist, on_gpu
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     K = args.steps
-    value = args.reads * world * K / elapsed / 1e6
+    value = args.total_reads * K / elapsed / 1e6
     out = chop_line(args, world, K, value, elapsed, ms, lengths, tot[0], tot[1], cutoff, gen_s,
                     [len(p[1]) for p in primers for _ in (0, 1)])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = chop_cpu_baseline(args.cpu_threads, cutoff)
+        cores, how = host_cores()
+        if args.cpu_threads:
+            cores, how = args.cpu_threads, f"--cpu-threads {args.cpu_threads}; detected: {how}"
+        out["cpu_baseline"] = chop_cpu_baseline(cores, how, cutoff)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -94,7 +94,9 @@ int dmx_pack(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens
 
 /* Replaces: the per-read hot loop of one or more cutadapt runs (ReverseComplementer ->
  * AdapterCutter.best_match -> Adapter.match_to -> Aligner.locate, for every read) for the whole
- * input.  Synchronous: uploads, runs both rounds on the GPU, downloads `out`. */
+ * input.  Synchronous: uploads, runs both rounds on the GPU, downloads `out`.  Any offsets >= 16
+ * that fit n_words are accepted; batches in dmx_pack's layout above 1.5 chunks (DMX_RUN_CHUNK
+ * reads, default 2^21) run as overlapped chunks, others in one shot (same results). */
 int dmx_run(dmx_ctx* ctx, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
             const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out);
 

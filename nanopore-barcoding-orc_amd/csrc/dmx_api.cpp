@@ -79,10 +79,14 @@ int ensure_pipeline(Ctx* c) {
     const size_t items = linked ? slots0 : n;
     // non-linked rounds may need one winner slot per (item, orientation): see orient_slot
     const size_t need = std::max(slots0, items) * (linked ? 1 : 2);
-    if (c->slot_cap < need || !c->d_res || c->cap_reads < n) {
-        const size_t s = need;
+    if (!c->d_res || c->res_cap < n) {   // the resident input set's result array
         int rc;
         if ((rc = dev_alloc(c, &c->d_res, n))) return rc;
+        c->res_cap = n;
+    }
+    if (c->slot_cap < need || c->cap_reads < n) {
+        const size_t s = need;
+        int rc;
         for (int r = 0; r < 2; ++r) {
             if ((rc = dev_alloc(c, &c->d_winner[r], s))) return rc;
             if ((rc = dev_alloc(c, &c->d_origin[r], s))) return rc;
@@ -210,6 +214,7 @@ int reset_counts(Ctx* c) {
     }
     CK(hipMemsetAsync(c->d_counts, 0, nc * sizeof(unsigned long long), c->stream));
     CK(hipStreamSynchronize(c->stream));
+    c->counts_reduced = false;
     return DMX_OK;
 }
 
@@ -570,10 +575,10 @@ int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uin
     if (c->d_nmask_alloc && c->n_words > nmw)
         CK(hipMemsetAsync(c->d_nmask + nmw, 0, (std::min(c->n_words, c->cap_words) - nmw) * 4,
                           c->stream));
-    if (!c->d_offs || c->cap_reads < n_reads) {
+    if (!c->d_offs || c->in_cap_reads < n_reads) {
         if ((rc = dev_alloc(c, &c->d_offs, n_reads))) return rc;
         if ((rc = dev_alloc(c, &c->d_lens, n_reads))) return rc;
-        c->cap_reads = 0;   // force pipeline re-allocation
+        c->in_cap_reads = n_reads;
     }
     c->n_reads = n_reads;
     c->n_words = n_words;
@@ -604,6 +609,7 @@ int dmx_exec(dmx_ctx* c) {
     CK(hipMemsetAsync(c->d_counters, 0, 32 * sizeof(uint32_t), st));
     CK(hipMemsetAsync(c->d_shard, 0, kShLists * kShards * kShardStride * sizeof(uint32_t), st));
     CK(hipMemsetAsync(c->d_counts, 0, c->n_counts * sizeof(unsigned long long), st));
+    c->counts_reduced = false;
     // A panel whose accepted matches can score <= 0 keeps one winner per orientation:
     // ReverseComplementer compares the two orientations' best scores with "no match" = 0, so
     // a read whose only forward match scores -1 is taken reverse-complemented (and unmatched).
@@ -781,6 +787,8 @@ void swap_inputs(Ctx* c) {
     std::swap(c->d_lens, c->alt.lens);
     std::swap(c->d_res, c->alt.res);
     std::swap(c->cap_words, c->alt.cap_words);
+    std::swap(c->in_cap_reads, c->alt.cap_reads);
+    std::swap(c->res_cap, c->alt.res_cap);
     std::swap(c->n_words, c->alt.n_words);
     c->d_seq = c->d_seq_alloc + kGuardWords;
     c->d_nmask = c->d_nmask_alloc + kGuardWords;
@@ -821,6 +829,8 @@ int alloc_set(Ctx* c, size_t words, size_t reads) {
     c->d_seq = c->d_seq_alloc + kGuardWords;
     c->d_nmask = c->d_nmask_alloc + kGuardWords;
     c->cap_words = words;
+    c->in_cap_reads = reads;
+    c->res_cap = reads;
     c->n_words = 0;
     CK(hipStreamSynchronize(c->stream));
     return DMX_OK;
@@ -864,18 +874,18 @@ int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const 
     CK(hipSetDevice(c->device));
     if (!c->cstream) CK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
     int rc;
-    // both sets sized for the largest chunk (the resident set's read capacity is cap_reads,
-    // shared with the pipeline buffers; the second set's is alt.cap_reads)
-    if (c->cap_words < maxw || c->cap_reads < maxn || !c->d_offs || !c->d_res) {
+    // both sets sized for the largest chunk; each set's capacities travel with its buffers
+    // (swap_inputs), apart from the pipeline's cap_reads
+    if (c->cap_words < maxw || c->in_cap_reads < maxn || c->res_cap < maxn || !c->d_offs ||
+        !c->d_res) {
         if ((rc = alloc_set(c, maxw, maxn))) return rc;
-        c->cap_reads = maxn;
     }
-    if (c->alt.cap_words < maxw || c->alt.cap_reads < maxn || !c->alt.offs || !c->alt.res) {
+    if (c->alt.cap_words < maxw || c->alt.cap_reads < maxn || c->alt.res_cap < maxn ||
+        !c->alt.offs || !c->alt.res) {
         swap_inputs(c);
         rc = alloc_set(c, maxw, maxn);
         swap_inputs(c);
         if (rc) return rc;
-        c->alt.cap_reads = maxn;
     }
     c->n_reads = maxn;
     chop_invalidate(c);
@@ -933,6 +943,7 @@ int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const 
                      hipMemcpyDeviceToHost));
     }
     CK(hipMemcpy(c->d_counts, total.data(), total.size() * 8, hipMemcpyHostToDevice));
+    c->counts_reduced = false;
     c->chunked = true;
     return DMX_OK;
 }
@@ -944,7 +955,12 @@ int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint
     if (!c || (n_reads && (!seq2b || !nmask || !offsets || !lens || !out))) return DMX_E_INVALID;
     size_t per = (size_t)1 << 21;   // reads per chunk of an overlapped run
     if (const char* e = std::getenv("DMX_RUN_CHUNK")) per = (size_t)std::strtoull(e, nullptr, 10);
-    if (per > 0 && n_reads > per + per / 2) {
+    // chunking rebases every chunk on a 32-nt boundary, which needs dmx_pack's layout at the
+    // chunk starts; any other (caller-packed) batch runs in one shot, whatever its size
+    bool chunkable = per > 0 && n_reads > per + per / 2;
+    for (size_t lo = 0; chunkable && lo < n_reads; lo += per)
+        chunkable = offsets[lo] >= (uint64_t)DMX_PACK_PAD && offsets[lo] % kPackAlign == 0;
+    if (chunkable) {
         if (!c->panel[0].set || (c->mode != DMX_MODE_SINGLE && !c->panel[1].set)) {
             c->err = "panels not set for this mode";
             return DMX_E_STATE;

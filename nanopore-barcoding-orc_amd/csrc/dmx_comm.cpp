@@ -127,9 +127,14 @@ int dmx_allreduce_counts(dmx_ctx* c, uint64_t* out, size_t n_out) {
         return DMX_E_INVALID;
     }
     if (hipSetDevice(c->device) != hipSuccess) return DMX_E_HIP;
-    const ncclResult_t r = ncclAllReduce(c->d_counts, c->d_counts, c->n_counts, ncclUint64,
-                                         ncclSum, c->comm, c->stream);
-    if (r != ncclSuccess) return nccl_fail(c, "ncclAllReduce", r);
+    // idempotent per exec: a second call returns the summed counts without summing them again
+    // (every rank follows the same call sequence, so either all ranks reduce or none does)
+    if (!c->counts_reduced) {
+        const ncclResult_t r = ncclAllReduce(c->d_counts, c->d_counts, c->n_counts, ncclUint64,
+                                             ncclSum, c->comm, c->stream);
+        if (r != ncclSuccess) return nccl_fail(c, "ncclAllReduce", r);
+        c->counts_reduced = true;
+    }
     if (out &&
         hipMemcpyAsync(out, c->d_counts, c->n_counts * 8, hipMemcpyDeviceToHost, c->stream) !=
             hipSuccess) {

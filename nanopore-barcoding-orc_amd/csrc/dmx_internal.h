@@ -38,7 +38,10 @@ struct Ctx {
 
     // resident batch
     size_t n_reads = 0, n_words = 0;
-    size_t cap_reads = 0, cap_words = 0;
+    size_t cap_reads = 0;     // pipeline buffers (winner slots, items, linked keys)
+    size_t cap_words = 0;     // d_seq / d_nmask of the resident input set
+    size_t in_cap_reads = 0;  // d_offs / d_lens of the resident input set
+    size_t res_cap = 0;       // d_res of the resident input set
     uint32_t* d_seq = nullptr;          // = d_seq_alloc + kGuardWords
     uint32_t* d_nmask = nullptr;
     uint32_t* d_seq_alloc = nullptr;    // packed buffers with zeroed guard words on both sides
@@ -55,7 +58,8 @@ struct Ctx {
         uint64_t* offs = nullptr;
         uint32_t* lens = nullptr;
         dmx_result* res = nullptr;
-        size_t cap_words = 0, cap_reads = 0, n_words = 0;
+        // capacities travel with their buffers (swap_inputs): words, offs/lens, res
+        size_t cap_words = 0, cap_reads = 0, res_cap = 0, n_words = 0;
     } alt;
     hipStream_t cstream = nullptr;      // copies of chunked runs
     bool chunked = false;               // the last dmx_run was chunked: dmx_fetch is refused
@@ -99,6 +103,7 @@ struct Ctx {
     ncclComm* comm = nullptr;
     int comm_ranks = 0, comm_rank = 0;
     uint64_t comm_group = 0;     // nonzero: made by dmx_comm_init_all (one process, grouped calls)
+    bool counts_reduced = false; // d_counts already summed over the ranks (cleared by dmx_exec)
 };
 
 void chop_release(Ctx* c);

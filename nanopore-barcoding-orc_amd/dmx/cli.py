@@ -97,7 +97,10 @@ def _phase(name: str, marks: list):
         marks.append((name, time.perf_counter() - _T_IMPORT))
 
 
-_CTX_CACHE: dict = {}   # devices -> contexts kept by the resident server (dmx/daemon.py)
+_CTX_CACHE: dict = {}   # (devices, open-time settings) -> contexts kept by the resident server
+# the DMX_* switches dmx_open reads once per context (csrc/dmx_api.cpp dmx_open): a cached
+# context is reused only by calls with the same values
+OPEN_TIME_ENV = ("DMX_NO_FILTER", "DMX_NO_VERIFY", "DMX_RESOLVE", "DMX_NO_SCREEN")
 
 
 def close_cached_contexts():
@@ -105,6 +108,16 @@ def close_cached_contexts():
         for c in ctxs:
             c.close()
     _CTX_CACHE.clear()
+
+
+def cached_group(devices) -> list:
+    """The resident server's contexts for these devices, opened under the current dmx_open-time
+    switches; one set (device memory) is kept at a time."""
+    key = (tuple(devices), tuple(os.environ.get(k, "") for k in OPEN_TIME_ENV))
+    if key not in _CTX_CACHE:
+        close_cached_contexts()
+        _CTX_CACHE[key] = lib.open_group(devices)
+    return _CTX_CACHE[key]
 
 
 def run(argv=None, keep_contexts: bool = False) -> int:
@@ -121,6 +134,10 @@ def run(argv=None, keep_contexts: bool = False) -> int:
         _unsupported("at least one -g/-a adapter is required")
     if not args.output:
         _unsupported("-o is required")
+    if "{name1}" in args.output or "{name2}" in args.output:
+        _unsupported("{name1}/{name2} (combinatorial demultiplexing of paired-end reads) is not "
+                     "implemented; single-end demultiplexing takes {name} (the fused two-round "
+                     "layout is bin/dmx-demux-loop)")
     aset = panel.AdapterSet()
     for where, spec in args.adapters:
         aset.add_spec(spec, where)
@@ -134,10 +151,7 @@ def run(argv=None, keep_contexts: bool = False) -> int:
     _phase("args", marks)
     devices = _devices(args)
     if keep_contexts:   # the server's contexts (panels and mode are set again below)
-        key = tuple(devices)
-        if key not in _CTX_CACHE:
-            _CTX_CACHE[key] = lib.open_group(devices)
-        ctxs = _CTX_CACHE[key]
+        ctxs = cached_group(devices)
     else:
         ctxs = lib.open_group(devices)
     _phase("open", marks)

@@ -10,8 +10,19 @@ stderr and exit status. The first call starts the server; it exits after `idle` 
 without a request. `DMX_DAEMON=0` makes every call run in its own process (the behaviour is
 the same either way; tests cover both).
 
+Isolation: one server per (user, checkout, SLURM job, GPU visibility). The socket name hashes
+SLURM_JOB_ID and the GPU-visibility variables (HIP/ROCR/CUDA_VISIBLE_DEVICES,
+GPU_DEVICE_ORDINAL), so a job never talks to another job's server (which would use the other
+job's GPUs and die with it, `04_cleaning_primers.sh:4,7` is a 96-task array), and the server,
+spawned by its first client, sees exactly the devices its callers see. A request is served
+with only its own DMX_* variables; contexts are cached per (devices, dmx_open-time switches).
+One request runs at a time: a call that arrives while another is running is answered "busy"
+and the client runs it in its own process instead of queueing. After a GPU error the server
+closes its contexts and exits, so the next call starts a fresh process.
+
 Protocol: request = u32 length + JSON {"argv", "cwd", "env"}; reply = frames u8 tag + u32 length
-+ payload, tags b"o" (stdout bytes), b"e" (stderr bytes), b"x" (exit status as text)."""
++ payload, tags b"o" (stdout bytes), b"e" (stderr bytes), b"x" (exit status as text), or a
+single b"b" frame (busy: run in-process)."""
 from __future__ import annotations
 
 import json
@@ -20,24 +31,33 @@ import socket
 import struct
 import sys
 import tempfile
+import threading
+import time
 import zlib
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def socket_path() -> str:
-    """One server per user and checkout (a different tree never answers for this one); the
-    same rule as the client's (bin/cutadapt _sock_path)."""
-    env = os.environ.get("DMX_DAEMON_SOCK")
-    if env:
-        return env
+# variables that decide which GPUs a process sees (and so which server may serve it)
+VISIBILITY_ENV = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+                  "GPU_DEVICE_ORDINAL")
+
+
+def socket_path(env=None) -> str:
+    """One server per user, checkout, SLURM job and GPU visibility; the same rule as the
+    client's (bin/cutadapt _sock_path)."""
+    env = os.environ if env is None else env
+    if env.get("DMX_DAEMON_SOCK"):
+        return env["DMX_DAEMON_SOCK"]
     tmp = "/tmp"
     for k in ("TMPDIR", "TEMP", "TMP"):
-        d = os.environ.get(k)
+        d = env.get(k)
         if d and os.path.isdir(d):
             tmp = d
             break
-    return os.path.join(tmp, f"dmx-{os.getuid()}-{zlib.crc32(PKG.encode()):08x}.sock")
+    scope = "|".join([PKG, env.get("SLURM_JOB_ID", "")] +
+                     [f"{k}={env.get(k, '<unset>')}" for k in VISIBILITY_ENV])
+    return os.path.join(tmp, f"dmx-{os.getuid()}-{zlib.crc32(scope.encode()):08x}.sock")
 
 
 def _recv_exact(conn, n: int) -> bytes:
@@ -81,16 +101,18 @@ class _Captured:
         return False
 
 
-def _handle(conn, base_env: dict):
+def _handle(conn) -> bool:
+    """Serve one request; returns True when the server must exit (a GPU error: its contexts
+    may hold a sticky HIP error)."""
     from . import cli, lib   # imported once, in the server process
     n = struct.unpack("<I", _recv_exact(conn, 4))[0]
     req = json.loads(_recv_exact(conn, n).decode())
-    # the caller's directory and DMX_* settings for this call only
-    for k in [k for k in os.environ if k.startswith("DMX_") and k not in base_env]:
+    # the caller's directory and exactly its DMX_* settings for this call
+    for k in [k for k in os.environ if k.startswith("DMX_")]:
         del os.environ[k]
-    os.environ.update({k: v for k, v in base_env.items() if k.startswith("DMX_")})
     os.environ.update({k: v for k, v in req.get("env", {}).items() if k.startswith("DMX_")})
     code = 1
+    fatal = False
     with _Captured() as cap:
         try:
             os.chdir(req["cwd"])
@@ -102,11 +124,13 @@ def _handle(conn, base_env: dict):
         except lib.DmxError as e:
             print(f"cutadapt (dmx): GPU error: {e}", file=sys.stderr)
             code = 1
+            fatal = True
         except Exception as e:             # keep serving; the caller sees the failure
             print(f"cutadapt (dmx): error: {type(e).__name__}: {e}", file=sys.stderr)
             code = 1
     conn.sendall(_frame(b"o", cap.out[0]) + _frame(b"e", cap.out[1]) +
                  _frame(b"x", str(int(code)).encode()))
+    return fatal
 
 
 def serve(path: str, idle: float):
@@ -115,27 +139,53 @@ def serve(path: str, idle: float):
         srv.bind(path)
     except OSError:
         return                                # another server owns the path
+    ino = os.stat(path).st_ino
     os.chmod(path, 0o600)
-    srv.listen(8)
-    srv.settimeout(idle)
-    base_env = dict(os.environ)
+    srv.listen(16)
+    srv.settimeout(0.25)
     home = os.getcwd()
-    try:
-        while True:
-            try:
-                conn, _ = srv.accept()
-            except socket.timeout:
-                break
+    busy = threading.Lock()
+    state = {"last": time.monotonic(), "fatal": False}
+
+    def work(conn):
+        try:
             with conn:
                 try:
-                    _handle(conn, base_env)
+                    state["fatal"] |= _handle(conn)
                 except (ConnectionError, OSError, ValueError):
                     pass
             os.chdir(home)
+        finally:
+            state["last"] = time.monotonic()
+            busy.release()
+
+    worker = None
+    try:
+        while not state["fatal"]:
+            try:
+                conn, _ = srv.accept()
+            except socket.timeout:
+                if not busy.locked() and time.monotonic() - state["last"] > idle:
+                    break
+                continue
+            if not busy.acquire(blocking=False):   # one call at a time; others run in-process
+                with conn:
+                    try:   # take the request off the wire first, so the client sees the reply
+                        conn.settimeout(2.0)
+                        _recv_exact(conn, struct.unpack("<I", _recv_exact(conn, 4))[0])
+                        conn.sendall(_frame(b"b", b""))
+                    except (OSError, ConnectionError, struct.error):
+                        pass
+                continue
+            worker = threading.Thread(target=work, args=(conn,), daemon=True)
+            worker.start()
+        if worker is not None:
+            worker.join()
     finally:
         srv.close()
-        try:
-            os.unlink(path)
+        try:   # only our own socket: a later server may have bound the path since
+            if os.stat(path).st_ino == ino:
+                os.unlink(path)
         except OSError:
             pass
         from . import cli

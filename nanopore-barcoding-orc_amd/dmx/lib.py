@@ -423,7 +423,11 @@ def open_group(devices) -> list:
     (dmx_comm_init_all), so run_batch sums their per-bin counts on the GPUs over xGMI."""
     ctxs = [Context(d) for d in devices]
     if len(ctxs) > 1:
-        comm_init_all(ctxs)
+        try:
+            comm_init_all(ctxs)
+        except DmxError as e:   # dmx_run_multi then sums the shards' counts on the host
+            print(f"dmx: RCCL communicator unavailable ({e}); per-bin counts are summed on the "
+                  "host", file=sys.stderr)
     return ctxs
 
 

@@ -152,6 +152,32 @@ def generate(config: str, n: int | None = None, seed: int | None = None, first: 
                 names1=names1, names2=names2)
 
 
+def shard_bounds(config: str, n_total: int, world: int, seed: int | None = None) -> list[int]:
+    """Contiguous read ranges [b[r], b[r+1]) of one seeded generation of n_total reads, balanced
+    on the sum of the drawn read lengths (the rule dmx_run_multi applies to a
+    batch's real lengths): every rank computes the same bounds without generating the reads."""
+    cfg = dict(CONFIGS[config])
+    seed = cfg["seed"] if seed is None else seed
+    n1, n2 = cfg["panel"]
+    for k in ("default_n", "seed", "panel"):
+        cfg.pop(k)
+    p = SynthParams(n1_used=n1, n2_used=n2, **cfg)
+    caps = np.empty(n_total, dtype=np.uint32)
+    lib().synth_lengths(ctypes.byref(p), seed, 0, n_total, caps.ctypes.data)
+    drawn = caps.astype(np.uint64) - np.uint64(2 * cfg["flank_max"] + 64)
+    acc = np.cumsum(drawn, dtype=np.uint64)
+    total = int(acc[-1]) if n_total else 0
+    bounds = [0]
+    for r in range(1, world):
+        # first read index whose prefix sum reaches r/world of the total (dmx_run_multi's cut)
+        bounds.append(int(np.searchsorted(acc, -(-total * r // world), side="left")) + 1
+                      if n_total else 0)
+    bounds.append(n_total)
+    for r in range(1, world + 1):
+        bounds[r] = max(bounds[r], bounds[r - 1])
+    return bounds
+
+
 def to_strings(d) -> list[str]:
     b = d["blob"]
     return [b[o:o + l].tobytes().decode("ascii") for o, l in zip(d["offsets"], d["lengths"])]

@@ -77,3 +77,55 @@ def test_chunked_run_multi_rccl_counts(c2x24, monkeypatch):
             c.close()
     assert res.tobytes() == res0.tobytes()
     assert counts.tolist() == counts0.tolist()
+
+
+def test_even_chunk_count_then_mid_sized_load(c2x24, monkeypatch):
+    """Capacities travel with their input sets: a one-shot load of the whole batch, a chunked
+    dmx_run with an even number of chunks (the second set ends resident), then a load sized
+    between the chunk and the first batch must reallocate, and match a fresh context."""
+    d, p = c2x24
+    n_mid = 12000
+    q = lib.pack(d["blob"], d["offsets"][:n_mid], d["lengths"][:n_mid])
+    monkeypatch.setenv("DMX_RUN_CHUNK", "5000")   # 20000 reads -> 4 chunks
+    with lib.Context(0) as ctx:
+        _setup(ctx, d)
+        ctx.load(p)
+        ctx.exec()
+        ctx.sync()
+        ctx.run(p)
+        ctx.load(q)
+        ctx.exec()
+        got = ctx.fetch()
+        got_counts = ctx.counts()
+    with lib.Context(0) as ctx:
+        _setup(ctx, d)
+        ctx.load(q)
+        ctx.exec()
+        exp = ctx.fetch()
+        exp_counts = ctx.counts()
+    assert got.tobytes() == exp.tobytes()
+    assert got_counts.tolist() == exp_counts.tolist()
+
+
+def test_unaligned_batch_runs_one_shot(c2x24, monkeypatch):
+    """A caller-packed batch whose offsets are not on dmx_pack's 32-nt grid is accepted at any
+    size (it runs in one shot instead of chunks) with the same results."""
+    d, p = c2x24
+    n = 6000
+    q = lib.pack(d["blob"], d["offsets"][:n], d["lengths"][:n])
+    # shift every read by 16 nt (one u32 word) inside a buffer one word longer
+    seq = np.concatenate([np.zeros(1, np.uint32), q.seq2b])
+    nm = np.zeros(len(seq), np.uint32)
+    bits = np.unpackbits(q.nmask.view(np.uint8), bitorder="little")
+    sh = np.concatenate([np.zeros(16, np.uint8), bits])[:len(nm) * 32]
+    nm[:] = np.packbits(sh, bitorder="little").view(np.uint32)[:len(nm)]
+    shifted = lib.Packed(seq, nm, q.offsets + 16, q.lengths)
+    monkeypatch.setenv("DMX_RUN_CHUNK", "1000")
+    with lib.Context(0) as ctx:
+        _setup(ctx, d)
+        got = ctx.run(shifted)
+    monkeypatch.setenv("DMX_RUN_CHUNK", "0")
+    with lib.Context(0) as ctx:
+        _setup(ctx, d)
+        exp = ctx.run(q)
+    assert got.tobytes() == exp.tobytes()
