@@ -14,7 +14,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # DMX_LIBDMX: an alternative in-tree build of the same library (A/B kernel variants)
-LIB_PATH = os.environ.get("DMX_LIBDMX") or os.path.join(HERE, "libdmx.so")
+# DMX_LIBDIR: a directory with another build of every library (host sanitizer builds)
+LIB_PATH = os.environ.get("DMX_LIBDMX") or os.path.join(os.environ.get("DMX_LIBDIR") or HERE,
+                                                      "libdmx.so")
 
 DMX_FRONT, DMX_BACK, DMX_RC = 0x01, 0x02, 0x10
 MODE_SINGLE, MODE_TWO_ROUND, MODE_LINKED = 0, 1, 2

@@ -16,7 +16,8 @@ import numpy as np
 from .lib import DmxError, Packed
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-IO_PATH = os.path.join(HERE, "libdmx_io.so")
+# DMX_LIBDIR: an alternative build directory (host sanitizer builds: make sanitize)
+IO_PATH = os.path.join(os.environ.get("DMX_LIBDIR") or HERE, "libdmx_io.so")
 IO_EXPORTS = ["dmx_io_abi_version", "dmx_reader_open", "dmx_reader_next", "dmx_reader_error",
               "dmx_reader_close", "dmx_batch_free", "dmx_sink_open", "dmx_sink_write",
               "dmx_sink_close", "dmx_sink_error", "dmx_sink_free", "dmx_sink_write_rows",

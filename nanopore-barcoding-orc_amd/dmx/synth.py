@@ -14,7 +14,7 @@ import numpy as np
 from . import panel as _panel
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdmx_synth.so")
+LIB_PATH = os.path.join(os.environ.get("DMX_LIBDIR") or HERE, "libdmx_synth.so")
 
 
 class SynthParams(ctypes.Structure):

@@ -16,7 +16,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liborc.so")
+# ORC_LIBDIR: a sanitizer build of the same library (tools/sanitize.sh)
+LIB_PATH = os.path.join(os.environ.get("ORC_LIBDIR") or HERE, "liborc.so")
 
 FRONT, BACK = 11, 14
 

@@ -117,7 +117,7 @@ def test_unaligned_batch_runs_one_shot(c2x24, monkeypatch):
     seq = np.concatenate([np.zeros(1, np.uint32), q.seq2b])
     nm = np.zeros(len(seq), np.uint32)
     bits = np.unpackbits(q.nmask.view(np.uint8), bitorder="little")
-    sh = np.concatenate([np.zeros(16, np.uint8), bits])[:len(nm) * 32]
+    sh = np.concatenate([np.zeros(16, np.uint8), bits, np.zeros(16, np.uint8)])
     nm[:] = np.packbits(sh, bitorder="little").view(np.uint32)[:len(nm)]
     shifted = lib.Packed(seq, nm, q.offsets + 16, q.lengths)
     monkeypatch.setenv("DMX_RUN_CHUNK", "1000")
