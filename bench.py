@@ -159,10 +159,10 @@ def pmc_traffic(workload: str, reads: int):
 
 # the two-round pipeline's kernels and the live stage events that time them (per round)
 KERNEL_STAGES = (("dmx::filter_kernel", "filter"), ("dmx::verify_kernel", "verify"),
-                 ("dmx::iscreen_kernel", "screen"), ("dmx::wscan_kernel<true>", "wscan"),
+                 ("dmx::iscreen4_kernel", "screen"), ("dmx::wscan_kernel<true>", "wscan"),
                  ("band_cand<7>+band_cand<11|15>+select_cand", "resolve"))
 PMC_NAMES = {"filter": ["filter_kernel"], "verify": ["verify_kernel"],
-             "screen": ["iscreen_kernel"], "wscan": ["wscan_kernel<true>"],
+             "screen": ["iscreen4_kernel", "iscreen_kernel"], "wscan": ["wscan_kernel<true>"],
              "resolve": ["band_cand_kernel<7>", "band_cand_kernel<11>", "band_cand_kernel<15>",
                          "select_cand_kernel"]}
 

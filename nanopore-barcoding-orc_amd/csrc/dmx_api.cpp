@@ -241,6 +241,8 @@ int dmx_open(int device, dmx_ctx** out) {
     c->force_ring = rs && std::strcmp(rs, "ring") == 0;
     const char* ns = std::getenv("DMX_NO_SCREEN");   // A/B: no index screen before the
     c->no_screen = ns && ns[0] == '1';               // window scan
+    const char* s1 = std::getenv("DMX_SCREEN_V1");   // A/B: the unpacked index screen
+    c->screen_v1 = s1 && s1[0] == '1';
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;

@@ -93,6 +93,7 @@ struct Ctx {
     Window* d_tasks = nullptr;           // index screen survivors (window piece of one adapter)
     size_t task_cap = 0;
     bool no_screen = false;              // DMX_NO_SCREEN=1: every window runs every adapter
+    bool screen_v1 = false;              // DMX_SCREEN_V1=1: one lane per (window, adapter) screen
     size_t n_counts = 0;
     hipEvent_t ev[15] = {};   // [3r..3r+2] round r stages, [6+r] finalize, [8] start,
                               // [9+2r] after filter, [10+2r] after verify, [13+r] after screen

@@ -1606,6 +1606,323 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
     if (threadIdx.x == 0 && s_nend) atomicAdd(&R.diag[3], s_nend);     // by 3' cells only
 }
 
+// ---------------------------------------------------------------------------------------------
+// Packed index screen (the same necessary conditions as iscreen_kernel): one lane
+// per (verified window, quad of adapters).  Each adapter's index block runs in a 16-bit half of a
+// dword — two adapters per dword, two dwords per lane — with gfx950's packed 16-bit VALU
+// (v_pk_add_u16 keeps the halves' carries apart, v_pk_lshlrev_b16 their shifts), so one
+// instruction steps two adapters.  A block longer than 16 rows is cut to its LAST 16 rows: with a
+// free start in the read, an alignment of all of I_a ending at column x restricted to those rows
+// is an alignment of the cut block ending at the same x of no larger cost, so D_cut <= D_I at
+// every column (the screen only ever tests D <= threshold: a lower bound keeps it necessary).
+// Rows of a 3' partial-I cell above the cut count as cost 0 (again a lower bound).  The block
+// sits in the top l' bits of its half with all-match padding below (it stays at cost 0 and acts
+// as row 0, as in myers_step_top); non-ACGT codes (table rows 4..7) match only the padding.
+// LDS: [code][quad] u64 with 64-B code rows, so the six lanes of a window (24 adapters) read six
+// consecutive u64 of one row and windows with other codes read other rows on other banks
+// (ds_read_b64, 64 banks: code c at banks 16c .. 16c + 11) — conflict-free.
+// ---------------------------------------------------------------------------------------------
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_pk(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+// Myers step of two 16-bit blocks (last row = bit 15 of each half); d: per-half last-row cost.
+__device__ __forceinline__ void myers_step_pk(uint32_t eq, uint32_t& pv, uint32_t& mv, u16x2& d) {
+    const uint32_t xv = eq | mv;
+    const uint32_t s = as_u32(as_pk(eq & pv) + as_pk(pv));
+    // Xh = (s ^ Pv) | Eq is never formed: Xh | Pv = s | Pv | Eq (one v_or3), and
+    // Pv & Xh = Pv & ((s ^ Pv) | Eq) is one v_bitop3
+    const uint32_t ph = mv | ~(s | pv | eq);
+    const uint32_t mh = pv & ((s ^ pv) | eq);
+    d = d + (as_pk(ph) >> (uint16_t)15) - (as_pk(mh) >> (uint16_t)15);
+    const uint32_t ph2 = as_u32(as_pk(ph) << (uint16_t)1);
+    const uint32_t mh2 = as_u32(as_pk(mh) << (uint16_t)1);
+    pv = mh2 | ~(xv | ph2);
+    mv = ph2 & xv;
+}
+
+// f * 32 as one v_lshl_add with the lane's row base (left to itself the compiler turns the
+// bit-field extract + scale into shift + mask + add: three VALU per column instead of two)
+__device__ __forceinline__ uint32_t lds_off32(uint32_t f, uint32_t base) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(r) : "v"(f), "v"(base));
+    return r;
+}
+
+// bit k of b (k < 8) -> bit 4k + 3 (the no-match bit of column k's nibble)
+__device__ __forceinline__ uint32_t spread_bits_nib(uint32_t b) {
+    uint32_t x = b & 0xFFu;
+    x = (x | (x << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    x = (x | (x << 3)) & 0x11111111u;
+    return x << 3;
+}
+
+constexpr int kScreenQuads = 8;             // adapters <= 32 (larger panels: iscreen_kernel)
+constexpr int kScreenRow = 8;               // u64 per code row (64 B)
+constexpr int kScreenCap = 128;             // per-wave task staging (4 pushes per lane per round)
+
+#ifndef DMX_SCREEN_WAVES
+#define DMX_SCREEN_WAVES 4
+#endif
+__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_SCREEN_WAVES))) void iscreen4_kernel(RoundArgs R) {
+    __shared__ uint64_t s_q[8 * kScreenRow];
+    __shared__ int8_t s_acc[72 * 4 * kScreenQuads];
+    __shared__ uint32_t s_par[4 * kScreenQuads];   // per adapter: l | kk << 8 | m << 16 | l' << 24
+    __shared__ int8_t s_pimax[4 * kScreenQuads];   // max acc[pre_len + r], r = 1 .. l - 1
+    __shared__ Window s_task[kScanBlock / 64][kScreenCap];
+    __shared__ uint32_t s_tc[kScanBlock / 64], s_nend;
+    const DevPanel* P = R.panel;
+    const int A = P->n_adapters;
+    const int Q = (A + 3) >> 2;
+    const int pl = P->pre_len, sl = P->filter_len, kf = P->kf;
+    for (int x = threadIdx.x; x < 8 * kScreenRow; x += blockDim.x) {
+        const int c = x / kScreenRow, q = x % kScreenRow;
+        uint64_t v = 0;
+        for (int h = 0; h < 4; ++h) {
+            const int a = 4 * q + h;
+            uint32_t half = 0xFFFFu;                  // absent adapter: padding only
+            if (a < A) {
+                const int l = (int)P->ad[a].m - pl - sl;
+                const int lc = min(l, 16);
+                const uint32_t pad = (1u << (16 - lc)) - 1u;
+                // rows pre_len + (l - lc) .. pre_len + l - 1 of the adapter, top lc bits
+                const uint32_t rows = c < 4 ? (uint32_t)((P->ad[a].peq[c] >> (pl + l - lc)) &
+                                                         ((1ull << lc) - 1ull))
+                                            : 0u;
+                half = (rows << (16 - lc)) | pad;
+            }
+            v |= (uint64_t)half << (16 * h);
+        }
+        s_q[c * kScreenRow + q] = v;
+    }
+    for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_acc[x] = P->ad[x / 72].acc[x % 72];
+    for (int a = threadIdx.x; a < A; a += blockDim.x) {
+        const int l = (int)P->ad[a].m - pl - sl;
+        s_par[a] = (uint32_t)l | ((uint32_t)(uint8_t)P->ad[a].kk << 8) |
+                   ((uint32_t)P->ad[a].m << 16) | ((uint32_t)min(l, 16) << 24);
+        int mx = -1;
+        for (int r = 1; r < l; ++r) mx = max(mx, (int)P->ad[a].acc[pl + r]);
+        s_pimax[a] = (int8_t)mx;
+    }
+    if (threadIdx.x < kScanBlock / 64) s_tc[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_nend = 0;
+    __shared__ uint32_t s_spre[kShards + 1];
+    ShardMap sm{s_spre, 0u};
+    sm.load(R.win2_count, R.win_scap);                 // (its barrier covers the above)
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t wsh = wave_shard();
+    const WaveStage<Window, kScreenCap> st{s_task[wv], &s_tc[wv], R.tasks + wsh * R.task_scap,
+                                           R.task_count + wsh * kShardStride, R.task_scap,
+                                           R.flags, 4u};
+    const Window* wl = R.win2;
+    const uint32_t nwin = sm.total();
+    const uint32_t total = nwin * (uint32_t)Q;
+    const bool front = P->where == kFront;
+    const int jsplit = front ? P->jsplit : 0;
+    const bool pshared = P->pshared != 0;
+
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride) {
+        const uint32_t t = base + threadIdx.x;
+        const bool live = t < total;
+        uint32_t near_m = 0, pass_m = 0, end_m = 0;   // per adapter k of the quad (bits 0..3)
+        Window w{};
+        int q = 0;
+        if (live) {
+            const uint32_t wi = t / (uint32_t)Q;
+            q = (int)(t - wi * (uint32_t)Q);
+            w = wl[sm.phys(wi)];
+            const int len = (int)w.len, j1 = (int)w.j1, j2 = (int)w.j2;
+            const int bm = w.bmin;
+            const int dP = (int)(w.info & 255u), dPe = (int)((w.info >> 8) & 255u);
+            const int dPn = (int)(w.info >> 24);
+            const bool lastc = !front && w.lastcol;
+            const uint32_t valid = A - 4 * q >= 4 ? 0xFu : ((1u << (A - 4 * q)) - 1u);
+            if (j1 < jsplit) near_m = valid;                 // the near piece keeps every adapter
+            const int jr = max(j1, jsplit);
+            const bool rows_base = bm != 255 && jr <= j2;
+            // per adapter: thresholds, first column of the band, which tests apply
+            int thr[4], thre[4], x1 = 1 << 30;
+            uint32_t need = 0, rows_m = 0;
+            const bool pinfo = ((w.info >> 16) & 1u) != 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int a = 4 * q + k;
+                const uint32_t par = (valid >> k) & 1u ? s_par[a] : 0u;
+                const int l = (int)(par & 255u), kk = (int)((par >> 8) & 255u);
+                const int m = (int)((par >> 16) & 255u);
+                thr[k] = kk - bm - dP;                        // (bm = 255: no hit column)
+                thre[k] = kk - dPe;
+                const bool rk = ((valid >> k) & 1u) && rows_base && thr[k] >= 0;
+                if (!rk) thr[k] = -1;
+                if (!lastc) thre[k] = -1;
+                // P-only last-column cells: identical for every adapter, the first one wins
+                // ties; an empty view keeps every adapter
+                if (((valid >> k) & 1u) && lastc && (len == 0 || (pinfo && (a == 0 || !pshared))))
+                    pass_m |= 1u << k;
+                if (((valid >> k) & 1u) && !((pass_m >> k) & 1u) && (rk || lastc)) {
+                    need |= 1u << k;
+                    if (rk) x1 = min(x1, jr - l - sl - kf);
+                    if (lastc) x1 = min(x1, len - (m - 1 - pl) - kf);
+                }
+                if (rk) rows_m |= 1u << k;
+            }
+            end_m = valid;                                   // (diagnostic: no last-row reason)
+            if (need) {
+                const bool rows = rows_m != 0;
+                const int xr_lo = jr - sl - kf, xr_hi = j2 - sl + kf;
+                const int xe_lo = len - sl + 1 - kf;
+                int xe = -1;
+                if (rows) xe = min(xr_hi, len);
+                if (lastc) xe = len;
+                const int nch = (xe - x1 + 15) >> 4;
+                const int jb = xe - 16 * nch;
+                const int xrh = min(xr_hi, len);
+                uint32_t lp[2];                              // l' of the four halves
+                {
+                    const uint32_t p0 = s_par[4 * q] >> 24, p1 = s_par[4 * q + 1] >> 24;
+                    const uint32_t p2 = s_par[4 * q + 2] >> 24, p3 = s_par[4 * q + 3] >> 24;
+                    lp[0] = (valid & 1u ? p0 : 0u) | ((valid & 2u ? p1 : 0u) << 16);
+                    lp[1] = (valid & 4u ? p2 : 0u) | ((valid & 8u ? p3 : 0u) << 16);
+                }
+                // block rows = the top l' bits of each half (D(i, x0) = i there, 0 below)
+                uint32_t pv0, pv1, mv0 = 0u, mv1 = 0u;
+                {
+                    const uint32_t r0 = (0xFFFFu << (16 - (lp[0] & 0xFFFFu))) & 0xFFFFu;
+                    const uint32_t r1 = (0xFFFFu << (16 - (lp[0] >> 16))) & 0xFFFFu;
+                    const uint32_t r2 = (0xFFFFu << (16 - (lp[1] & 0xFFFFu))) & 0xFFFFu;
+                    const uint32_t r3 = (0xFFFFu << (16 - (lp[1] >> 16))) & 0xFFFFu;
+                    pv0 = r0 | (r1 << 16);
+                    pv1 = r2 | (r3 << 16);
+                }
+                u16x2 d0 = as_pk(lp[0]), d1 = as_pk(lp[1]);
+                TaskView tv;
+                tv.read = 0;
+                tv.n = w.n;
+                tv.strand = w.strand;
+                tv.start = w.start;
+                tv.len = w.len;
+                tv.off = w.off;
+                tv.o = w.o;
+                tv.a = 0;
+                const char* qb = reinterpret_cast<const char*>(s_q);
+                const uint32_t q8 = 8u * (uint32_t)q;   // the lane's quad within a code row
+                uint32_t c0 = 0, n0 = 0, c1 = 0, n1 = 0;   // two chunks in flight
+                if (nch > 0) fetch16s(R.seq, R.nmask, tv, jb, c0, n0);
+                if (nch > 1) fetch16s(R.seq, R.nmask, tv, jb + 16, c1, n1);
+                for (int kc = 0; kc < nch && (need & ~pass_m); ++kc) {
+                    const int p0 = jb + 16 * kc;
+                    const uint32_t codes = c0, nb = n0;
+                    c0 = c1;
+                    n0 = n1;
+                    if (kc + 2 < nch) fetch16s(R.seq, R.nmask, tv, p0 + 32, c1, n1);
+                    const bool inR = rows && p0 + 16 >= xr_lo && p0 + 1 <= xrh;
+                    const bool inE = lastc && p0 + 16 >= xe_lo;
+                    const int qlo = min(inR ? xr_lo : (1 << 30), inE ? xe_lo : (1 << 30)) - p0 - 1;
+                    // nibble q of lo/hi: code * 2 + no-match * 8, i.e. the byte offset / 32 of
+                    // the column's code row ([code][quad] u64, 64-B rows)
+                    uint32_t lo = ((spread_codes(codes, 0x0c010c00u) >> 1));
+                    uint32_t hi = ((spread_codes(codes, 0x0c030c02u) >> 1));
+                    if (__builtin_amdgcn_ballot_w64(nb != 0u)) {
+                        lo |= spread_bits_nib(nb);
+                        hi |= spread_bits_nib(nb >> 8);
+                    }
+                    uint32_t cm0 = 0xFFFFFFFFu, cm1 = 0xFFFFFFFFu;
+                    u16x2 m0 = as_pk(cm0), m1 = as_pk(cm1);
+                    if (__builtin_amdgcn_ballot_w64(qlo > 0) == 0) {   // every column counts
+#pragma unroll
+                        for (int c = 0; c < 16; ++c) {
+                            const uint64_t e = *reinterpret_cast<const uint64_t*>(
+                                qb + lds_off32(__builtin_amdgcn_ubfe(c < 8 ? lo : hi,
+                                                                     4 * (c & 7), 4), q8));
+                            myers_step_pk((uint32_t)e, pv0, mv0, d0);
+                            myers_step_pk((uint32_t)(e >> 32), pv1, mv1, d1);
+                            m0 = __builtin_elementwise_min(m0, d0);
+                            m1 = __builtin_elementwise_min(m1, d1);
+                        }
+                    } else {
+#pragma unroll
+                        for (int c = 0; c < 16; ++c) {
+                            const uint64_t e = *reinterpret_cast<const uint64_t*>(
+                                qb + lds_off32(__builtin_amdgcn_ubfe(c < 8 ? lo : hi,
+                                                                     4 * (c & 7), 4), q8));
+                            myers_step_pk((uint32_t)e, pv0, mv0, d0);
+                            myers_step_pk((uint32_t)(e >> 32), pv1, mv1, d1);
+                            if (c >= qlo) {
+                                m0 = __builtin_elementwise_min(m0, d0);
+                                m1 = __builtin_elementwise_min(m1, d1);
+                            }
+                        }
+                    }
+                    cm0 = as_u32(m0);
+                    cm1 = as_u32(m1);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t cmk = ((k < 2 ? cm0 : cm1) >> (16 * (k & 1))) & 0xFFFFu;
+                        const int tk = max(inR ? thr[k] : -1, inE ? thre[k] : -1);
+                        if (((need >> k) & 1u) && !((pass_m >> k) & 1u) && (int)cmk <= tk) {
+                            pass_m |= 1u << k;
+                            if (inR) end_m &= ~(1u << k);
+                        }
+                    }
+                }
+                // partial I_a at the read end: cells (pre_len + r, len), r = 1 .. l - 1
+                if (lastc) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (!((need >> k) & 1u) || ((pass_m >> k) & 1u)) continue;
+                        const int a = 4 * q + k;
+                        if (dPn > (int)s_pimax[a]) continue;   // no row can pass (D >= 0)
+                        const uint32_t par = s_par[a];
+                        const int l = (int)(par & 255u), lc = (int)(par >> 24);
+                        const uint32_t pvh = ((k < 2 ? pv0 : pv1) >> (16 * (k & 1))) & 0xFFFFu;
+                        const uint32_t mvh = ((k < 2 ? mv0 : mv1) >> (16 * (k & 1))) & 0xFFFFu;
+                        bool ok = false;
+                        int dd = 0;
+                        for (int r = 1; r < l && !ok; ++r) {
+                            if (r > l - lc) {   // row r of I_a = bit 16 - l + r - 1 of the half
+                                const int b = 16 - l + r - 1;
+                                dd += (int)((pvh >> b) & 1u) - (int)((mvh >> b) & 1u);
+                            }                   // rows above the cut: cost >= 0
+                            ok = dPn + dd <= (int)s_acc[72 * a + pl + r];
+                        }
+                        if (ok) pass_m |= 1u << k;
+                    }
+                }
+            }
+            pass_m &= valid;
+            end_m &= pass_m;
+        }
+        // pushes: at most 4 per lane, one wave-uniform round per adapter of the quad; a flush
+        // before each round keeps the slice from overflowing (kScreenCap >= 64 + 64)
+        const int jr = max((int)w.j1, jsplit);
+        const bool lastc = !front && w.lastcol;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            __builtin_amdgcn_wave_barrier();
+            if (st.count() > kScreenCap - 64) st.flush();
+            if ((near_m >> k) & 1u)
+                st.push(make_task(w, w.j1, (uint32_t)min((int)w.j2, jsplit - 1), false, 4 * q + k));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            __builtin_amdgcn_wave_barrier();
+            if (st.count() > kScreenCap - 64) st.flush();
+            if ((pass_m >> k) & 1u) {
+                st.push(make_task(w, (uint32_t)jr, w.j2, lastc, 4 * q + k));
+                if ((end_m >> k) & 1u) atomicAdd(&s_nend, 1u);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (st.count() > kScreenCap / 2) st.flush();
+    }
+    __builtin_amdgcn_wave_barrier();
+    st.flush();
+    __syncthreads();
+    if (threadIdx.x == 0 && s_nend) atomicAdd(&R.diag[3], s_nend);     // by 3' cells only
+}
+
 // Window scan: one lane per (window, adapter) — or, after the index screen, per surviving
 // (piece, adapter) — in a block-uniform grid stride over the device-side count, so that the
 // block can flush its staged records between strides.
@@ -2561,8 +2878,12 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         if (hp.verify)
             hipLaunchKernelGGL(verify_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
         hipEventRecord(c->ev[10 + 2 * round], st);
-        if (R.screen)
-            hipLaunchKernelGGL(iscreen_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
+        if (R.screen) {   // packed quads for panels of <= 32 adapters (DMX_SCREEN_V1: A/B)
+            if (hp.n <= 4 * kScreenQuads && !c->screen_v1)
+                hipLaunchKernelGGL(iscreen4_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
+            else
+                hipLaunchKernelGGL(iscreen_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
+        }
         hipEventRecord(c->ev[13 + round], st);
         if (band) hipLaunchKernelGGL(wscan_kernel<true>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(wscan_kernel<false>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);

@@ -100,7 +100,8 @@ def _phase(name: str, marks: list):
 _CTX_CACHE: dict = {}   # (devices, open-time settings) -> contexts kept by the resident server
 # the DMX_* switches dmx_open reads once per context (csrc/dmx_api.cpp dmx_open): a cached
 # context is reused only by calls with the same values
-OPEN_TIME_ENV = ("DMX_NO_FILTER", "DMX_NO_VERIFY", "DMX_RESOLVE", "DMX_NO_SCREEN")
+OPEN_TIME_ENV = ("DMX_NO_FILTER", "DMX_NO_VERIFY", "DMX_RESOLVE", "DMX_NO_SCREEN",
+                 "DMX_SCREEN_V1")
 
 
 def close_cached_contexts():

@@ -326,3 +326,58 @@ def test_two_round_nonpositive_scores(ctx):
     ctx.set_panel(1, p2, lib.DMX_BACK | lib.DMX_RC, 3, 2)
     ctx.set_mode(lib.MODE_TWO_ROUND)
     _assert_same(ctx.run(lib.pack(blob, offs, lens)), exp)
+
+
+def _pis_panel(rng, n, pre, suf, lmin, lmax):
+    """P + I_a + S panels (shared prefix and suffix, index blocks of lmin..lmax nt): the shape the
+    index screen runs on, including blocks longer than the packed screen's 16-bit
+    halves (cut to their last 16 rows)."""
+    P = "".join(rng.choice(list("ACGT"), pre))
+    S = "".join(rng.choice(list("ACGT"), suf))
+    return [P + "".join(rng.choice(list("ACGT"), int(rng.integers(lmin, lmax + 1)))) + S
+            for _ in range(n)]
+
+
+@pytest.mark.parametrize("seed,n,lmin,lmax,where", [
+    (1, 24, 17, 17, "front"), (2, 24, 17, 17, "back"), (3, 13, 1, 16, "back"),
+    (4, 30, 12, 32, "front"), (5, 7, 20, 32, "back"), (6, 32, 5, 24, "back")])
+def test_packed_index_screen(ctx, seed, n, lmin, lmax, where, monkeypatch):
+    """The packed index screen (four adapters per lane in 16-bit halves) against the oracle, the
+    one-lane-per-adapter screen (DMX_SCREEN_V1) and no screen, on P + I_a + S panels with index
+    blocks of 1..32 nt, two rounds (the other round's panel has the real M13 shape)."""
+    rng = np.random.default_rng(seed)
+    pre, suf = int(rng.integers(10, 21)), int(rng.integers(10, 21))
+    lmax = min(lmax, 64 - pre - suf)
+    pan = _pis_panel(rng, n, pre, suf, min(lmin, lmax), lmax)
+    d = synth.generate("c2", n=1500, seed=seed)
+    reads = synth.to_strings(d)
+    extra = _reads_with(rng, pan, 3000, L=(0, 500), err=0.05)
+    seqs = reads + extra
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    if where == "front":
+        p1, p2 = pan, d["sp27"]
+    else:
+        p1, p2 = d["sp5"], pan
+    exp = oracle.run_batch(oracle.Panel(p1, oracle.FRONT), oracle.Panel(p2, oracle.BACK), blob,
+                           offs, lens, mode=1, threads=8)
+    packed = lib.pack(blob, offs, lens)
+    tasks = {}
+    for variant in ("packed", "v1", "none"):
+        monkeypatch.delenv("DMX_SCREEN_V1", raising=False)
+        monkeypatch.delenv("DMX_NO_SCREEN", raising=False)
+        if variant == "v1":
+            monkeypatch.setenv("DMX_SCREEN_V1", "1")
+        if variant == "none":
+            monkeypatch.setenv("DMX_NO_SCREEN", "1")
+        with lib.Context(0) as c:
+            c.set_panel(0, p1, lib.DMX_FRONT | lib.DMX_RC)
+            c.set_panel(1, p2, lib.DMX_BACK | lib.DMX_RC)
+            c.set_mode(lib.MODE_TWO_ROUND)
+            c.load(packed)
+            c.exec()
+            _assert_same(c.fetch(), exp)
+            tasks[variant] = c.stats()["tasks"]
+    # the packed screen is the same kind of filter: it still prunes (blocks > 16 nt lose rows)
+    r = 0 if where == "front" else 1
+    assert tasks["packed"][r] >= tasks["v1"][r]
+    assert tasks["packed"][r] <= 2 * tasks["v1"][r] + 100

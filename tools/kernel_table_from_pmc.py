@@ -20,7 +20,7 @@ import json
 import os
 import sys
 
-KERNELS = ("filter_kernel", "verify_kernel", "iscreen_kernel", "wscan_kernel<true>",
+KERNELS = ("filter_kernel", "verify_kernel", "iscreen_kernel", "iscreen4_kernel", "wscan_kernel<true>",
            "band_cand_kernel<7>", "band_cand_kernel<11>", "band_cand_kernel<15>", "select_cand_kernel",
            "finalize0_kernel", "finalize1_kernel", "chop_kernel")
 
