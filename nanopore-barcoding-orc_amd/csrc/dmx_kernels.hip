@@ -1276,6 +1276,101 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
 }
 
 // ---------------------------------------------------------------------------------------------
+// Consecutive 64-position stretches of a view, read as whole aligned 64-nt blocks of the packed
+// read (one 16-B code load + one 8-B mask load per block, instead of two 4-B gathers per 16
+// positions): the two blocks holding the current stretch and the next block in flight.  A lane's
+// stretches start 64 positions apart, so its bit alignment inside the blocks never changes and the
+// extraction is the filter's (seg_extract): word selects + funnel shifts, no indexed registers.
+// Strand 1 walks the global blocks downwards and reverses + complements each 16-position chunk.
+// ---------------------------------------------------------------------------------------------
+struct ViewBlocks {
+    uint32_t cw[12], nw[6];      // [0..7]/[0..3]: blocks B, B + 1 (ascending); [8..11]/[4..5]:
+                                 // the block in flight (B + 2 on strand 0, B - 1 on strand 1)
+    uint32_t m1, m2, r, r2;
+    const uint4* sp;
+    const uint2* np;
+    int64_t nxt;                 // the next block to load
+    bool rev;
+
+    __device__ __forceinline__ void load(int k, int64_t b) {
+        const uint4 c4 = sp[b];
+        cw[4 * k + 0] = c4.x;
+        cw[4 * k + 1] = c4.y;
+        cw[4 * k + 2] = c4.z;
+        cw[4 * k + 3] = c4.w;
+        const uint2 n2 = np[b];
+        nw[2 * k + 0] = n2.x;
+        nw[2 * k + 1] = n2.y;
+    }
+    // view positions [p, p + 64 * n_stretch) of the view (strand, start, n, off) of tv
+    __device__ __forceinline__ void init(const RoundArgs& R, const TaskView& tv, int p) {
+        rev = tv.strand != 0;
+        const int64_t g = rev ? (int64_t)tv.off + (int64_t)tv.n - 1 - tv.start - p - 63
+                              : (int64_t)tv.off + tv.start + p;
+        const int64_t blk = g >> 6;               // floor: the buffers carry guard words
+        const uint32_t sh = (uint32_t)(g & 63);
+        sp = reinterpret_cast<const uint4*>(R.seq);
+        np = reinterpret_cast<const uint2*>(R.nmask);
+        load(0, blk);
+        load(1, blk + 1);
+        nxt = rev ? blk - 1 : blk + 2;
+        load(2, nxt);
+        nxt += rev ? -1 : 1;
+        m1 = ((sh >> 4) & 1u) ? ~0u : 0u;
+        m2 = ((sh >> 5) & 1u) ? ~0u : 0u;
+        r = (2u * sh) & 31u;
+        r2 = sh & 31u;
+    }
+    // the current stretch as 4 chunks (view order), then slide by one block; `more`: a later
+    // stretch will be needed after the next one (load its block now)
+    __device__ __forceinline__ void extract(uint32_t vc[4], uint32_t vn[4], bool more) {
+        uint32_t a[7], t[5], asc[4], tn[3];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) a[k] = bsel(m1, cw[k + 1], cw[k]);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) t[k] = bsel(m2, a[k + 2], a[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) asc[k] = align32(t[k + 1], t[k], r);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) tn[k] = bsel(m2, nw[k + 1], nw[k]);
+        const uint32_t an[2] = {align32(tn[1], tn[0], r2), align32(tn[2], tn[1], r2)};
+        if (!rev) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                vc[c] = asc[c];
+                vn[c] = (an[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int d = 3 - c;
+                vc[c] = ~rev_pairs(asc[d]);                        // complement = 3 - code
+                vn[c] = __brev((an[d >> 1] >> (16 * (d & 1))) & 0xFFFFu) >> 16;
+            }
+        }
+        // slide: strand 0 (lo, hi, in flight) -> (hi, in flight, next);
+        //        strand 1 (lo, hi, in flight) -> (in flight, lo, next)
+        const uint32_t rm = rev ? ~0u : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t lo = cw[k], hi = cw[4 + k], fl = cw[8 + k];
+            cw[k] = bsel(rm, fl, hi);
+            cw[4 + k] = bsel(rm, lo, fl);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t lo = nw[k], hi = nw[2 + k], fl = nw[4 + k];
+            nw[k] = bsel(rm, fl, hi);
+            nw[2 + k] = bsel(rm, lo, fl);
+        }
+        if (more) {
+            load(2, nxt);
+            nxt += rev ? -1 : 1;
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
 // verify: one lane per filter window; 32-bit Myers of the shared PREFIX block over the columns
 // where the prefix of an alignment ending in the window would end.  Keeps the window only if
 //   (rows) some full alignment ending in [j1, j2] could cost <= kf: bmin + min D_pre <= kf
@@ -1350,30 +1445,29 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
                     if (end_lo <= 0) dmin_end = L;
                     if (near_lo <= 0) dmin_near = L;
                 }
-                // two 16-column chunks in flight: the next chunk's gather is issued before this
-                // chunk's steps (one lane per window: the loads are scattered, latency-bound)
-                uint32_t c_nx = 0, n_nx = 0, c_nx2 = 0, n_nx2 = 0;
-                if (js < hi)
-                    fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, (uint32_t)js, c_nx,
-                            n_nx);
-                if (js + 16 < hi)
-                    fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start,
-                            (uint32_t)(js + 16), c_nx2, n_nx2);
-                for (int p0 = js; p0 < hi; p0 += 16) {
-                    const uint32_t codes = c_nx, nb = n_nx;
-                    c_nx = c_nx2;
-                    n_nx = n_nx2;
-                    if (p0 + 32 < hi)
-                        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start,
-                                (uint32_t)(p0 + 32), c_nx2, n_nx2);
-                    const int cnt = min(16, hi - p0);
-                    for (int q = 0; q < cnt; ++q) {
-                        const uint32_t code = ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
-                        myers_step32(s_ppeq[code], pv, mv, d, hbit);
-                        const int j = p0 + q + 1;
-                        if (j >= rlo && j <= rhi) dmin_rows = min(dmin_rows, d);
-                        if (j >= end_lo) dmin_end = min(dmin_end, d);
-                        if (j >= near_lo) dmin_near = min(dmin_near, d);
+                // the columns js + 1 .. hi as 64-position stretches of whole aligned blocks
+                // (one lane per window: the block loads are scattered, so few and wide)
+                const int nst = (hi - js + 63) >> 6;
+                ViewBlocks vb;
+                if (nst > 0) vb.init(R, tv, js);
+                for (int st_i = 0; st_i < nst; ++st_i) {
+                    uint32_t vc[4], vn[4];
+                    vb.extract(vc, vn, st_i + 2 < nst);
+#pragma unroll
+                    for (int ch = 0; ch < 4; ++ch) {
+                        const int p0 = js + 64 * st_i + 16 * ch;
+                        const int cnt = min(16, hi - p0);
+                        if (cnt <= 0) break;
+                        const uint32_t codes = vc[ch], nb = vn[ch];
+                        for (int q = 0; q < cnt; ++q) {
+                            const uint32_t code = ((codes >> (2 * q)) & 3u) |
+                                                  (((nb >> q) & 1u) << 2);
+                            myers_step32(s_ppeq[code], pv, mv, d, hbit);
+                            const int j = p0 + q + 1;
+                            if (j >= rlo && j <= rhi) dmin_rows = min(dmin_rows, d);
+                            if (j >= end_lo) dmin_end = min(dmin_end, d);
+                            if (j >= near_lo) dmin_near = min(dmin_near, d);
+                        }
                     }
                 }
                 if (!rows_free && (int)w.bmin + dmin_rows <= kf) keep = true;
@@ -2392,20 +2486,45 @@ __device__ __forceinline__ void band_dp2(const uint8_t* rm, const uint32_t* seq,
     score = ie - max(-origin, 0) - 2 * cost - v;
 }
 
-// Band kernel over one candidate list (fixed band width W, so every lane of a wave runs the same
-// code).  Per block round of 256 candidates: cheap checks first (score upper bound against the
-// slot's lower bound and current winner; cost-0 cells need no DP), then the surviving cells are
-// compacted in LDS — band-interior ones from the front, ones touching column 0 or the view end
-// from the back — so full waves run each DP variant.  The slot's best is the minimum key over all
-// its candidates (key order = locate's / best_match's / ReverseComplementer's selection order).
-template <int W>
+// The DP of one queued cell with the narrowest exact band for the wave: cells are sorted by cost
+// before a DP pass, so a wave's cells share a cost (or two neighbouring ones) and the wave runs
+// 2c + 1 diagonals for its largest cost c (wave-uniform branch; H >= c keeps the band exact).
+template <int C, int CMAX, bool EDGE>
+__device__ __forceinline__ void band_dp_cost(int wc, const uint8_t* rm, const uint32_t* seq,
+                                             const uint32_t* nmask, const TaskView& tv,
+                                             bool front, int ie, int je, int& cost, int& origin,
+                                             int& score) {
+    if constexpr (C < CMAX) {
+        if (wc <= C) {
+            band_dp2<2 * C + 1, EDGE>(rm, seq, nmask, tv, front, ie, je, cost, origin, score);
+            return;
+        }
+        band_dp_cost<C + 1, CMAX, EDGE>(wc, rm, seq, nmask, tv, front, ie, je, cost, origin,
+                                         score);
+    } else {
+        band_dp2<2 * C + 1, EDGE>(rm, seq, nmask, tv, front, ie, je, cost, origin, score);
+    }
+}
+
+// Band kernel over one candidate list (costs CMIN..CMAX; cost-0 cells need no DP).  Every block
+// takes 256 candidates at a time through cheap checks first (score upper bound against the slot's
+// lower bound and current winner; cost-0 cells are pure diagonals), and appends the survivors to
+// one of two LDS queues: band-interior cells, and cells whose band reaches column 0 or the view
+// end.  A queue runs a DP pass whenever it holds 256 cells (and once more, partially, at the end),
+// so the DP waves are full whatever the prune rate; a pass first sorts its cells by cost, so each
+// wave runs the narrowest band its cells allow (band_dp_cost).  The slot's best is the minimum
+// key over all its candidates (key order = locate's / best_match's / ReverseComplementer's order).
+template <int CMIN, int CMAX>
 __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
     // s_rm[i * kMaxAdapters + a]: bit c = adapter a's char i matches read code c.  Row-major, so
     // the lanes of a wave (one row i, different adapters) read neighbouring bytes: no bank
     // conflicts (an adapter-major table put every adapter's row i in one of 4 banks).
     __shared__ uint8_t s_rm[kMaxAdapters * 64];
-    __shared__ uint32_t s_q[256];
-    __shared__ uint32_t s_qi, s_qe, s_n;
+    __shared__ uint32_t s_q[2][512];                 // queued cells: [0] interior, [1] edge
+    __shared__ uint8_t s_qc[2][512];                 // their costs
+    __shared__ uint32_t s_sorted[256];
+    __shared__ uint8_t s_sc[256];
+    __shared__ uint32_t s_hist[8], s_nq[2], s_n;
     const DevPanel* P = R.panel;
     const int A = P->n_adapters;
     for (int x = threadIdx.x; x < 64 * A; x += blockDim.x) {
@@ -2416,8 +2535,8 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
         s_rm[i * kMaxAdapters + a] = (uint8_t)r;
     }
     if (threadIdx.x == 0) {
-        s_qi = 0;
-        s_qe = 0;
+        s_nq[0] = 0;
+        s_nq[1] = 0;
         s_n = 0;
     }
     __shared__ uint32_t s_spre[kShards + 1];
@@ -2426,7 +2545,76 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
     const uint32_t total = sm.total();
     const Cand* cl = R.cand[list];
     Outcome* outs = R.cand_out[list];
-    constexpr int H = W / 2;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+
+    // One DP pass over the top `cnt` (<= 256) cells of queue e (block-uniform call).
+    auto dp_pass = [&](int e, uint32_t cnt) {
+        const uint32_t lo = s_nq[e] - cnt;
+        if (threadIdx.x < 8) s_hist[threadIdx.x] = 0;
+        __syncthreads();
+        uint32_t ci = 0, cost = 0, pos = 0;
+        const bool have = threadIdx.x < cnt;
+        if (have) {
+            ci = s_q[e][lo + threadIdx.x];
+            cost = s_qc[e][lo + threadIdx.x];
+            pos = atomicAdd(&s_hist[cost], 1u);
+        }
+        __syncthreads();
+        if (have) {
+            uint32_t before = 0;
+            for (uint32_t c = 0; c < cost; ++c) before += s_hist[c];
+            s_sorted[before + pos] = ci;
+            s_sc[before + pos] = (uint8_t)cost;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            s_nq[e] = lo;
+            s_n += cnt;
+        }
+        if (64u * wave < cnt) {                      // waves with cells (wave-uniform)
+            const uint32_t last = min(64u * wave + 63u, cnt - 1u);
+            const int wc = (int)s_sc[last];          // the wave's largest cost (sorted)
+            if (threadIdx.x < cnt) {
+                const uint32_t cj = s_sorted[threadIdx.x];
+                const Cand c = cl[cj];
+                const uint32_t slot = slot_of(R, c.item, c.sub);
+                const int cst = c.cost, iend = c.iend;
+                const int j = (int)c.j;
+                const DevAdapter& ad = P->ad[c.a];
+                const uint64_t t = iend == ad.m ? (uint64_t)j : (uint64_t)c.len + 1 + iend;
+                TaskView tv;
+                tv.read = 0;
+                tv.n = c.n;
+                tv.strand = c.strand;
+                tv.start = c.start;
+                tv.len = c.len;
+                tv.off = c.off;
+                tv.o = c.o;
+                tv.a = c.a;
+                int c2, origin, score;
+                if (e == 0)
+                    band_dp_cost<CMIN == 0 ? 1 : CMIN, CMAX, false>(
+                        wc, s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend, j, c2,
+                        origin, score);
+                else
+                    band_dp_cost<CMIN == 0 ? 1 : CMIN, CMAX, true>(
+                        wc, s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend, j, c2,
+                        origin, score);
+                if (c2 != cst) atomicOr(R.flags, 2u);    // band / scan disagreement: bug
+                const int lr = iend + (origin < 0 ? origin : 0);
+                if (lr >= 0 && cst <= (int)ad.acc[lr]) {
+                    Outcome out;
+                    out.key = make_key(score, c.o, cst, c.a, t);
+                    out.origin = origin;
+                    out.pad = 0;
+                    atomicMin(&R.winner[slot], (unsigned long long)out.key);
+                    outs[cj] = out;
+                }
+            }
+        }
+        __syncthreads();
+    };
+
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
         const uint32_t ti = base + threadIdx.x;
         if (ti < total) {
@@ -2455,59 +2643,24 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
                     }
                 } else {
                     const int dx = j - iend;
-                    const bool edge = dx - H < 0 || j + H > (int)c.len;
-                    const uint32_t q = edge ? 255u - atomicAdd(&s_qe, 1u) : atomicAdd(&s_qi, 1u);
-                    s_q[q] = ci;
+                    const int H = CMAX;       // the widest band this kernel may run
+                    const int e = (dx - H < 0 || j + H > (int)c.len) ? 1 : 0;
+                    const uint32_t q = atomicAdd(&s_nq[e], 1u);
+                    s_q[e][q] = ci;
+                    s_qc[e][q] = (uint8_t)cost;
                 }
             }
             outs[ci] = out;
         }
         __syncthreads();
-        const uint32_t ni = s_qi, ne = s_qe;
-        const bool mine = threadIdx.x < ni || threadIdx.x >= 256u - ne;
-        if (mine) {
-            const uint32_t ci = s_q[threadIdx.x];
-            const Cand c = cl[ci];
-            const uint32_t slot = slot_of(R, c.item, c.sub);
-            const int cost = c.cost, iend = c.iend;
-            const int j = (int)c.j;
-            const DevAdapter& ad = P->ad[c.a];
-            const uint64_t t = iend == ad.m ? (uint64_t)j : (uint64_t)c.len + 1 + iend;
-            TaskView tv;
-            tv.read = 0;
-            tv.n = c.n;
-            tv.strand = c.strand;
-            tv.start = c.start;
-            tv.len = c.len;
-            tv.off = c.off;
-            tv.o = c.o;
-            tv.a = c.a;
-            int c2, origin, score;
-            if (threadIdx.x < ni)
-                band_dp2<W, false>(s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend,
-                                   j, c2, origin, score);
-            else
-                band_dp2<W, true>(s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend,
-                                  j, c2, origin, score);
-            if (c2 != cost) atomicOr(R.flags, 2u);    // band / scan disagreement: bug
-            const int lr = iend + (origin < 0 ? origin : 0);
-            if (lr >= 0 && cost <= (int)ad.acc[lr]) {
-                Outcome out;
-                out.key = make_key(score, c.o, cost, c.a, t);
-                out.origin = origin;
-                out.pad = 0;
-                atomicMin(&R.winner[slot], (unsigned long long)out.key);
-                outs[ci] = out;
-            }
-        }
-        const int nd = __syncthreads_count(mine);
-        if (threadIdx.x == 0) {
-            s_n += (uint32_t)nd;
-            s_qi = 0;
-            s_qe = 0;
-        }
+        for (int e = 0; e < 2; ++e)                 // full passes (each queue ends below 256)
+            while (s_nq[e] >= 256u) dp_pass(e, 256u);
+        // every thread has read the queue counts before any thread pushes again (a fast wave's
+        // next-round push would otherwise send a slow wave alone into dp_pass's barriers)
         __syncthreads();
     }
+    for (int e = 0; e < 2; ++e)
+        if (s_nq[e]) dp_pass(e, s_nq[e]);
     if (threadIdx.x == 0 && s_n) atomicAdd(R.diag + 1, s_n);
 }
 
@@ -2896,11 +3049,11 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     }
     hipEventRecord(c->ev[round * 3 + 1], st);
     if (band) {
-        hipLaunchKernelGGL(band_cand_kernel<7>, dim3(256 * 8), dim3(256), 0, st, R, 0);
+        hipLaunchKernelGGL((band_cand_kernel<0, 3>), dim3(256 * 8), dim3(256), 0, st, R, 0);
         if (c->band_wide[round])
-            hipLaunchKernelGGL(band_cand_kernel<15>, dim3(256 * 4), dim3(256), 0, st, R, 1);
+            hipLaunchKernelGGL((band_cand_kernel<4, 7>), dim3(256 * 4), dim3(256), 0, st, R, 1);
         else   // every cost in list 1 is <= 5: a band of 2 * 5 + 1 diagonals is exact
-            hipLaunchKernelGGL(band_cand_kernel<11>, dim3(256 * 4), dim3(256), 0, st, R, 1);
+            hipLaunchKernelGGL((band_cand_kernel<4, 5>), dim3(256 * 4), dim3(256), 0, st, R, 1);
         hipLaunchKernelGGL(select_cand_kernel, dim3(1024), dim3(256), 0, st, R);
         hipEventRecord(c->ev[round * 3 + 2], st);
         return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
