@@ -96,8 +96,11 @@ def spawn_ranks(n: int) -> int:
 
 METRIC = "Mreads/s two-round SP5×SP27 demux; % HBM roofline; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
-VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CUs x 4 SIMD32 x 2.4 GHz, 32-bit lane-ops
-VALU_CEILING_FILE = os.path.join(ROOT, "profiles", "r2_valu_ceiling.json")
+VALU_LANES = 256 * 128                      # lane-ops per shader cycle: 256 CUs x 4 SIMD32
+VALU_PEAK_TOPS = VALU_LANES * 2.4e9 / 1e12  # at the nominal 2.4 GHz, 32-bit lane-ops
+VALU_CEILING_FILE = os.path.join(ROOT, "profiles", "r3_valu_ceiling.json")
+if not os.path.exists(VALU_CEILING_FILE):
+    VALU_CEILING_FILE = os.path.join(ROOT, "profiles", "r2_valu_ceiling.json")
 
 
 def _valu_ceiling() -> float:
@@ -123,13 +126,48 @@ def pmc_table(workload: str, reads: int):
         return None
 
 
-def pmc_valu_insts(workload: str, reads: int, kernel: str, last_only: bool = False):
-    """SQ_INSTS_VALU of the kernel's launches in one PMC'd step (all launches, or the last)."""
+def pmc_valu_insts(workload: str, reads: int, kernel: str, last_only: bool = False,
+                   first_only: bool = False):
+    """SQ_INSTS_VALU of the kernel's launches in one PMC'd step (all launches, the last or the
+    first)."""
     pmc = pmc_table(workload, reads)
     launches = (pmc or {}).get("kernels", {}).get(kernel, [])
     if not launches:
         return None
-    return launches[-1]["valu_insts"] if last_only else sum(e["valu_insts"] for e in launches)
+    if last_only:
+        return launches[-1]["valu_insts"]
+    if first_only:
+        return launches[0]["valu_insts"]
+    return sum(e["valu_insts"] for e in launches)
+
+
+def pmc_clock(workload: str, reads: int, kernel: str, launch=None):
+    """Effective shader clock (GHz) of the kernel's PMC'd launches: GRBM_GUI_ACTIVE / 8 XCDs /
+    duration (MI355X_MICROARCH.md 'DVFS give-back'), time-weighted; None without the counter."""
+    pmc = pmc_table(workload, reads)
+    launches = (pmc or {}).get("kernels", {}).get(kernel, [])
+    if launch is not None:
+        launches = launches[launch:launch + 1]
+    pts = [(e["clock_ghz"], e["ms"]) for e in launches if e.get("clock_ghz")]
+    if not pts:
+        return None
+    return sum(c * m for c, m in pts) / sum(m for _, m in pts)
+
+
+def valu_roof(rate, clk_ghz, what: str):
+    """roofline['valu']: the dominant kernel's VALU issue rate against the peak at the clock it
+    ran at (and the nominal 2.4 GHz peak)."""
+    out = {"unit": "T lane-ops/s", "achieved": round(rate / 1e12, 3) if rate else None,
+           "nominal_peak": round(VALU_PEAK_TOPS, 2),
+           "measured_ceiling": round(VALU_CEILING / 1e12, 2), "what": what}
+    if rate and clk_ghz:
+        peak = VALU_LANES * clk_ghz * 1e9
+        out.update({"clock_ghz": round(clk_ghz, 3), "peak_at_clock": round(peak / 1e12, 3),
+                    "frac": round(rate / peak, 4),
+                    "clock_source": "GRBM_GUI_ACTIVE / 8 / launch duration of the PMC'd launches "
+                                    "(profiles/kernel_pmc.json); the ceiling's own clock is "
+                                    "stamped in-kernel (profiles/r3_valu_ceiling.json)"})
+    return out
 
 
 def filter_algorithmic_bytes(lengths: np.ndarray, n_windows: int) -> float:
@@ -160,11 +198,11 @@ def pmc_traffic(workload: str, reads: int):
 # the two-round pipeline's kernels and the live stage events that time them (per round)
 KERNEL_STAGES = (("dmx::filter_kernel", "filter"), ("dmx::verify_kernel", "verify"),
                  ("dmx::iscreen4_kernel", "screen"), ("dmx::wscan_kernel<true>", "wscan"),
-                 ("band_cand<7>+band_cand<11|15>+select_cand", "resolve"))
+                 ("band_cand<0,3>+band_cand<4,5|7>+select_cand", "resolve"))
 PMC_NAMES = {"filter": ["filter_kernel"], "verify": ["verify_kernel"],
              "screen": ["iscreen4_kernel", "iscreen_kernel"], "wscan": ["wscan_kernel<true>"],
-             "resolve": ["band_cand_kernel<7>", "band_cand_kernel<11>", "band_cand_kernel<15>",
-                         "select_cand_kernel"]}
+             "resolve": ["band_cand_kernel<0, 3>", "band_cand_kernel<4, 5>",
+                         "band_cand_kernel<4, 7>", "select_cand_kernel"]}
 
 
 def kernel_table(workload: str, reads: int, stage: dict, K: int, step_ms: float):
@@ -180,16 +218,23 @@ def kernel_table(workload: str, reads: int, stage: dict, K: int, step_ms: float)
                "share_of_step": round(sum(ms) / step_ms, 4)}
         if pmc is not None:
             valu = hbm = 0.0
+            clk = []
             for kn in PMC_NAMES[st]:
                 for launch in pmc["kernels"].get(kn, []):
                     valu += launch["valu_insts"]
                     hbm += launch["hbm_bytes"]
+                    if launch.get("clock_ghz"):
+                        clk.append((launch["clock_ghz"], launch["ms"]))
             if sum(ms) > 0 and valu > 0:
                 rate = valu * 64 / (sum(ms) / 1e3)
                 ent["valu_lane_ops_per_s"] = rate
                 ent["valu_frac_of_ceiling"] = round(rate / VALU_CEILING, 4)
                 ent["hbm_gb_per_s"] = round(hbm / (sum(ms) / 1e3) / 1e9, 1)
                 ent["hbm_frac"] = round(hbm / (sum(ms) / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                if clk:   # time-weighted effective clock of the PMC'd launches (GRBM_GUI_ACTIVE)
+                    g = sum(c * m for c, m in clk) / sum(m for _, m in clk)
+                    ent["clock_ghz"] = round(g, 3)
+                    ent["valu_frac_of_peak_at_clock"] = round(rate / (VALU_LANES * g * 1e9), 4)
         out[name] = ent
     if pmc is not None:
         out["_source"] = (pmc["source"] + "; VALU ceiling " + os.path.relpath(VALU_CEILING_FILE,
@@ -341,7 +386,11 @@ def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, 
                      "share_of_step": round(2 * filt_ms / (elapsed / K * 1e3), 4),
                      "note": "the dominant kernel (largest share of the step, see 'kernels'); "
                              "a bit-vector scan, VALU-bound by construction (DESIGN.md §5): "
-                             "'valu' gives its issue rate against the measured ceiling"},
+                             "roofline.valu gives its issue rate against the VALU peak at the "
+                             "clock it ran at",
+                     "valu": valu_roof(col_rate * ops_col if ops_col else None,
+                                       pmc_clock(args.workload, args.reads, "filter_kernel"),
+                                       "dmx::filter_kernel, both rounds")},
         "valu": {"filter_columns_per_s": col_rate,
                  "filter_lane_ops_per_column": ops_col,
                  "filter_lane_ops_per_s": col_rate * ops_col if ops_col else None,
@@ -374,6 +423,9 @@ def linked_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen
     L = lengths.astype(np.float64)
     alg_bytes = float(np.sum(np.ceil(L / 4) + np.ceil(L / 8) + 12.0))
     achieved = alg_bytes / (scan_ms / 1e3) / 1e9
+    traffic, traffic_src = pmc_traffic("c5", args.reads)
+    vi = pmc_valu_insts("c5", args.reads, "scan_kernel<true>", first_only=True)
+    rate = vi * 64 / (scan_ms / 1e3) if vi else None
     return {
         "metric": "Mreads/s linked-primer trimming (config 5, cutadapt -g F...R per pair)",
         "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
@@ -386,10 +438,14 @@ def linked_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen
                    "pairs": A0, "reads_per_gpu": args.shards, "reads_total": args.total_reads,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": round(alg_bytes),
                      "kernel": "dmx::scan_kernel<true>", "avg_launch_ms": round(scan_ms, 3),
-                     "note": "VALU-bound bit-vector scan (DESIGN.md §5)"},
+                     "note": "VALU-bound bit-vector scan (DESIGN.md §5); the round-1 launch "
+                             "(every front primer over every consensus)",
+                     "valu": valu_roof(rate, pmc_clock("c5", args.reads, "scan_kernel<true>", 0),
+                                       "dmx::scan_kernel<true>, round 1 (fronts)")},
         "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
         "trimmed_fraction": round(trimmed / max(1, len(lengths)), 4),
         "gen_s": round(gen_s, 1),
@@ -561,33 +617,57 @@ def main():
     pcie = None
     if host_batch is not None and not args.no_pcie:
         # the boundary's host-memory path: upload, both rounds, download of every result, with
-        # copies overlapped with kernels (dmx_run's double-buffered chunks); not the headline
-        ctx.sync()
-        barrier_sync()
-        t1 = time.perf_counter()
-        ctx.run(host_batch)
-        ctx.sync()
-        barrier_sync()
-        pe = time.perf_counter() - t1
-        if dist is not None:
-            import torch
-            tt = torch.tensor([pe], dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            pe = float(tt.item())
+        # copies overlapped with kernels (dmx_run's double-buffered chunks); not the headline.
+        # Inputs as a resident host pipeline holds them: the no-match mask as its exceptions
+        # (dmx_mask_exceptions, part of packing) and the batch buffers page-locked once
+        # (dmx_host_register, as reused batch buffers are), both outside the timed region.
+        def timed(fn):
+            ctx.sync()
+            barrier_sync()
+            t1 = time.perf_counter()
+            fn(host_batch)
+            ctx.sync()
+            barrier_sync()
+            pe = time.perf_counter() - t1
+            if dist is not None:
+                import torch
+                tt = torch.tensor([pe], dtype=torch.float64)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                pe = float(tt.item())
+            return pe
+        pe_dense = timed(ctx.run)                    # dense mask, pageable memory
+        exc_idx, exc_val = host_batch.exceptions()
+        pinned = lib.host_register([host_batch.seq2b, host_batch.offsets, host_batch.lengths,
+                                    exc_idx, exc_val])
+        try:
+            pe = timed(ctx.run_sparse)
+        finally:
+            lib.host_unregister(pinned)
         pcie = {"value": round(args.total_reads / pe / 1e6, 4), "unit": "Mreads/s",
                 "ms": round(pe * 1e3, 3),
                 "chunk_reads": int(os.environ.get("DMX_RUN_CHUNK", 1 << 21)),
-                # 2-bit codes, the data half of the 1-bit mask, offsets, lengths
-                "h2d_bytes_per_gpu": int(host_batch.seq2b.nbytes +
-                                         min(host_batch.nmask.nbytes,
-                                             host_batch.seq2b.nbytes // 2 + 8) +
-                                         host_batch.offsets.nbytes +
+                # 2-bit codes, the mask's nonzero words (index + value), offsets, lengths
+                "h2d_bytes_per_gpu": int(host_batch.seq2b.nbytes + exc_idx.nbytes +
+                                         exc_val.nbytes + host_batch.offsets.nbytes +
                                          host_batch.lengths.nbytes),
+                "h2d_bytes_per_read": round((host_batch.seq2b.nbytes + exc_idx.nbytes +
+                                             exc_val.nbytes + host_batch.offsets.nbytes +
+                                             host_batch.lengths.nbytes) /
+                                            max(1, host_batch.n_reads), 1),
                 "d2h_bytes_per_gpu": int(args.reads * 40),   # dmx_result
-                "note": "dmx_run from pageable host memory (one call, inputs not resident): "
-                        "uploads, both rounds, download of every per-read result; the next "
-                        "chunk's upload and the previous chunk's download overlap each chunk's "
-                        "kernels"}
+                "pinned_buffers": len(pinned),
+                "pageable_dense": {"value": round(args.total_reads / pe_dense / 1e6, 4),
+                                   "ms": round(pe_dense * 1e3, 3),
+                                   "h2d_bytes_per_gpu": int(
+                                       host_batch.seq2b.nbytes +
+                                       min(host_batch.nmask.nbytes,
+                                           host_batch.seq2b.nbytes // 2 + 8) +
+                                       host_batch.offsets.nbytes + host_batch.lengths.nbytes)},
+                "note": "dmx_run_sparse from page-locked host memory (one call, inputs not "
+                        "resident): uploads (2-bit codes + the no-match mask's nonzero words), "
+                        "both rounds, download of every per-read result; the next chunk's "
+                        "upload and the previous chunk's download overlap each chunk's kernels. "
+                        "pageable_dense: dmx_run with the dense mask from pageable memory"}
         del host_batch
 
     if pcie is not None:

@@ -100,6 +100,22 @@ int dmx_pack(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens
 int dmx_run(dmx_ctx* ctx, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
             const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out);
 
+/* As dmx_run, with the no-match mask given sparsely: its nonzero 32-bit words (mask word index
+ * = nt / 32, as in dmx_pack's nmask) as strictly increasing exc_idx[] with their values
+ * exc_val[].  Almost every nt of a read is A/C/G/T, so this uploads ~1% of the dense bitmap's
+ * bytes; the device zero-fills the mask and scatters the exceptions.  Same results as dmx_run. */
+int dmx_run_sparse(dmx_ctx* ctx, const uint32_t* seq2b, const uint32_t* exc_idx,
+                   const uint32_t* exc_val, size_t n_exc, const uint64_t* offsets,
+                   const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out);
+/* Host helper (no GPU): the nonzero words of a dmx_pack no-match mask of n_words words, in
+ * increasing index order (first `cap` written); returns their total number. */
+size_t dmx_mask_exceptions(const uint32_t* nmask, size_t n_words, uint32_t* out_idx,
+                           uint32_t* out_val, size_t cap);
+/* Page-lock (pin) / release caller host memory that batches are uploaded from (reused batch
+ * buffers): pinned uploads run at the DMA rate instead of through pageable staging. */
+int dmx_host_register(void* ptr, size_t bytes);
+int dmx_host_unregister(void* ptr);
+
 /* Number of visible HIP devices (0 if none). */
 int dmx_device_count(void);
 

@@ -8,9 +8,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -273,12 +275,14 @@ void dmx_close(dmx_ctx* c) {
             if (c->d_cand[r][l]) hipFree(c->d_cand[r][l]);
             if (c->d_cand_out[r][l]) hipFree(c->d_cand_out[r][l]);
         }
-    void* alt[] = {c->alt.seq_alloc, c->alt.nmask_alloc, c->alt.offs, c->alt.lens, c->alt.res};
+    void* alt[] = {c->alt.seq_alloc, c->alt.nmask_alloc, c->alt.offs, c->alt.lens, c->alt.res,
+                   c->alt.exc, c->d_exc};
     for (void* b : alt)
         if (b) hipFree(b);
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
     if (c->cstream) hipStreamDestroy(c->cstream);
+    if (c->dstream) hipStreamDestroy(c->dstream);
     hipStreamDestroy(c->stream);
     delete c;
 }
@@ -544,9 +548,35 @@ int dmx_pack(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens
     return DMX_OK;
 }
 
-int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
-             const uint32_t* lens, size_t n_words, size_t n_reads) {
-    if (!c || (n_reads && (!seq2b || !nmask || !offsets || !lens))) return DMX_E_INVALID;
+}  // extern "C"
+
+namespace {
+
+// Mask words [mw0, mw0 + nmw) of the caller's batch into the resident set's d_nmask on stream s:
+// a copy of the dense bitmap, or zero-fill + a scatter of the exceptions in that range (sorted
+// by index, so the range is one binary search).  The exceptions are staged in the set's d_exc.
+int upload_mask(Ctx* c, const MaskSrc& m, size_t mw0, size_t nmw, hipStream_t s) {
+    if (m.dense) {
+        CK(hipMemcpyAsync(c->d_nmask, m.dense + mw0, nmw * 4, hipMemcpyHostToDevice, s));
+        return DMX_OK;
+    }
+    CK(hipMemsetAsync(c->d_nmask, 0, nmw * 4, s));
+    const uint32_t* lo = std::lower_bound(m.idx, m.idx + m.n, (uint32_t)mw0);
+    const uint32_t* hi = std::lower_bound(lo, m.idx + m.n, (uint32_t)(mw0 + nmw));
+    const size_t n = (size_t)(hi - lo), first = (size_t)(lo - m.idx);
+    if (!n) return DMX_OK;
+    if (c->exc_cap < n || !c->d_exc) {
+        int rc;
+        if ((rc = dev_alloc(c, &c->d_exc, 2 * n))) return rc;
+        c->exc_cap = n;
+    }
+    CK(hipMemcpyAsync(c->d_exc, m.idx + first, n * 4, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(c->d_exc + n, m.val + first, n * 4, hipMemcpyHostToDevice, s));
+    return launch_mask_scatter(c->d_nmask, c->d_exc, (uint32_t)n, (uint32_t)mw0, s);
+}
+
+int load_impl(dmx_ctx* c, const uint32_t* seq2b, const MaskSrc& mask, const uint64_t* offsets,
+              const uint32_t* lens, size_t n_words, size_t n_reads) {
     if (n_reads >= (1ull << 31)) {
         c->err = "too many reads in one batch";
         return DMX_E_UNSUPPORTED;
@@ -585,7 +615,7 @@ int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uin
     c->n_reads = n_reads;
     c->n_words = n_words;
     CK(hipMemcpyAsync(c->d_seq, seq2b, n_words * 4, hipMemcpyHostToDevice, c->stream));
-    CK(hipMemcpyAsync(c->d_nmask, nmask, nmw * 4, hipMemcpyHostToDevice, c->stream));
+    if ((rc = upload_mask(c, mask, 0, nmw, c->stream))) return rc;
     if (n_reads) {
         CK(hipMemcpyAsync(c->d_offs, offsets, n_reads * 8, hipMemcpyHostToDevice, c->stream));
         CK(hipMemcpyAsync(c->d_lens, lens, n_reads * 4, hipMemcpyHostToDevice, c->stream));
@@ -595,6 +625,18 @@ int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uin
     c->chunked = false;
     chop_invalidate(c);
     return DMX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
+             const uint32_t* lens, size_t n_words, size_t n_reads) {
+    if (!c || (n_reads && (!seq2b || !nmask || !offsets || !lens))) return DMX_E_INVALID;
+    MaskSrc m;
+    m.dense = nmask;
+    return load_impl(c, seq2b, m, offsets, lens, n_words, n_reads);
 }
 
 int dmx_exec(dmx_ctx* c) {
@@ -778,7 +820,8 @@ namespace {
 // One chunk of a chunked dmx_run: reads [lo, hi) of the caller's dmx_pack batch, rebased.
 struct Chunk {
     size_t lo, hi, w0, words;
-    std::vector<uint64_t> offs;
+    uint64_t g0;      // the chunk's nt base: its offsets are rebased by -g0 on the device
+    size_t exc_lo, exc_n;   // its range of the sparse mask's exceptions
 };
 
 // The buffers of the resident batch (Ctx fields) <-> the second set.
@@ -791,6 +834,8 @@ void swap_inputs(Ctx* c) {
     std::swap(c->cap_words, c->alt.cap_words);
     std::swap(c->in_cap_reads, c->alt.cap_reads);
     std::swap(c->res_cap, c->alt.res_cap);
+    std::swap(c->d_exc, c->alt.exc);
+    std::swap(c->exc_cap, c->alt.exc_cap);
     std::swap(c->n_words, c->alt.n_words);
     c->d_seq = c->d_seq_alloc + kGuardWords;
     c->d_nmask = c->d_nmask_alloc + kGuardWords;
@@ -798,8 +843,11 @@ void swap_inputs(Ctx* c) {
 
 // Upload one chunk into the current set on the copy stream (host-blocking for pageable
 // memory, while the compute stream keeps running), zeroing a longer previous chunk's tail.
-int upload_chunk(Ctx* c, const Chunk& k, const uint32_t* seq2b, const uint32_t* nmask,
-                 const uint32_t* lens) {
+// Upload one chunk into the current set on the copy stream (asynchronous: the caller syncs
+// cstream before the set is used), zeroing a longer previous chunk's tail.  Offsets go up as the
+// caller gave them and are rebased on the device.
+int upload_chunk(Ctx* c, const Chunk& k, const uint32_t* seq2b, const MaskSrc& mask,
+                 const uint64_t* offsets, const uint32_t* lens) {
     hipStream_t s = c->cstream;
     // the nmask words of a range (1 bit per nt: half as many); the rest of the buffer stays
     // zero (the guard)
@@ -809,13 +857,32 @@ int upload_chunk(Ctx* c, const Chunk& k, const uint32_t* seq2b, const uint32_t* 
         CK(hipMemsetAsync(c->d_seq + k.words, 0, (c->n_words - k.words) * 4, s));
     if (old_nmw > nmw) CK(hipMemsetAsync(c->d_nmask + nmw, 0, (old_nmw - nmw) * 4, s));
     CK(hipMemcpyAsync(c->d_seq, seq2b + k.w0, k.words * 4, hipMemcpyHostToDevice, s));
-    CK(hipMemcpyAsync(c->d_nmask, nmask + k.w0 / 2, nmw * 4, hipMemcpyHostToDevice, s));
+    int rc;
+    if ((rc = upload_mask(c, mask, k.w0 / 2, nmw, s))) return rc;
     const size_t n = k.hi - k.lo;
-    CK(hipMemcpyAsync(c->d_offs, k.offs.data(), n * 8, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(c->d_offs, offsets + k.lo, n * 8, hipMemcpyHostToDevice, s));
+    if ((rc = launch_rebase_offsets(c->d_offs, (uint32_t)n, k.g0, s))) return rc;
     CK(hipMemcpyAsync(c->d_lens, lens + k.lo, n * 4, hipMemcpyHostToDevice, s));
-    CK(hipStreamSynchronize(s));
     c->n_words = k.words;
     return DMX_OK;
+}
+
+// fn(lo, hi) over [0, n) on up to 16 host threads
+extern "C++" template <class F>
+void parallel_ranges(size_t n, F fn) {
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t nth = n < (1u << 16) ? 1 : hw;
+    if (nth == 1) {
+        fn((size_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + nth - 1) / nth;
+    for (size_t t = 0; t < nth; ++t) {
+        const size_t lo = t * per, hi = std::min(n, lo + per);
+        if (lo < hi) th.emplace_back(fn, lo, hi);
+    }
+    for (auto& x : th) x.join();
 }
 
 int alloc_set(Ctx* c, size_t words, size_t reads) {
@@ -843,11 +910,11 @@ int alloc_set(Ctx* c, size_t words, size_t reads) {
 // k+1 and downloads chunk k-1's results on the copy stream; per-bin counts are summed on the
 // host and left in d_counts for dmx_counts / dmx_allreduce_counts.  The batch must come from
 // dmx_pack (offsets on kPackAlign boundaries after DMX_PACK_PAD).
-int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
-                const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out,
-                size_t per) {
+int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const MaskSrc& nmask,
+                const uint64_t* offsets, const uint32_t* lens, size_t n_words, size_t n_reads,
+                dmx_result* out, size_t per) {
     std::vector<Chunk> ch;
-    size_t maxw = 0, maxn = 0;
+    size_t maxw = 0, maxn = 0, maxe = 0;
     for (size_t lo = 0; lo < n_reads; lo += per) {
         Chunk k;
         k.lo = lo;
@@ -856,25 +923,46 @@ int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const 
             c->err = "dmx_run: offsets must come from dmx_pack";
             return DMX_E_INVALID;
         }
-        const uint64_t g0 = offsets[lo] - DMX_PACK_PAD;   // a 32-nt (nmask word) boundary
-        k.offs.resize(k.hi - lo);
-        uint64_t end = 0;
-        for (size_t r = lo; r < k.hi; ++r) {
-            k.offs[r - lo] = offsets[r] - g0;
-            end = std::max<uint64_t>(end, k.offs[r - lo] + lens[r]);
-        }
-        k.w0 = (size_t)(g0 / 16);
-        if (k.w0 >= n_words) {
+        k.g0 = offsets[lo] - DMX_PACK_PAD;   // a 32-nt (nmask word) boundary
+        ch.push_back(k);
+    }
+    // each chunk's end (the largest rebased offset + length): one parallel pass over the reads
+    std::vector<uint64_t> ends(ch.size(), 0);
+    {
+        std::vector<std::vector<uint64_t>> part;
+        std::mutex mu;
+        parallel_ranges(n_reads, [&](size_t lo, size_t hi) {
+            std::vector<uint64_t> e(ch.size(), 0);
+            for (size_t r = lo; r < hi; ++r) {
+                const size_t k = r / per;
+                e[k] = std::max<uint64_t>(e[k], offsets[r] + lens[r] - ch[k].g0);
+            }
+            std::lock_guard<std::mutex> g(mu);
+            part.push_back(std::move(e));
+        });
+        for (const auto& e : part)
+            for (size_t k = 0; k < ch.size(); ++k) ends[k] = std::max(ends[k], e[k]);
+    }
+    for (size_t k = 0; k < ch.size(); ++k) {
+        Chunk& x = ch[k];
+        x.w0 = (size_t)(x.g0 / 16);
+        if (x.w0 >= n_words) {
             c->err = "dmx_run: offsets beyond the packed buffer";
             return DMX_E_INVALID;
         }
-        k.words = std::min(n_words - k.w0, (size_t)((end + DMX_PACK_PAD + 31) / 32 * 2 + 4));
-        maxw = std::max(maxw, k.words);
-        maxn = std::max(maxn, k.hi - lo);
-        ch.push_back(std::move(k));
+        x.words = std::min(n_words - x.w0, (size_t)((ends[k] + DMX_PACK_PAD + 31) / 32 * 2 + 4));
+        maxw = std::max(maxw, x.words);
+        maxn = std::max(maxn, x.hi - x.lo);
+        if (!nmask.dense) {   // the chunk's exceptions: mask words [w0 / 2, w0 / 2 + nmw)
+            const size_t mw0 = x.w0 / 2, nmw = std::min(x.words, (x.words + 1) / 2 + 2);
+            const uint32_t* a = std::lower_bound(nmask.idx, nmask.idx + nmask.n, (uint32_t)mw0);
+            const uint32_t* b = std::lower_bound(a, nmask.idx + nmask.n, (uint32_t)(mw0 + nmw));
+            maxe = std::max(maxe, (size_t)(b - a));
+        }
     }
     CK(hipSetDevice(c->device));
     if (!c->cstream) CK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    if (!c->dstream) CK(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
     int rc;
     // both sets sized for the largest chunk; each set's capacities travel with its buffers
     // (swap_inputs), apart from the pipeline's cap_reads
@@ -889,11 +977,19 @@ int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const 
         swap_inputs(c);
         if (rc) return rc;
     }
+    for (int set = 0; set < 2 && maxe; ++set) {   // exception staging, sized before the loop
+        if (c->exc_cap < maxe || !c->d_exc) {
+            if ((rc = dev_alloc(c, &c->d_exc, 2 * maxe))) return rc;
+            c->exc_cap = maxe;
+        }
+        swap_inputs(c);
+    }
     c->n_reads = maxn;
     chop_invalidate(c);
     c->chunked = false;
     std::vector<uint64_t> total, part;
-    if ((rc = upload_chunk(c, ch[0], seq2b, nmask, lens))) return rc;
+    if ((rc = upload_chunk(c, ch[0], seq2b, nmask, offsets, lens))) return rc;
+    CK(hipStreamSynchronize(c->cstream));
     for (size_t i = 0; i < ch.size(); ++i) {
         const size_t n = ch[i].hi - ch[i].lo;
         c->n_reads = n;
@@ -901,16 +997,17 @@ int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const 
         for (;; ++attempt) {
             if ((rc = dmx_exec(c))) return rc;
             // meanwhile: the next chunk into the other set, the previous chunk's results out
+            // (uploads on cstream and the download on dstream run in both directions at once;
+            // the other set's inputs and its result array are disjoint buffers)
             if (attempt == 0) {
                 swap_inputs(c);
                 if (i + 1 < ch.size() &&
-                    (rc = upload_chunk(c, ch[i + 1], seq2b, nmask, lens)))
+                    (rc = upload_chunk(c, ch[i + 1], seq2b, nmask, offsets, lens)))
                     return rc;
                 if (i > 0) {
                     const size_t pn = ch[i - 1].hi - ch[i - 1].lo;
                     CK(hipMemcpyAsync(out + ch[i - 1].lo, c->d_res, pn * sizeof(dmx_result),
-                                      hipMemcpyDeviceToHost, c->cstream));
-                    CK(hipStreamSynchronize(c->cstream));
+                                      hipMemcpyDeviceToHost, c->dstream));
                 }
                 swap_inputs(c);
             }
@@ -935,6 +1032,8 @@ int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const 
         CK(hipMemcpy(part.data(), c->d_counts, c->n_counts * 8, hipMemcpyDeviceToHost));
         if (total.size() != part.size()) total.assign(part.size(), 0);
         for (size_t x = 0; x < part.size(); ++x) total[x] += part[x];
+        CK(hipStreamSynchronize(c->cstream));   // the next chunk is in, the previous one out
+        CK(hipStreamSynchronize(c->dstream));
         swap_inputs(c);   // the next chunk (uploaded above) becomes the resident batch
     }
     // the last chunk's results sit in the other set now
@@ -952,9 +1051,10 @@ int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const 
 
 }  // namespace
 
-int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
-            const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out) {
-    if (!c || (n_reads && (!seq2b || !nmask || !offsets || !lens || !out))) return DMX_E_INVALID;
+namespace {
+
+int run_impl(dmx_ctx* c, const uint32_t* seq2b, const MaskSrc& mask, const uint64_t* offsets,
+             const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out) {
     size_t per = (size_t)1 << 21;   // reads per chunk of an overlapped run
     if (const char* e = std::getenv("DMX_RUN_CHUNK")) per = (size_t)std::strtoull(e, nullptr, 10);
     // chunking rebases every chunk on a 32-nt boundary, which needs dmx_pack's layout at the
@@ -967,15 +1067,22 @@ int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint
             c->err = "panels not set for this mode";
             return DMX_E_STATE;
         }
-        for (size_t r = 0; r < n_reads; ++r)
-            if (offsets[r] < 16 || (offsets[r] + lens[r] + 64) > (uint64_t)n_words * 16 ||
-                lens[r] >= (1u << 30)) {
-                c->err = "read offsets/lengths do not fit the packed buffer (use dmx_pack)";
-                return DMX_E_INVALID;
-            }
-        return run_chunked(c, seq2b, nmask, offsets, lens, n_words, n_reads, out, per);
+        std::atomic<bool> bad{false};
+        parallel_ranges(n_reads, [&](size_t lo, size_t hi) {
+            for (size_t r = lo; r < hi; ++r)
+                if (offsets[r] < 16 || (offsets[r] + lens[r] + 64) > (uint64_t)n_words * 16 ||
+                    lens[r] >= (1u << 30)) {
+                    bad = true;
+                    return;
+                }
+        });
+        if (bad) {
+            c->err = "read offsets/lengths do not fit the packed buffer (use dmx_pack)";
+            return DMX_E_INVALID;
+        }
+        return run_chunked(c, seq2b, mask, offsets, lens, n_words, n_reads, out, per);
     }
-    int rc = dmx_load(c, seq2b, nmask, offsets, lens, n_words, n_reads);
+    int rc = load_impl(c, seq2b, mask, offsets, lens, n_words, n_reads);
     if (rc) return rc;
     for (int attempt = 0; attempt < 8; ++attempt) {
         if ((rc = dmx_exec(c))) return rc;
@@ -995,6 +1102,88 @@ int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint
     }
     c->err = "candidate cluster buffer overflow";
     return DMX_E_NOMEM;
+}
+
+}  // namespace
+
+int dmx_run(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
+            const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out) {
+    if (!c || (n_reads && (!seq2b || !nmask || !offsets || !lens || !out))) return DMX_E_INVALID;
+    MaskSrc m;
+    m.dense = nmask;
+    return run_impl(c, seq2b, m, offsets, lens, n_words, n_reads, out);
+}
+
+int dmx_run_sparse(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* exc_idx,
+                   const uint32_t* exc_val, size_t n_exc, const uint64_t* offsets,
+                   const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out) {
+    if (!c || (n_reads && (!seq2b || !offsets || !lens || !out)) ||
+        (n_exc && (!exc_idx || !exc_val)))
+        return DMX_E_INVALID;
+    const size_t nmw = std::min(n_words, (n_words + 1) / 2 + 2);
+    std::atomic<bool> bad{false};
+    parallel_ranges(n_exc, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i)
+            if (exc_idx[i] >= nmw || (i && exc_idx[i] <= exc_idx[i - 1])) {
+                bad = true;
+                return;
+            }
+    });
+    if (bad) {
+        c->err = "dmx_run_sparse: exception indices must be strictly increasing mask words";
+        return DMX_E_INVALID;
+    }
+    MaskSrc m;
+    m.idx = exc_idx;
+    m.val = exc_val;
+    m.n = n_exc;
+    return run_impl(c, seq2b, m, offsets, lens, n_words, n_reads, out);
+}
+
+size_t dmx_mask_exceptions(const uint32_t* nmask, size_t n_words, uint32_t* out_idx,
+                           uint32_t* out_val, size_t cap) {
+    if (!nmask) return 0;
+    const size_t nmw = std::min(n_words, (n_words + 1) / 2 + 2);   // the words carrying data
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t nth = nmw < (1u << 20) ? 1 : hw;
+    std::vector<size_t> cnt(nth + 1, 0);
+    const size_t per = (nmw + nth - 1) / nth;
+    auto count = [&](size_t t) {
+        size_t n = 0;
+        for (size_t w = t * per, e = std::min(nmw, w + per); w < e; ++w) n += nmask[w] != 0;
+        cnt[t + 1] = n;
+    };
+    auto fill = [&](size_t t) {
+        size_t o = cnt[t];
+        for (size_t w = t * per, e = std::min(nmw, w + per); w < e; ++w)
+            if (nmask[w]) {
+                if (o < cap) {
+                    out_idx[o] = (uint32_t)w;
+                    out_val[o] = nmask[w];
+                }
+                ++o;
+            }
+    };
+    auto par = [&](auto fn) {
+        if (nth == 1) return fn((size_t)0);
+        std::vector<std::thread> th;
+        for (size_t t = 0; t < nth; ++t) th.emplace_back(fn, t);
+        for (auto& x : th) x.join();
+    };
+    par(count);
+    for (size_t t = 0; t < nth; ++t) cnt[t + 1] += cnt[t];
+    if (out_idx && out_val && cap) par(fill);
+    return cnt[nth];
+}
+
+int dmx_host_register(void* p, size_t bytes) {
+    if (!p || !bytes) return DMX_E_INVALID;
+    return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? DMX_OK : DMX_E_HIP;
+}
+
+int dmx_host_unregister(void* p) {
+    if (!p) return DMX_E_INVALID;
+    return hipHostUnregister(p) == hipSuccess ? DMX_OK : DMX_E_HIP;
 }
 
 int dmx_device_count(void) {

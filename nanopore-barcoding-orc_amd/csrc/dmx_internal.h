@@ -48,6 +48,8 @@ struct Ctx {
     uint32_t* d_nmask_alloc = nullptr;  // (the filter loads whole aligned 64-nt blocks)
     uint64_t* d_offs = nullptr;
     uint32_t* d_lens = nullptr;
+    uint32_t* d_exc = nullptr;          // sparse no-match mask staging: [idx][val] (dmx_run_sparse)
+    size_t exc_cap = 0;
 
     // dmx_run of a large batch: chunks alternate between the buffers above and this second
     // set (inputs + results), so the next chunk's upload and the previous chunk's download
@@ -58,10 +60,12 @@ struct Ctx {
         uint64_t* offs = nullptr;
         uint32_t* lens = nullptr;
         dmx_result* res = nullptr;
-        // capacities travel with their buffers (swap_inputs): words, offs/lens, res
-        size_t cap_words = 0, cap_reads = 0, res_cap = 0, n_words = 0;
+        uint32_t* exc = nullptr;
+        // capacities travel with their buffers (swap_inputs): words, offs/lens, res, exceptions
+        size_t cap_words = 0, cap_reads = 0, res_cap = 0, n_words = 0, exc_cap = 0;
     } alt;
-    hipStream_t cstream = nullptr;      // copies of chunked runs
+    hipStream_t cstream = nullptr;      // uploads of chunked runs
+    hipStream_t dstream = nullptr;      // result downloads of chunked runs (the other direction)
     bool chunked = false;               // the last dmx_run was chunked: dmx_fetch is refused
 
     // pipeline state
@@ -113,6 +117,20 @@ int reset_counts(Ctx* c);      // size d_counts for the current panels/mode and 
 void chop_invalidate(Ctx* c);   // a new dmx_load makes the last dmx_chop_exec's results stale
 int launch_round(Ctx* c, int round, hipStream_t st);
 int launch_finalize(Ctx* c, int round, hipStream_t st);
+// offs[i] -= g0 for a chunk's offsets uploaded as the caller gave them (stream st)
+int launch_rebase_offsets(uint64_t* offs, uint32_t n, uint64_t g0, hipStream_t st);
+// mask[idx[i] - base] = val[i] for the n staged exceptions at d_exc ([idx][val]); stream st
+int launch_mask_scatter(uint32_t* mask, const uint32_t* d_exc, uint32_t n, uint32_t base,
+                        hipStream_t st);
+
+// Where a batch's no-match mask comes from: the dense bitmap (1 bit per nt) of dmx_pack, or its
+// nonzero words as sorted (index, value) exceptions (dmx_mask_exceptions, dmx_run_sparse).
+struct MaskSrc {
+    const uint32_t* dense = nullptr;
+    const uint32_t* idx = nullptr;
+    const uint32_t* val = nullptr;
+    size_t n = 0;
+};
 
 }  // namespace dmx
 

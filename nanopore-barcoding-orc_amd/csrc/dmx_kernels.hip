@@ -3078,6 +3078,32 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
 }
 
+__global__ void mask_scatter_kernel(uint32_t* mask, const uint32_t* exc, uint32_t n,
+                                    uint32_t base) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        mask[exc[i] - base] = exc[n + i];
+}
+
+__global__ void rebase_offsets_kernel(uint64_t* offs, uint32_t n, uint64_t g0) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        offs[i] -= g0;
+}
+
+int launch_rebase_offsets(uint64_t* offs, uint32_t n, uint64_t g0, hipStream_t st) {
+    if (!n) return DMX_OK;
+    const uint32_t grid = min((n + 255u) / 256u, 2048u);
+    hipLaunchKernelGGL(rebase_offsets_kernel, dim3(grid), dim3(256), 0, st, offs, n, g0);
+    return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
+}
+
+int launch_mask_scatter(uint32_t* mask, const uint32_t* d_exc, uint32_t n, uint32_t base,
+                        hipStream_t st) {
+    if (!n) return DMX_OK;
+    const uint32_t grid = min((n + 255u) / 256u, 1024u);
+    hipLaunchKernelGGL(mask_scatter_kernel, dim3(grid), dim3(256), 0, st, mask, d_exc, n, base);
+    return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
+}
+
 int launch_finalize(Ctx* c, int round, hipStream_t st) {
     FinalArgs F;
     F.lens = c->d_lens;

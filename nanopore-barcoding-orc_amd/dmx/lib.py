@@ -35,7 +35,8 @@ EXPORTS = ["dmx_abi_version", "dmx_open", "dmx_close", "dmx_last_error", "dmx_se
            "dmx_sync", "dmx_fetch", "dmx_counts", "dmx_stats", "dmx_device_count",
            "dmx_run_multi", "dmx_locate", "dmx_chop_set", "dmx_chop_exec", "dmx_chop_fetch",
            "dmx_chop_stats", "dmx_comm_unique_id", "dmx_comm_init_rank", "dmx_comm_init_all",
-           "dmx_comm_size", "dmx_allreduce_counts", "dmx_debug_fetch"]
+           "dmx_comm_size", "dmx_allreduce_counts", "dmx_debug_fetch", "dmx_run_sparse",
+           "dmx_mask_exceptions", "dmx_host_register", "dmx_host_unregister"]
 COMM_ID_BYTES = 128
 
 LOC_IGNORE_CASE, LOC_ONLY_POSITIVE = 0x1, 0x2
@@ -120,6 +121,11 @@ def load() -> ctypes.CDLL:
     L.dmx_comm_size.argtypes = [P]
     L.dmx_allreduce_counts.argtypes = [P, c_u64p, c_size]
     L.dmx_debug_fetch.argtypes = [P, c_int, c_int, P, c_size]
+    L.dmx_run_sparse.argtypes = [P, P, P, P, c_size, c_u64p, P, c_size, c_size, P]
+    L.dmx_mask_exceptions.argtypes = [P, c_size, P, P, c_size]
+    L.dmx_mask_exceptions.restype = c_size
+    L.dmx_host_register.argtypes = [P, c_size]
+    L.dmx_host_unregister.argtypes = [P]
     if L.dmx_abi_version() != 3:
         raise DmxError("libdmx ABI mismatch")
     _lib = L
@@ -136,6 +142,18 @@ class Packed:
     @property
     def n_reads(self) -> int:
         return int(len(self.lengths))
+
+    def exceptions(self):
+        """The no-match mask's nonzero words as (indices, values) (dmx_mask_exceptions)."""
+        if getattr(self, "_exc", None) is None:
+            L = load()
+            n = L.dmx_mask_exceptions(self.nmask.ctypes.data, self.n_words, None, None, 0)
+            idx = np.empty(max(n, 1), dtype=np.uint32)
+            val = np.empty(max(n, 1), dtype=np.uint32)
+            L.dmx_mask_exceptions(self.nmask.ctypes.data, self.n_words, idx.ctypes.data,
+                                  val.ctypes.data, n)
+            self._exc = (idx[:n], val[:n])
+        return self._exc
 
     @property
     def n_words(self) -> int:
@@ -222,6 +240,17 @@ class Context:
         self._check(self._L.dmx_run(self._h, p.seq2b.ctypes.data, p.nmask.ctypes.data,
                                     p.offsets.ctypes.data, p.lengths.ctypes.data, p.n_words,
                                     p.n_reads, out.ctypes.data), "dmx_run")
+        self._n_loaded = p.n_reads
+        return out
+
+    def run_sparse(self, p: Packed) -> np.ndarray:
+        """dmx_run with the no-match mask uploaded as its exceptions (dmx_run_sparse)."""
+        idx, val = p.exceptions()
+        out = np.zeros(p.n_reads, dtype=RESULT_DTYPE)
+        self._check(self._L.dmx_run_sparse(self._h, p.seq2b.ctypes.data, idx.ctypes.data,
+                                           val.ctypes.data, len(idx), p.offsets.ctypes.data,
+                                           p.lengths.ctypes.data, p.n_words, p.n_reads,
+                                           out.ctypes.data), "dmx_run_sparse")
         self._n_loaded = p.n_reads
         return out
 
@@ -371,6 +400,22 @@ class Context:
                 "traces": cl[6:8].tolist(), "windows_raw": cl[8:10].tolist(),
                 "tasks": cl[10:12].tolist(),
                 "flags": fl.value}
+
+
+def host_register(arrays) -> list:
+    """Page-lock the given numpy arrays (upload sources); returns the registered ones."""
+    L = load()
+    done = []
+    for a in arrays:
+        if a.nbytes and L.dmx_host_register(a.ctypes.data, a.nbytes) == 0:
+            done.append(a)
+    return done
+
+
+def host_unregister(arrays):
+    L = load()
+    for a in arrays:
+        L.dmx_host_unregister(a.ctypes.data)
 
 
 def device_count() -> int:

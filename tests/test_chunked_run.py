@@ -129,3 +129,27 @@ def test_unaligned_batch_runs_one_shot(c2x24, monkeypatch):
         _setup(ctx, d)
         exp = ctx.run(q)
     assert got.tobytes() == exp.tobytes()
+
+
+@pytest.mark.parametrize("chunk", [0, 4096])
+def test_sparse_mask_run_matches_dense(c2x24, chunk, monkeypatch):
+    """dmx_run_sparse (the no-match mask as its nonzero words, scattered on the device) equals
+    dmx_run with the dense mask, one-shot and chunked, with N-heavy reads mixed in."""
+    d, _ = c2x24
+    blob = d["blob"].copy()
+    rng = np.random.default_rng(4)
+    blob[rng.random(len(blob)) < 0.003] = ord("N")
+    p = lib.pack(blob, d["offsets"], d["lengths"])
+    monkeypatch.setenv("DMX_RUN_CHUNK", str(chunk))
+    with lib.Context(0) as ctx:
+        _setup(ctx, d)
+        dense = ctx.run(p)
+        pinned = lib.host_register([p.seq2b, p.offsets, p.lengths] + list(p.exceptions()))
+        try:
+            sparse = ctx.run_sparse(p)
+            c_sparse = ctx.counts()
+        finally:
+            lib.host_unregister(pinned)
+        again = ctx.run(p)
+    assert sparse.tobytes() == dense.tobytes() == again.tobytes()
+    assert c_sparse.sum() > 0

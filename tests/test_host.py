@@ -152,3 +152,21 @@ def test_loop_composite_coordinates_match_two_calls():
         full = fastx.revcomp(s.encode()) if o2[i] else s.encode()
         assert full[s2[i]:e2[i]] == t2
         assert nrc[i] == res["rc1"][i] + res["rc2"][i]
+
+
+def test_mask_exceptions_match_dense_mask():
+    """dmx_mask_exceptions lists exactly the nonzero no-match words, in order (the sparse upload
+    of dmx_run_sparse); single- and multi-threaded ranges."""
+    for n, nfrac in ((300, 0.01), (40000, 0.002)):
+        d = synth.generate("c2", n=n, seed=7)
+        blob = d["blob"].copy()
+        rng = np.random.default_rng(n)
+        hit = rng.random(len(blob)) < nfrac
+        blob[hit] = ord("N")
+        p = lib.pack(blob, d["offsets"], d["lengths"])
+        idx, val = p.exceptions()
+        nmw = min(p.n_words, (p.n_words + 1) // 2 + 2)
+        nz = np.nonzero(p.nmask[:nmw])[0]
+        assert idx.tolist() == nz.tolist()
+        assert val.tolist() == p.nmask[nz].tolist()
+        assert len(idx) > 0

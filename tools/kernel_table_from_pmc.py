@@ -20,16 +20,21 @@ import json
 import os
 import sys
 
-KERNELS = ("filter_kernel", "verify_kernel", "iscreen_kernel", "iscreen4_kernel", "wscan_kernel<true>",
-           "band_cand_kernel<7>", "band_cand_kernel<11>", "band_cand_kernel<15>", "select_cand_kernel",
-           "finalize0_kernel", "finalize1_kernel", "chop_kernel")
+KERNELS = ("filter_kernel", "verify_kernel", "iscreen_kernel", "iscreen4_kernel",
+           "wscan_kernel<true>", "band_cand_kernel<0, 3>", "band_cand_kernel<4, 5>",
+           "band_cand_kernel<4, 7>", "select_cand_kernel", "finalize0_kernel", "finalize1_kernel",
+           "chop_kernel", "scan_kernel<true>", "finalize0_linked_kernel",
+           "finalize1_linked_kernel", "finalize2_linked_kernel")
+# VALU lane-ops per shader cycle of the whole chip: 256 CUs x 4 SIMD x 32 lanes
+VALU_LANES_PER_CLK = 256 * 4 * 32
 
 
 def dispatches(d):
     acc = collections.OrderedDict()
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
         name = r["Kernel_Name"]
-        k = next((k for k in KERNELS if k in name), None)
+        k = next((k for k in KERNELS if "::" + k + "(" in name or " " + k + "(" in name
+                  or name.startswith(k + "(")), None)
         if k is None:
             continue
         ent = acc.setdefault(int(r["Dispatch_Id"]), {"kernel": k, "ms": (
@@ -56,6 +61,12 @@ def main():
             "lds_insts": c["SQ_INSTS_LDS"],
             "lds_conflict_cycles_per_inst": c["SQ_LDS_BANK_CONFLICT"] / max(1.0, c["SQ_INSTS_LDS"]),
         })
+        if "GRBM_GUI_ACTIVE" in c:   # effective clock of this launch (pass 3's own duration)
+            clk = c["GRBM_GUI_ACTIVE"] / 8.0 / (c["ms"] / 1e3)
+            rate = valu * 64 / (c["ms"] / 1e3)
+            ent[-1].update({"clock_ghz": clk / 1e9,
+                            "valu_peak_at_clock": VALU_LANES_PER_CLK * clk,
+                            "valu_frac_of_peak_at_clock": rate / (VALU_LANES_PER_CLK * clk)})
     data = {}
     if os.path.exists(out):
         data = json.load(open(out))
@@ -70,7 +81,9 @@ def main():
     for k, v in table.items():
         print(k, [(e["ms"], f"{e['valu_lane_ops_per_s'] / 1e12:.1f}T",
                    f"{e['hbm_bytes'] / 1e9:.2f}GB", f"wait {e['wait_frac']:.2f}",
-                   f"lds {e['lds_conflict_cycles_per_inst']:.2f}") for e in v])
+                   f"lds {e['lds_conflict_cycles_per_inst']:.2f}",
+                   f"clk {e.get('clock_ghz', 0):.2f}GHz",
+                   f"valu@clk {e.get('valu_frac_of_peak_at_clock', 0):.2f}") for e in v])
 
 
 if __name__ == "__main__":

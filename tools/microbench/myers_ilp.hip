@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <algorithm>
+#include <vector>
 #include "../../nanopore-barcoding-orc_amd/csrc/dmx_device.h"
 using namespace dmx;
 
@@ -66,10 +68,78 @@ __global__ __launch_bounds__(256) void addloop(uint32_t* out, int steps) {
     out[blockIdx.x * 256 + threadIdx.x] = a + b + c + d;
 }
 
+// The same chains with the shader clock stamped around the loop by the first lane of every block
+// (MI355X_MICROARCH.md 'DVFS give-back' item 6: clock = d(s_memtime) / d(s_memrealtime) x 100 MHz).
+// The stamps go to their own buffer; nothing else reads them.
+__global__ __launch_bounds__(256) void addloop_stamped(uint32_t* out, int steps,
+                                                       unsigned long long* stamps) {
+    uint32_t a = threadIdx.x, b = blockIdx.x, c = a ^ b, d = a + b;
+    unsigned long long t0 = 0, r0 = 0;
+    if (threadIdx.x == 0) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    for (int s = 0; s < steps; ++s) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            a = __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+            b = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96);
+            c = __builtin_amdgcn_bitop3_b32(c, d, a, 0x96);
+            d = __builtin_amdgcn_bitop3_b32(d, a, b, 0x96);
+        }
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = a + b + c + d;
+    if (threadIdx.x == 0) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+        stamps[2 * blockIdx.x] = t1 - t0;
+        stamps[2 * blockIdx.x + 1] = r1 - r0;
+    }
+}
+
 int main() {
     uint32_t* d_out;
     hipMalloc(&d_out, 256u * 65536 * 4);
     const int steps = 2048, blocks = 8192;
+    {   // clock under load: >= 2 s of back-to-back launches, then one stamped launch
+        unsigned long long* d_st;
+        hipMalloc(&d_st, 2ull * blocks * 8);
+        hipEvent_t a, b, w0, w1;
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+        hipEventCreate(&w0);
+        hipEventCreate(&w1);
+        float warm = 0.f;
+        int launches = 0;
+        hipEventRecord(w0);
+        while (warm < 2000.f) {
+            for (int i = 0; i < 8; ++i)
+                hipLaunchKernelGGL(addloop, dim3(blocks), dim3(256), 0, 0, d_out, 512);
+            launches += 8;
+            hipEventRecord(w1);
+            hipEventSynchronize(w1);
+            hipEventElapsedTime(&warm, w0, w1);
+        }
+        hipEventRecord(a);
+        hipLaunchKernelGGL(addloop_stamped, dim3(blocks), dim3(256), 0, 0, d_out, 512, d_st);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        std::vector<unsigned long long> st(2ull * blocks);
+        hipMemcpy(st.data(), d_st, st.size() * 8, hipMemcpyDeviceToHost);
+        std::vector<double> mhz;
+        for (int i = 0; i < blocks; ++i)
+            if (st[2 * i + 1]) mhz.push_back((double)st[2 * i] / (double)st[2 * i + 1] * 100.0);
+        std::sort(mhz.begin(), mhz.end());
+        const double med = mhz.empty() ? 0.0 : mhz[mhz.size() / 2];
+        const double ops = (double)blocks * 256 * 512 * 64;
+        printf("stamped bitop3 chain x4 after %.0f ms / %d launches: %.3f ms  %.2f T lane-ops/s  "
+               "clock %.0f MHz (median of %zu blocks, p10 %.0f p90 %.0f)\n", warm, launches, ms,
+               ops / ms / 1e9, med, mhz.size(), mhz.empty() ? 0.0 : mhz[mhz.size() / 10],
+               mhz.empty() ? 0.0 : mhz[mhz.size() * 9 / 10]);
+        hipFree(d_st);
+    }
     {
         hipEvent_t a, b;
         hipEventCreate(&a);

@@ -66,7 +66,7 @@ def random_panel(rng):
         L = int(rng.integers(lo, hi + 1))
         s = rand_seq(rng, L)
         if shared:
-            s = (pre + rand_seq(rng, int(rng.integers(3, 18))) + suf)[:64]
+            s = (pre + rand_seq(rng, int(rng.integers(3, 29))) + suf)[:64]
         s = "".join(c if rng.random() >= wild else str(rng.choice(list("NRYSWKMBDHV"))) for c in s)
         out.append(s)
     return out
