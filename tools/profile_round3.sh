@@ -28,7 +28,7 @@ run_pmc() {   # workload reads dominant-kernel
 }
 run_pmc c2x24 10000000 filter_kernel
 run_pmc c4 6250000 filter_kernel
-run_pmc c5 10000000 "scan_kernel<true>"
+run_pmc c5 10000000 "scan_kernel<true>@0"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o run \
   -- python3 bench.py --no-cpu-baseline --no-pcie > "$out/stats.log" 2>&1
 cp "$out/stats/run_kernel_stats.csv" "$out/kernel_stats_c2x24_10M.csv"

@@ -5,11 +5,12 @@ WRITE_SIZE collected in separate runs of `bench.py --steps 1 --warmup 0`).
 Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE
 are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced read, so it
 is doubled (the filter's loads are 16-B and 8-B per lane); WRITE_SIZE is taken as reported.
-usage: traffic_from_pmc.py FETCH_DIR WRITE_DIR WORKLOAD READS OUT_JSON [KERNEL]
+usage: traffic_from_pmc.py FETCH_DIR WRITE_DIR WORKLOAD READS OUT_JSON [KERNEL[@LAUNCH]]
 
 KERNEL defaults to filter_kernel (every launch of one step is averaged).  For chop_kernel the run
 also holds the small autotune launches, so only the largest launch (the timed 10M-read pass) is
-kept; the same launch index is read from the WRITE_SIZE pass.
+kept; the same launch index is read from the WRITE_SIZE pass.  KERNEL@N keeps launch N of the
+step (scan_kernel<true>@0: config 5's round-1 front scan, the bench line's dominant kernel).
 """
 import collections
 import csv
@@ -31,9 +32,15 @@ def per_dispatch(d, counter, kernel="filter_kernel"):
 def main():
     fdir, wdir, workload, reads, out = sys.argv[1:6]
     kernel = sys.argv[6] if len(sys.argv) > 6 else "filter_kernel"
+    launch = None
+    if "@" in kernel:
+        kernel, launch = kernel.split("@")
+        launch = int(launch)
     fetch = per_dispatch(fdir, "FETCH_SIZE", kernel)
     write = per_dispatch(wdir, "WRITE_SIZE", kernel)
-    if kernel != "filter_kernel":
+    if launch is not None:
+        fetch, write = [fetch[launch]], [write[launch]]
+    elif kernel != "filter_kernel":
         i = max(range(len(fetch)), key=fetch.__getitem__)
         fetch, write = [fetch[i]], [write[i]]
     n = min(len(fetch), len(write))
@@ -48,8 +55,9 @@ def main():
         "source": ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), filter_kernel, "
                    "FETCH_SIZE x2 (gfx950 wide-read correction), averaged over the round-1 and "
                    "round-2 launches of one step") if kernel == "filter_kernel" else
-                  (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), {kernel}, the "
-                   "timed launch; FETCH_SIZE x2 (gfx950 wide-read correction, uncalibrated for "
+                  (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), {kernel}, "
+                   + (f"launch {launch} of one step" if launch is not None else "the timed launch")
+                   + "; FETCH_SIZE x2 (gfx950 wide-read correction, uncalibrated for "
                    "this kernel's 4-B loads, so an upper bound on reads)"),
     }
     with open(out, "w") as fh:
