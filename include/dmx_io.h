@@ -97,6 +97,18 @@ int dmx_batch_mean_qual(const dmx_batch* b, double* out);
 /* Free a sink after dmx_sink_close (or to abandon it). */
 void dmx_sink_free(dmx_sink* s);
 
+/* Round-2 cache of the unchanged 02_cutadapt_loop.sh (a resident process runs its 13 calls):
+ * keep the uncompressed text of this sink's gzip outputs in memory (the rendered buffers, not a
+ * copy) up to max_bytes retained in the process; call before the first write.  At
+ * dmx_sink_close each output is registered under its real path, inode, size, mtime and the
+ * CRC-32 of its first 64 KiB; dmx_reader_open of that file, unchanged on disk, then reads the
+ * text from memory (no read, no inflate) and drops it.  Replaces: re-reading and inflating each
+ * SP5 bin in the round-2 calls (scripts/02_cutadapt_loop.sh:91-103). */
+int dmx_sink_retain(dmx_sink* s, uint64_t max_bytes);
+/* Bytes of retained output text held in this process; drop all of it. */
+uint64_t dmx_io_retained_bytes(void);
+void dmx_io_drop_retained(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -417,7 +417,9 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
             ++l;
         common = l;
     }
-    const int flen = std::min(common, 32);
+    int flen = std::min(common, 32);
+    if (const char* fm = std::getenv("DMX_FILTER_MAXLEN"))   // A/B: a shorter suffix block
+        flen = std::min(flen, std::max(1, std::atoi(fm)));
     bool uniform = true;
     for (int a = 1; a < n; ++a) uniform &= hp.ad[a].where == hp.ad[0].where;
     int kf_all = -1;

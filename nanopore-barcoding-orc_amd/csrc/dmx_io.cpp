@@ -16,11 +16,13 @@
 #include "../../include/dmx_io.h"
 
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <atomic>
@@ -29,6 +31,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -221,6 +224,122 @@ struct PrefixSource : Source {
         }
         return (long)got;
     }
+};
+
+// ------------------------------------------------------------------------------------------
+// Retained outputs (the round-2 cache of the unchanged 02_cutadapt_loop.sh).
+// A sink opened with dmx_sink_retain keeps the uncompressed text it rendered for each gzip output
+// (the buffers it compressed: moved, never copied).  At close the file's identity is recorded —
+// real path, inode, size, mtime (ns) and the CRC-32 of its first 64 KiB as written — and a later
+// dmx_reader_open of the same file, unchanged on disk, reads the text from memory instead of
+// reading and inflating the file (then drops it: each bin is read once by the script).  Any
+// mismatch reads the file.  Bounded by the caps the sinks were opened with.
+struct Retained {
+    std::vector<Bytes> pieces;
+    uint64_t bytes = 0;
+    dev_t dev = 0;
+    ino_t ino = 0;
+    off_t size = 0;
+    int64_t mtime_ns = 0;
+    uint32_t head_crc = 0;
+};
+std::mutex g_ret_mu;
+std::map<std::string, Retained> g_retained;
+uint64_t g_ret_bytes = 0;
+
+int64_t mtime_ns(const struct stat& st) {
+    return (int64_t)st.st_mtim.tv_sec * 1000000000ll + st.st_mtim.tv_nsec;
+}
+
+// CRC-32 of the first min(64 KiB, size) bytes of the file; false if unreadable
+bool head_crc(const char* path, uint32_t& crc) {
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) return false;
+    uint8_t buf[65536];
+    size_t got = 0;
+    while (got < sizeof(buf)) {
+        const ssize_t n = ::read(fd, buf + got, sizeof(buf) - got);
+        if (n < 0 && errno == EINTR) continue;
+        if (n <= 0) break;
+        got += (size_t)n;
+    }
+    ::close(fd);
+    crc = libdeflate_crc32(0u, buf, got);
+    return true;
+}
+
+std::string real_path(const char* p) {
+    char rp[PATH_MAX];
+    return realpath(p, rp) ? std::string(rp) : std::string();
+}
+
+// The retained text of `path` if the file on disk is the one that was written (moved out of
+// the registry), else false.
+bool take_retained(const char* path, Retained& out) {
+    const std::string rp = real_path(path);
+    if (rp.empty()) return false;
+    struct stat st;
+    if (::stat(rp.c_str(), &st) != 0) return false;
+    Retained r;
+    {
+        std::lock_guard<std::mutex> g(g_ret_mu);
+        auto it = g_retained.find(rp);
+        if (it == g_retained.end()) return false;
+        r = std::move(it->second);
+        g_ret_bytes -= r.bytes;
+        g_retained.erase(it);
+    }
+    uint32_t crc = 0;
+    if (r.dev != st.st_dev || r.ino != st.st_ino || r.size != st.st_size ||
+        r.mtime_ns != mtime_ns(st) || !head_crc(rp.c_str(), crc) || crc != r.head_crc)
+        return false;
+    out = std::move(r);
+    return true;
+}
+
+// The retained text as a source: pieces copied out in order (large reads in parallel).
+struct MemSource : Source {
+    std::vector<Bytes> pieces;
+    size_t pi = 0, off = 0;
+    int threads = 1;
+    long read(uint8_t* dst, size_t cap) override {
+        // the copies of this read: (piece, offset, length, destination)
+        struct Cp {
+            const uint8_t* s;
+            uint8_t* d;
+            size_t n;
+        };
+        std::vector<Cp> cps;
+        size_t got = 0;
+        const size_t pi0 = pi;
+        while (got < cap && pi < pieces.size()) {
+            const size_t n = std::min(cap - got, pieces[pi].size() - off);
+            cps.push_back({pieces[pi].data() + off, dst + got, n});
+            got += n;
+            off += n;
+            if (off == pieces[pi].size()) {
+                ++pi;
+                off = 0;
+            }
+        }
+        if (got >= (8u << 20) && threads > 1) {
+            // split into ~1 MiB copies over the pool
+            std::vector<Cp> parts;
+            for (const Cp& c : cps)
+                for (size_t a = 0; a < c.n; a += (1u << 20))
+                    parts.push_back({c.s + a, c.d + a, std::min<size_t>(1u << 20, c.n - a)});
+            std::atomic<size_t> next{0};
+            parallel(threads, [&](int) {
+                for (size_t k; (k = next.fetch_add(1)) < parts.size();)
+                    memcpy(parts[k].d, parts[k].s, parts[k].n);
+            });
+        } else {
+            for (const Cp& c : cps) memcpy(c.d, c.s, c.n);
+        }
+        for (size_t k = pi0; k < pi; ++k) Bytes().swap(pieces[k]);   // consumed: memory back
+        return (long)got;
+    }
+    size_t chunk_hint() const override { return 64u << 20; }
 };
 
 // zlib inflate of a gzip file; concatenated members (pigz / bgzip / our own writer) are read
@@ -956,6 +1075,21 @@ int dmx_io_abi_version(void) { return DMX_IO_ABI_VERSION; }
 int dmx_reader_open(const char* path, size_t batch_bytes, int threads, dmx_reader** out) {
     if (!path || !out) return -1;
     *out = nullptr;
+    if (strcmp(path, "-")) {   // a file this process wrote with dmx_sink_retain, unchanged
+        Retained ret;
+        if (take_retained(path, ret)) {
+            auto* r = new dmx_reader();
+            auto m = std::make_unique<MemSource>();
+            m->pieces = std::move(ret.pieces);
+            m->threads = clamp_threads(threads);
+            r->src = std::move(m);
+            r->batch_bytes = std::max<size_t>(batch_bytes, 1u << 16);
+            r->threads = clamp_threads(threads);
+            r->th = std::thread([r] { r->produce(); });
+            *out = r;
+            return 0;
+        }
+    }
     auto fd = std::make_unique<FdSource>();
     if (!strcmp(path, "-")) {
         fd->fd = 0;
@@ -1051,6 +1185,9 @@ struct Out {
     bool gz = false;
     bool any = false;
     uint64_t n = 0, bp = 0;
+    std::vector<Bytes> kept;    // dmx_sink_retain: the rendered text, in output order
+    uint64_t kept_bytes = 0;
+    bool keep = false;          // still retaining (dropped when the cap would be exceeded)
 };
 
 struct Job {
@@ -1167,6 +1304,7 @@ extern "C" int dmx_io_gzip(const uint8_t* src, size_t n, int level, uint8_t* out
 
 struct dmx_sink {
     std::vector<Out> outs;
+    uint64_t retain_cap = 0;    // process-wide retained-bytes cap (0: no retention)
     bool fasta_out = false;
     int level = 1;
     int threads = 1;
@@ -1337,6 +1475,25 @@ bool dmx_sink::process(Job& j, std::string& e) {
             bool ok = true;
             if (f.gz) {
                 for (const Bytes& pm : part[t][o]) ok = ok && put(pm);
+                if (f.keep && !buf[t][o].empty()) {   // retain the text: move, not copy
+                    const uint64_t nb = buf[t][o].size();
+                    bool fits;
+                    {
+                        std::lock_guard<std::mutex> g(g_ret_mu);
+                        fits = g_ret_bytes + nb <= retain_cap;
+                        if (fits) g_ret_bytes += nb;
+                    }
+                    if (fits) {
+                        f.kept_bytes += nb;
+                        f.kept.push_back(std::move(buf[t][o]));
+                    } else {                          // over the cap: this output goes to disk
+                        std::lock_guard<std::mutex> g(g_ret_mu);
+                        g_ret_bytes -= f.kept_bytes;
+                        f.kept_bytes = 0;
+                        f.keep = false;
+                        std::vector<Bytes>().swap(f.kept);
+                    }
+                }
             } else {
                 ok = put(buf[t][o]);
             }
@@ -1516,11 +1673,39 @@ int dmx_sink_close(dmx_sink* s, uint64_t* n_written, uint64_t* bp_written) {
                 rc = -3;
             }
         }
-        if (f.fp == stdout ? fflush(f.fp) != 0 : fclose(f.fp) != 0) {
+        const bool is_std = f.fp == stdout;
+        if (is_std ? fflush(f.fp) != 0 : fclose(f.fp) != 0) {
             s->api_err = "close failed: " + f.path + ": " + strerror(errno);
             rc = -3;
         }
         f.fp = nullptr;
+        if (f.keep) {   // register the retained text under the file's identity as written
+            Retained r;
+            struct stat st;
+            const std::string rp = is_std ? std::string() : real_path(f.path.c_str());
+            if (rc == 0 && !rp.empty() && ::stat(rp.c_str(), &st) == 0 &&
+                head_crc(rp.c_str(), r.head_crc)) {
+                r.pieces = std::move(f.kept);
+                r.bytes = f.kept_bytes;
+                r.dev = st.st_dev;
+                r.ino = st.st_ino;
+                r.size = st.st_size;
+                r.mtime_ns = mtime_ns(st);
+                std::lock_guard<std::mutex> g(g_ret_mu);
+                auto it = g_retained.find(rp);
+                if (it != g_retained.end()) {   // an older retained copy of the same path
+                    g_ret_bytes -= it->second.bytes;
+                    g_retained.erase(it);
+                }
+                g_retained.emplace(rp, std::move(r));
+            } else {
+                std::lock_guard<std::mutex> g(g_ret_mu);
+                g_ret_bytes -= f.kept_bytes;
+            }
+            f.kept_bytes = 0;
+            f.keep = false;
+            std::vector<Bytes>().swap(f.kept);
+        }
         if (n_written) n_written[o] = f.n;
         if (bp_written) bp_written[o] = f.bp;
     }
@@ -1529,6 +1714,26 @@ int dmx_sink_close(dmx_sink* s, uint64_t* n_written, uint64_t* bp_written) {
 }
 
 const char* dmx_sink_error(dmx_sink* s) { return s ? s->api_err.c_str() : "null sink"; }
+
+int dmx_sink_retain(dmx_sink* s, uint64_t max_bytes) {
+    if (!s) return -1;
+    std::unique_lock<std::mutex> lk(s->mu);
+    s->cv.wait(lk, [&] { return !s->busy; });
+    s->retain_cap = max_bytes;
+    for (auto& f : s->outs) f.keep = max_bytes > 0 && f.gz && f.path != "-" && f.n == 0;
+    return 0;
+}
+
+uint64_t dmx_io_retained_bytes(void) {
+    std::lock_guard<std::mutex> g(g_ret_mu);
+    return g_ret_bytes;
+}
+
+void dmx_io_drop_retained(void) {
+    std::lock_guard<std::mutex> g(g_ret_mu);
+    for (const auto& kv : g_retained) g_ret_bytes -= kv.second.bytes;   // (open sinks' bytes
+    g_retained.clear();                                                 //  stay counted)
+}
 
 void dmx_sink_free(dmx_sink* s) {
     if (!s) return;

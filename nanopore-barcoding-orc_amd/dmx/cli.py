@@ -109,6 +109,7 @@ def close_cached_contexts():
         for c in ctxs:
             c.close()
     _CTX_CACHE.clear()
+    nio.drop_retained()
 
 
 def cached_group(devices) -> list:
@@ -179,7 +180,10 @@ def run(argv=None, keep_contexts: bool = False) -> int:
     t0 = time.perf_counter()
     a1 = len(ads) if linked else 0
     totals = np.zeros((len(ads) + 1, a1 + 1), dtype=np.int64)
-    sink = nio.Sink(paths, fasta_out, level, threads=args.cores)
+    # the resident server keeps gzip outputs' text for the script's next calls, which read the
+    # round-1 bins back (02_cutadapt_loop.sh:91-103): DMX_RETAIN_MB caps it (0 disables)
+    retain = (int(os.environ.get("DMX_RETAIN_MB", "8192")) << 20) if keep_contexts else 0
+    sink = nio.Sink(paths, fasta_out, level, threads=args.cores, retain_bytes=retain)
     _phase("sink", marks)
     tw = [0.0, 0.0, 0.0]   # read wait, GPU, plan + write enqueue
     try:

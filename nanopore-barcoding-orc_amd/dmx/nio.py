@@ -21,7 +21,8 @@ IO_PATH = os.path.join(os.environ.get("DMX_LIBDIR") or HERE, "libdmx_io.so")
 IO_EXPORTS = ["dmx_io_abi_version", "dmx_reader_open", "dmx_reader_next", "dmx_reader_error",
               "dmx_reader_close", "dmx_batch_free", "dmx_sink_open", "dmx_sink_write",
               "dmx_sink_close", "dmx_sink_error", "dmx_sink_free", "dmx_sink_write_rows",
-              "dmx_batch_mean_qual", "dmx_io_gzip"]
+              "dmx_batch_mean_qual", "dmx_io_gzip", "dmx_sink_retain", "dmx_io_retained_bytes",
+              "dmx_io_drop_retained"]
 
 
 class _CBatch(ctypes.Structure):
@@ -65,6 +66,9 @@ def load() -> ctypes.CDLL:
     L.dmx_sink_free.argtypes = [P]
     L.dmx_sink_free.restype = None
     L.dmx_io_gzip.argtypes = [ctypes.c_char_p, c_size, c_int, P, c_size, P]
+    L.dmx_sink_retain.argtypes = [P, ctypes.c_uint64]
+    L.dmx_io_retained_bytes.restype = ctypes.c_uint64
+    L.dmx_io_drop_retained.restype = None
     if L.dmx_io_abi_version() != 1:
         raise DmxError("libdmx_io ABI mismatch")
     _io = L
@@ -183,10 +187,22 @@ class Reader:
         self.close()
 
 
+def retained_bytes() -> int:
+    """Output text held for later readers (dmx_sink_retain)."""
+    return int(load().dmx_io_retained_bytes())
+
+
+def drop_retained():
+    load().dmx_io_drop_retained()
+
+
 class Sink:
     """Outputs (created now) receiving records in input order; '.gz' paths are gzip members."""
 
-    def __init__(self, paths, fasta_out: bool, level: int = 1, threads: int = 0):
+    def __init__(self, paths, fasta_out: bool, level: int = 1, threads: int = 0,
+                 retain_bytes: int = 0):
+        """retain_bytes > 0: keep the gzip outputs' text in memory (up to that many bytes held
+        in the process) for a later Reader of the same, unchanged files (dmx_sink_retain)."""
         self._L = load()
         self.paths = list(paths)
         arr = (ctypes.c_char_p * len(self.paths))(*[p.encode() for p in self.paths])
@@ -200,6 +216,8 @@ class Sink:
             self._h = None
             raise OSError(msg)
         self.n_written = self.bp_written = None
+        if retain_bytes > 0:
+            self._L.dmx_sink_retain(self._h, int(retain_bytes))
 
     def write(self, batch: NativeBatch, out_idx, start, stop, rc, n_rc):
         n = len(batch)

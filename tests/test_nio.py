@@ -3,6 +3,7 @@
 The Python reader/renderer in dmx/fastx.py restates dnaio/xopen's conventions in a few lines and
 serves as the checker here; the CLI itself uses the native path."""
 import gzip
+import os
 import re
 import subprocess
 import zlib
@@ -30,7 +31,8 @@ def _records(n, seed=0, crlf=False):
 
 def test_io_library_exports_every_declared_symbol():
     hdr = open(f"{ROOT}/include/dmx_io.h").read()
-    declared = set(re.findall(r"^\s*(?:int|void|const char\*)\s+(dmx_\w+)\(", hdr, re.M))
+    declared = set(re.findall(r"^\s*(?:int|void|const char\*|uint64_t)\s+(dmx_\w+)\(", hdr,
+                              re.M))
     assert declared == set(nio.IO_EXPORTS)
     out = subprocess.run(["nm", "-D", "--defined-only", nio.IO_PATH], capture_output=True,
                          text=True, check=True).stdout
@@ -250,3 +252,54 @@ def test_huffman_gzip_members_inflate_with_zlib():
     fq = b"".join(b"@r%d\n%s\n+\n%s\n" % (i, b"ACGT" * (i % 50 + 1), b"I" * (4 * (i % 50 + 1)))
                   for i in range(20000))
     assert len(nio.gzip_member(fq, 1)) < 0.45 * len(fq)
+
+
+def test_retained_outputs_read_back_without_the_file(tmp_path):
+    """dmx_sink_retain (the resident server's round-2 cache, 02_cutadapt_loop.sh:91-103): a
+    reader of an unchanged retained .gz output gets the same records from memory; a changed
+    file (or a second read) goes to disk; the cap is honoured."""
+    recs, text = _records(3000, seed=5)
+    src = tmp_path / "in.fastq"
+    src.write_text(text)
+    outs = [str(tmp_path / f"bin{i}.fastq.gz") for i in range(3)]
+    nio.drop_retained()
+    base = nio.retained_bytes()
+
+    def write_bins(retain):
+        with nio.Reader(str(src), 64 << 10, threads=4) as r:
+            s = nio.Sink(outs, False, 1, threads=4, retain_bytes=retain)
+            for b in r:
+                k = len(b)
+                idx = (np.arange(k) % 3).astype(np.int32)
+                s.write(b, idx, np.zeros(k, np.int32), b.lens.astype(np.int32),
+                        (np.arange(k) % 2).astype(np.uint8), np.zeros(k, np.uint8))
+                b.free()
+            s.close()
+
+    def read_all(path):
+        got = []
+        with nio.Reader(path, 64 << 10, threads=4) as r:
+            for b in r:
+                got += [(b.header(i), b.sequence(i), b.quality(i)) for i in range(len(b))]
+                b.free()
+        return got
+
+    write_bins(0)
+    ref = [read_all(p) for p in outs]       # from disk
+    assert nio.retained_bytes() == base
+    write_bins(1 << 30)
+    held = nio.retained_bytes()
+    assert held > 0
+    assert read_all(outs[0]) == ref[0]      # from memory
+    assert nio.retained_bytes() < held
+    assert read_all(outs[0]) == ref[0]      # again: from disk
+    os.utime(outs[1], ns=(1, 1))            # a changed file is read from disk
+    assert read_all(outs[1]) == ref[1]
+    assert read_all(outs[2]) == ref[2]
+    assert nio.retained_bytes() == base
+    write_bins(1000)                        # over the cap: nothing retained
+    assert nio.retained_bytes() == base
+    assert [read_all(p) for p in outs] == ref
+    write_bins(1 << 30)
+    nio.drop_retained()
+    assert nio.retained_bytes() == base
