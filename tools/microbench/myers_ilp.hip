@@ -68,6 +68,25 @@ __global__ __launch_bounds__(256) void addloop(uint32_t* out, int steps) {
     out[blockIdx.x * 256 + threadIdx.x] = a + b + c + d;
 }
 
+// Eight independent v_bitop3 chains per lane (each op depends only on its own chain): the VALU
+// issue rate without dependency stalls, i.e. the practical peak at 8 waves per SIMD.
+__global__ __launch_bounds__(256) void indep8(uint32_t* out, int steps) {
+    uint32_t v[8];
+    const uint32_t k1 = threadIdx.x * 0x9E3779B9u, k2 = blockIdx.x ^ 0x85EBCA6Bu;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = threadIdx.x + c;
+    for (int s = 0; s < steps; ++s) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) v[c] = __builtin_amdgcn_bitop3_b32(v[c], k1, k2, 0x96);
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc += v[c];
+    out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
 // The same chains with the shader clock stamped around the loop by the first lane of every block
 // (MI355X_MICROARCH.md 'DVFS give-back' item 6: clock = d(s_memtime) / d(s_memrealtime) x 100 MHz).
 // The stamps go to their own buffer; nothing else reads them.
@@ -139,6 +158,20 @@ int main() {
                ops / ms / 1e9, med, mhz.size(), mhz.empty() ? 0.0 : mhz[mhz.size() / 10],
                mhz.empty() ? 0.0 : mhz[mhz.size() * 9 / 10]);
         hipFree(d_st);
+    }
+    {   // independent chains
+        hipEvent_t a, b;
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+        hipLaunchKernelGGL(indep8, dim3(blocks), dim3(256), 0, 0, d_out, 2048);
+        hipEventRecord(a);
+        hipLaunchKernelGGL(indep8, dim3(blocks), dim3(256), 0, 0, d_out, 2048);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        const double ops = (double)blocks * 256 * 2048 * 64;
+        printf("bitop3 independent x8: %.3f ms  %.2f T lane-ops/s\n", ms, ops / ms / 1e9);
     }
     {
         hipEvent_t a, b;

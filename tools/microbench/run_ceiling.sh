@@ -14,6 +14,7 @@ import json, re, sys
 res = """$res"""
 lines = [l for l in res.splitlines() if l.strip()]
 m = re.search(r"\nbitop3 chain x4: ([0-9.]+) ms\s+([0-9.]+) T lane-ops/s", "\n" + res)
+mi = re.search(r"bitop3 independent x8: ([0-9.]+) ms\s+([0-9.]+) T lane-ops/s", res)
 ms_ = re.search(r"stamped bitop3 chain x4 after ([0-9.]+) ms / (\d+) launches: ([0-9.]+) ms\s+"
                 r"([0-9.]+) T lane-ops/s\s+clock ([0-9.]+) MHz \(median of (\d+) blocks, p10 "
                 r"([0-9.]+) p90 ([0-9.]+)\)", res)
@@ -23,6 +24,8 @@ out = {"what": "VALU issue ceiling, gfx950 (MI355X): v_bitop3 dependency chains 
                "8192 x 256 threads; 64-bit Myers step (myers_step_hw) by chains per lane and waves "
                "per SIMD", "source": "tools/microbench/myers_ilp.hip",
        "bitop3_t_lane_ops_per_s": float(m.group(2)) if m else None,
+       "bitop3_dependent_chain_t_lane_ops_per_s": float(m.group(2)) if m else None,
+       "bitop3_independent_t_lane_ops_per_s": float(mi.group(2)) if mi else None,
        "nominal_t_lane_ops_per_s": 256 * 4 * 32 * 2.4e9 / 1e12,
        "stamped": (dict(warm_ms=float(ms_.group(1)), warm_launches=int(ms_.group(2)),
                         ms=float(ms_.group(3)), t_lane_ops_per_s=float(ms_.group(4)),
