@@ -567,9 +567,10 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        ctx.exec()
+    for _ in range(args.warmup):   # the whole step body, read-backs included (their first
+        ctx.exec()                  # calls set up host staging: ~9 ms once on c5)
         ctx.sync()
+        ctx.stats()
         allreduce_counts()
 
     stage = {k: 0.0 for k in ("scan0", "resolve0", "finalize0", "scan1", "resolve1",
@@ -584,7 +585,9 @@ def main():
     t = time.perf_counter()
     counts = None
     flags = 0
+    step_wall = []
     for _ in range(args.steps):
+        ts = time.perf_counter()
         ctx.exec()
         ctx.sync()
         st = ctx.stats()
@@ -597,6 +600,7 @@ def main():
         traces += np.array(st["traces"], dtype=np.float64)
         flags |= st["flags"]
         counts = allreduce_counts()
+        step_wall.append((time.perf_counter() - ts) * 1e3)
     barrier_sync()
     elapsed = time.perf_counter() - t
     if flags:
@@ -614,6 +618,7 @@ def main():
     else:
         out = two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s,
                              clusters, windows, windows_raw, resolved, traces)
+    out["step_wall_ms"] = [round(x, 3) for x in step_wall]   # this rank's, for outliers
     pcie = None
     if host_batch is not None and not args.no_pcie:
         # the boundary's host-memory path: upload, both rounds, download of every result, with

@@ -157,6 +157,27 @@ int main() {
                "clock %.0f MHz (median of %zu blocks, p10 %.0f p90 %.0f)\n", warm, launches, ms,
                ops / ms / 1e9, med, mhz.size(), mhz.empty() ? 0.0 : mhz[mhz.size() / 10],
                mhz.empty() ? 0.0 : mhz[mhz.size() * 9 / 10]);
+        // the same work unstamped, straight after (the stamps' branch and stores aside, the
+        // two launches differ only in when they run)
+        hipEventRecord(a);
+        hipLaunchKernelGGL(addloop, dim3(blocks), dim3(256), 0, 0, d_out, 512);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        hipEventElapsedTime(&ms, a, b);
+        printf("unstamped bitop3 chain x4 right after: %.3f ms  %.2f T lane-ops/s\n", ms,
+               ops / ms / 1e9);
+        hipEventRecord(a);
+        hipLaunchKernelGGL(addloop_stamped, dim3(blocks), dim3(256), 0, 0, d_out, 512, d_st);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        hipEventElapsedTime(&ms, a, b);
+        hipMemcpy(st.data(), d_st, st.size() * 8, hipMemcpyDeviceToHost);
+        mhz.clear();
+        for (int i = 0; i < blocks; ++i)
+            if (st[2 * i + 1]) mhz.push_back((double)st[2 * i] / (double)st[2 * i + 1] * 100.0);
+        std::sort(mhz.begin(), mhz.end());
+        printf("stamped again: %.3f ms  %.2f T lane-ops/s  clock %.0f MHz\n", ms, ops / ms / 1e9,
+               mhz.empty() ? 0.0 : mhz[mhz.size() / 2]);
         hipFree(d_st);
     }
     {   // independent chains

@@ -5,7 +5,7 @@
 set -e -o pipefail
 here=$(dirname "$0")
 out=$1
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o /tmp/myers_ilp "$here/myers_ilp.hip"
+/opt/rocm/bin/hipcc -Wno-unused-value -O3 -std=c++17 --offload-arch=gfx950 -o /tmp/myers_ilp "$here/myers_ilp.hip"
 clk0=$(timeout -k 5 30 rocm-smi --showclocks 2>/dev/null | grep -i "sclk" | head -2 | tr '\n' ' ' || true)
 res=$(timeout -k 10 120 /tmp/myers_ilp)
 clk1=$(timeout -k 5 30 rocm-smi --showclocks 2>/dev/null | grep -i "sclk" | head -2 | tr '\n' ' ' || true)
