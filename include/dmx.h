@@ -227,10 +227,12 @@ int dmx_locate(dmx_ctx* ctx, const char* const* patterns, const int* plens, int 
  * least infix edit distance over the read, best, is <= k, every read column whose least
  * distance equals best is a hit (stop), with the start of the longest optimal alignment
  * ending there (edlib's reverse SHW alignment, last position).
- * Segments: a read's hits sorted by (start, stop, label) are paired greedily left to right;
- * consecutive hits (a, b) with a rule (rule_left[r], rule_right[r]) form a segment on strand
- * rule_strand[r] (0 '+', 1 '-'; the first rule of a pair wins) spanning [a.start, b.stop) with
- * keep_primers (pychopper -p), else [a.stop, b.start) (empty if the hits overlap). */
+ * Segments: in a read's hits sorted by (start, stop, label), consecutive hits (a, b) with a
+ * rule (rule_left[r], rule_right[r]) are a candidate segment on strand rule_strand[r] (0 '+',
+ * 1 '-'; the first rule of a pair wins) spanning [a.start, b.stop) with keep_primers
+ * (pychopper -p), else [a.stop, b.start) (empty if the hits overlap).  The read's segments are
+ * the best path over its candidates: no two share a hit, greatest summed length (pychopper's
+ * usable length), ties -> the earlier candidate. */
 #define DMX_CHOP_MAX_PRIMERS 8
 #define DMX_CHOP_MAX_RULES 32
 typedef struct dmx_chop_hit {

@@ -438,13 +438,17 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
                 !(c->no_filter);
     if (hp.filter) {
         dp.filter_len = flen;
-        // the block's rows in the top flen bits (last row = bit 31); the rows below match
+        int slen = flen;
+        if (const char* fs = std::getenv("DMX_FILTER_SCANLEN"))   // A/B: scan a shorter suffix
+            slen = std::min(flen, std::max(kMinFilterLen, std::atoi(fs)));
+        dp.scan_len = slen;
+        // the scanned rows in the top slen bits (last row = bit 31); the rows below match
         // every code, N included, so they stay at cost 0 like row 0 (filter_kernel)
-        const int pad = 32 - flen;
+        const int pad = 32 - slen;
         for (int code = 0; code < 8; ++code)
             dp.filter_peq[code] = pad > 0 ? (1u << pad) - 1u : 0u;
-        const char* blk = seqs[0] + lens[0] - flen;
-        for (int i = 0; i < flen; ++i) {
+        const char* blk = seqs[0] + lens[0] - slen;
+        for (int i = 0; i < slen; ++i) {
             const uint8_t mask = iupac_mask(blk[i]);
             for (int code = 0; code < 4; ++code)
                 if (mask & (1u << code)) dp.filter_peq[code] |= 1u << (pad + i);

@@ -15,11 +15,12 @@
 //             best <= k every column with D(j) == best is a hit (edlib's end locations) whose
 //             start is that of the LONGEST optimal alignment ending there (edlib's reverse SHW
 //             alignment, last position);
-//   segments  the read's hits sorted by (start, stop, label) are paired greedily left to right:
-//             consecutive hits (a, b) whose labels form a configuration rule (-c, e.g.
-//             "+:SP5,-SP27|-:SP27,-SP5") delimit one segment on the rule's strand and are both
-//             consumed; otherwise a is skipped.  Span [a.start, b.stop) with -p (keep primers),
-//             else [a.stop, b.start) (empty if the hits overlap).
+//   segments  the read's hits sorted by (start, stop, label); consecutive hits (a, b) whose
+//             labels form a configuration rule (-c, e.g. "+:SP5,-SP27|-:SP27,-SP5") are a
+//             candidate segment on the rule's strand, span [a.start, b.stop) with -p (keep
+//             primers), else [a.stop, b.start) (empty if the hits overlap).  The segments are
+//             the best path over the candidates: no shared hit, greatest summed length
+//             (pychopper's usable length), ties -> the earlier candidate.
 // The host (dmx/chop.py) classifies reads by segment count and writes the outputs.
 //
 // MI355X design — integer/bit work, VALU-bound like the demux filter (no MFMA, no GEMM shape):
@@ -36,7 +37,7 @@
 //                 dropped and one lane per hit finds its start (an anchored Myers scan of the
 //                 reverse-complement label over the reverse-complement view, m + best
 //                 columns); the block groups its hits by read (counting scatter), one
-//                 lane per read insertion-sorts its few hits and pairs them, and the block
+//                 lane per read insertion-sorts its few hits and picks its segments, and the block
 //                 reserves its ranges of the global hit and segment lists with one atomic each.
 //   chop_blkscan_kernel, chop_order_kernel
 //                 move every block's ranges into read order (block order = read order), so the
@@ -310,8 +311,8 @@ __device__ __forceinline__ uint32_t chop_last_le(const uint32_t* pre, uint32_t n
     return lo;
 }
 
-// Once every read's hits are sorted in srt[s_off[t] .. s_off[t + 1]): one lane per read pairs
-// them greedily into seg[s_off[t] ...] (seg must not alias srt), the block reserves its output
+// Once every read's hits are sorted in srt[s_off[t] .. s_off[t + 1]): one lane per read picks
+// the best path over its candidate segments into seg[s_off[t] ...] (seg must not alias srt), the block reserves its output
 // ranges (one atomic per list) and writes them.  srt / seg: LDS (chop_kernel) or global scratch
 // (chop_big_kernel).  Every thread must call it.
 __device__ void chop_pair_write(const ChopArgs& A, uint32_t b, uint32_t r0, uint32_t nr,
@@ -322,11 +323,34 @@ __device__ void chop_pair_write(const ChopArgs& A, uint32_t b, uint32_t r0, uint
     if (threadIdx.x < nr) {
         const uint32_t t = threadIdx.x;
         const uint32_t o = s_off[t], c = s_off[t + 1] - o;
+        // Best path, right to left: b1 / b2 = greatest summed length over hits a+1.. / a+2..;
+        // candidate a (consecutive hits a, a+1 forming a rule) is taken when it reaches at
+        // least b1 (ties -> the earlier candidate).  Decisions go to the first word of seg[o+a]
+        // (free until the forward pass writes segment ns <= a over it, after reading it).
+        uint32_t* take = reinterpret_cast<uint32_t*>(seg + o);
+        uint64_t b1 = 0, b2 = 0;
+        for (uint32_t a = c > 1u ? c - 1u : 0u; a-- > 0;) {
+            const dmx_chop_hit h1 = srt[o + a], h2 = srt[o + a + 1];
+            uint64_t cur = b1;
+            uint32_t tk = 0;
+            if (s_rule[h1.label * kChopMaxLabels + h2.label] >= 0) {
+                const int32_t x0 = keep ? h1.start : h1.stop;
+                const int32_t x1 = keep ? h2.stop : h2.start;
+                const uint64_t v = (uint64_t)(uint32_t)max(0, x1 - x0) + b2;
+                if (v >= b1) {
+                    cur = v;
+                    tk = 1u;
+                }
+            }
+            take[4 * a] = tk;
+            b2 = b1;
+            b1 = cur;
+        }
         uint32_t ns = 0;
         for (uint32_t a = 0; a + 1 < c;) {
-            const dmx_chop_hit h1 = srt[o + a], h2 = srt[o + a + 1];
-            const int ri = s_rule[h1.label * kChopMaxLabels + h2.label];
-            if (ri >= 0) {
+            if (take[4 * a]) {
+                const dmx_chop_hit h1 = srt[o + a], h2 = srt[o + a + 1];
+                const int ri = s_rule[h1.label * kChopMaxLabels + h2.label];
                 dmx_chop_seg sg;
                 sg.read = h1.read;
                 const int32_t x0 = keep ? h1.start : h1.stop;

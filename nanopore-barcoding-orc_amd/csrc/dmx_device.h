@@ -60,6 +60,11 @@ struct DevPanel {
     int32_t filter_len;
     int32_t kf;          // max over adapters of kk
     int32_t max_mk;      // max over adapters of m + k + 1
+    // rows the filter kernel scans: the LAST scan_len (<= filter_len) rows of the block.  A
+    // suffix of the block ends at the same column and costs no more, so its cost is a lower
+    // bound of b(j) and the filter stays a necessary condition (verify / screen keep filter_len)
+    int32_t scan_len;
+    int32_t pad_scan;
     uint32_t filter_peq[8];
     int8_t pf[72];       // max over adapters of pacc[L]
     // Shared-prefix verification (0 = disabled): the first `pre_len` (<= 32) characters are common

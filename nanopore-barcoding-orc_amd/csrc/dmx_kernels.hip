@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     if (vbeg >= n_views) return;                       // block-uniform
     const uint32_t nv = min(n_views - vbeg, kSegViewsPerBlock);
     const int A = P->n_adapters;
-    const int L = P->filter_len;
+    const int L = P->scan_len;                         // the block's last L rows (<= filter_len)
     const int kf = P->kf;
     const uint32_t W = (uint32_t)(L + kf);
     const uint32_t SEG = (uint32_t)kSegSpan - W;       // host guarantees W <= 96
@@ -2545,7 +2545,7 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
     const uint32_t total = sm.total();
     const Cand* cl = R.cand[list];
     Outcome* outs = R.cand_out[list];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t wave = threadIdx.x >> 6;
 
     // One DP pass over the top `cnt` (<= 256) cells of queue e (block-uniform call).
     auto dp_pass = [&](int e, uint32_t cnt) {

@@ -16,10 +16,11 @@ Segment records are oriented (strand '-' reverse-complemented, qualities reverse
 given).  QC: a FASTQ read whose mean quality (-10 log10 of the mean error probability, Phred+33)
 is below -Q goes to -K if given, else is dropped.  Cutoff -q: maximum edit distance as a
 fraction of the primer length (k = int(q * m)); without -q it is tuned on the first -Y
-QC-passing reads of the first batch over 0.05, 0.10, ..., 0.40 (the value giving the most reads
-with exactly one segment — spurious hits at loose cutoffs split reads into fused "rescues";
-ties -> the smaller).  -k is accepted and unused (-b and -c define primers and
-layout); only -m edlib is implemented.
+QC-passing reads of the first batch over -L values evenly spaced on [0.1, 0.6] (the value whose
+segments have the most usable bases, i.e. the greatest summed segment length; ties -> the
+smaller).  A read's segments are the best path over its candidate segments (consecutive primer
+hits forming a config rule; no shared hit, greatest summed length).  -k is accepted and unused
+(-b and -c define primers and layout); only -m edlib is implemented.
 """
 from __future__ import annotations
 
@@ -34,7 +35,7 @@ from . import __version__, lib, nio, panel
 
 PRIMERS_FASTA = os.path.join(panel.DATA_DIR, "M13_seqs_for_pychopper.fa")
 CONFIG_FILE = os.path.join(panel.DATA_DIR, "M13_config_for_pychopper.txt")
-AUTOTUNE_CUTOFFS = (0.05, 0.1, 0.15, 0.2, 0.25, 0.3, 0.35, 0.4)
+AUTOTUNE_SAMPLES = 30
 PASS, RESCUED, UNCLASS, SHORT, QCFAIL = range(5)
 
 
@@ -69,6 +70,11 @@ def parse_config(text: str, names):
         except (ValueError, KeyError) as e:
             raise ValueError(f"bad pychopper config rule {part!r}") from e
     return rules
+
+
+def autotune_cutoffs(samples: int = AUTOTUNE_SAMPLES):
+    """The -q grid tried without -q (-L samples evenly spaced over [0.1, 0.6])."""
+    return [float(x) for x in np.linspace(0.1, 0.6, num=samples)]
 
 
 def plan_rows(nseg, segs, lens, qc_ok, min_len: int, outs):
@@ -156,15 +162,18 @@ class Chopper:
         nseg, _, segs, _ = self.ctx.chop_fetch()
         return nseg, segs
 
-    def autotune(self, sample_idx) -> float:
-        """The cutoff of AUTOTUNE_CUTOFFS with the most sampled reads having exactly one
-        segment (ties -> the smaller)."""
-        best, best_n = AUTOTUNE_CUTOFFS[0], -1
-        for q in AUTOTUNE_CUTOFFS:
+    def autotune(self, sample_idx, samples: int = AUTOTUNE_SAMPLES) -> float:
+        """The grid cutoff whose segments over the sampled reads have the greatest summed length
+        (usable bases; ties -> the smaller)."""
+        grid = autotune_cutoffs(samples)
+        best, best_n = grid[0], -1
+        sel = np.zeros(self.ctx._n_loaded, dtype=bool)
+        sel[sample_idx] = True
+        for q in grid:
             self.set_cutoff(q)
-            self.ctx.chop_exec()
-            nseg = self.ctx.chop_fetch(segs=False)[0]
-            c = int((nseg[sample_idx] == 1).sum())
+            nseg, segs = self.run()
+            ok = sel[segs["read"].astype(np.int64)]
+            c = int((segs["stop"].astype(np.int64)[ok] - segs["start"][ok]).sum())
             if c > best_n:
                 best, best_n = q, c
         return best
@@ -192,6 +201,8 @@ def build_parser():
     p.add_argument("-Q", dest="min_qual", type=float, default=7.0)
     p.add_argument("-z", dest="min_len", type=int, default=50)
     p.add_argument("-Y", dest="autotune_n", type=int, default=10000)
+    p.add_argument("-L", dest="autotune_samples", type=int, default=AUTOTUNE_SAMPLES,
+                   help="cutoff values tried when tuning -q (evenly spaced on [0.1, 0.6])")
     p.add_argument("-w", dest="rescued")
     p.add_argument("-u", dest="unclass")
     p.add_argument("-l", dest="short")
@@ -219,6 +230,8 @@ def run(argv=None) -> int:
         _err("only -m edlib is implemented (the pHMM backend is not on this path)")
     if args.cutoff is not None and not 0.0 <= args.cutoff < 1.0:
         _err("-q must be in [0, 1)")
+    if args.autotune_samples < 1:
+        _err("-L must be at least 1")
     primers = load_primers(args.primers)
     with open(args.config) as fh:
         rules = parse_config(fh.read(), [p[0] for p in primers])
@@ -249,7 +262,7 @@ def run(argv=None) -> int:
                     if cutoff is None:   # tune on the -Y sample alone, then load the batch
                         ctx.load(sample_packed(batch.packed,
                                                np.nonzero(qc_ok)[0][:args.autotune_n]))
-                        cutoff = ch.autotune(np.arange(ctx._n_loaded))
+                        cutoff = ch.autotune(np.arange(ctx._n_loaded), args.autotune_samples)
                     ctx.load(batch.packed)
                     ch.set_cutoff(cutoff)
                     nseg, segs = ch.run()

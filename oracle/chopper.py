@@ -18,16 +18,21 @@ options:
             start the smallest s with editdist(label, read[s:j)) == best (edlib takes the last
             position of its reverse SHW alignment: the longest optimal alignment) —
             oracle/chop_oracle.c (plain O(mn) DP) or `hits_py` (pure Python, tiny cases)
-  segments  a read's hits sorted by (start, stop, label) are paired greedily left to right by
-            the config rules (M13_config_for_pychopper.txt:1 "+:SP5,-SP27|-:SP27,-SP5"); span
-            [a.start, b.stop) with -p (keep primers), else [a.stop, b.start) (empty if they
-            overlap)
+  segments  a read's hits sorted by (start, stop, label); every pair of consecutive hits (a, b)
+            whose labels form a config rule (M13_config_for_pychopper.txt:1
+            "+:SP5,-SP27|-:SP27,-SP5"; the first rule naming the pair) is a candidate segment on
+            that rule's strand, span [a.start, b.stop) with -p (keep primers), else
+            [a.stop, b.start) (empty if they overlap).  The read's segments are the best path
+            over the candidates: no two chosen candidates share a hit, and the chosen set has
+            the greatest summed length (pychopper's usable length); on a tie the earlier
+            candidate is taken (right-to-left DP, `segments`)
   classes   FASTQ mean quality (-10 log10 of the mean error probability) < -Q -> qcfail;
             0 segments -> unclassified (record unchanged); 1 -> pass (short if < -z);
             >= 2 -> every segment rescued (short if < -z); '-' segments reverse-complemented;
             segment records named "{start}:{stop}|{id} strand=+|-" + the original comment
-  autotune  without -q: the cutoff of 0.05, 0.10, ..., 0.40 giving the most reads with
-            exactly one segment among the first -Y QC-passing reads (ties -> the smaller)
+  autotune  without -q: over the grid linspace(0.1, 0.6, -L) (-L = 30 samples), the cutoff
+            whose segments have the greatest summed length (usable bases) over the first -Y
+            QC-passing reads (ties -> the smaller cutoff)
 
 Only tests/ (and bench.py's cpu_baseline leg, through `batch_hit_counts`) use this module, as
 the checker of libdmx's `dmx_chop_*` (HIP) path and of the `bin/pychopper` drop-in.
@@ -41,7 +46,12 @@ import numpy as np
 
 import oracle as _orc
 
-AUTOTUNE_CUTOFFS = (0.05, 0.1, 0.15, 0.2, 0.25, 0.3, 0.35, 0.4)
+AUTOTUNE_SAMPLES = 30
+
+
+def autotune_cutoffs(samples: int = AUTOTUNE_SAMPLES):
+    """The -q grid tried without -q: `samples` values evenly spaced over [0.1, 0.6]."""
+    return [float(x) for x in np.linspace(0.1, 0.6, num=samples)]
 
 _COMP = str.maketrans("ACGTUMRWSYKVHDBNacgtumrwsykvhdbn", "TGCAAKYWSRMBDHVNtgcaakywsrmbdhvn")
 _IUPAC = {"A": "A", "C": "C", "G": "G", "T": "T", "U": "T", "R": "AG", "Y": "CT", "S": "CG",
@@ -159,22 +169,40 @@ def read_hits(labs, read: str, cutoff: float, impl=None):
 
 
 def segments(hits, rules, keep: bool):
-    """Greedy left-to-right pairing: [(start, stop, strand, rule)]."""
+    """Best path over the candidate segments of one read's sorted hits:
+    [(start, stop, strand, rule)], left to right."""
     table = {}
     for r, (a, b, st) in enumerate(rules):
         table.setdefault((a, b), (r, st))
-    segs, i = [], 0
-    while i + 1 < len(hits):
+    c = len(hits)
+    cand = [None] * c
+    for i in range(c - 1):
         h1, h2 = hits[i], hits[i + 1]
         rs = table.get((h1[2], h2[2]))
-        if rs is None:
+        if rs is not None:
+            a = h1[0] if keep else h1[1]
+            b = h2[1] if keep else h2[0]
+            cand[i] = (a, max(a, b), rs[1], rs[0])
+    best = [0] * (c + 2)    # best[i]: greatest summed length using hits i.. only
+    take = [False] * c
+    for i in range(c - 2, -1, -1):
+        best[i] = best[i + 1]
+        if cand[i] is not None:
+            t = cand[i][1] - cand[i][0] + best[i + 2]
+            if t >= best[i + 1]:
+                best[i], take[i] = t, True
+    segs, i = [], 0
+    while i + 1 < c:
+        if take[i]:
+            segs.append(cand[i])
+            i += 2
+        else:
             i += 1
-            continue
-        a = h1[0] if keep else h1[1]
-        b = h2[1] if keep else h2[0]
-        segs.append((a, max(a, b), rs[1], rs[0]))
-        i += 2
     return segs
+
+
+def usable_length(segs) -> int:
+    return sum(b - a for a, b, _, _ in segs)
 
 
 def mean_qual(qual: str) -> float:
@@ -223,13 +251,15 @@ def chop_records(records, primers, config: str, cutoff: float, keep: bool = True
 
 
 def autotune(records, primers, config: str, keep: bool = True, min_qual: float = 7.0,
-             sample: int = 10000, fasta: bool = False) -> float:
+             sample: int = 10000, fasta: bool = False, samples: int = AUTOTUNE_SAMPLES) -> float:
+    """-q when not given: the grid value with the most usable bases (summed segment length)
+    over the first `sample` QC-passing reads; ties -> the smaller cutoff."""
     labs = labels(primers)
     rules = parse_config(config, [p[0] for p in primers])
     pool = [s for _, s, q in records if fasta or mean_qual(q) >= min_qual][:sample]
     best, best_n = None, -1
-    for q in AUTOTUNE_CUTOFFS:
-        c = sum(1 for s in pool if len(segments(read_hits(labs, s, q), rules, keep)) == 1)
+    for q in autotune_cutoffs(samples):
+        c = sum(usable_length(segments(read_hits(labs, s, q), rules, keep)) for s in pool)
         if c > best_n:
             best, best_n = q, c
     return best

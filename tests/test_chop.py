@@ -49,6 +49,68 @@ def test_oracle_c_dp_matches_python_dp():
         assert ochop.hits_c(pat, read, cutoff) == ochop.hits_py(pat, read, cutoff), (pat, read)
 
 
+def _segments_brute(hits, rules, keep):
+    """Every set of hit-disjoint candidates; the greatest summed length, ties -> the set that
+    takes the earliest candidate where two sets first differ."""
+    table = {}
+    for r, (a, b, st) in enumerate(rules):
+        table.setdefault((a, b), (r, st))
+    cand = {}
+    for i in range(len(hits) - 1):
+        rs = table.get((hits[i][2], hits[i + 1][2]))
+        if rs is not None:
+            a = hits[i][0] if keep else hits[i][1]
+            b = hits[i + 1][1] if keep else hits[i + 1][0]
+            cand[i] = (a, max(a, b), rs[1], rs[0])
+    best = None
+    idx = sorted(cand)
+    for mask in range(1 << len(idx)):
+        pick = [idx[j] for j in range(len(idx)) if mask >> j & 1]
+        if any(b - a < 2 for a, b in zip(pick, pick[1:])):
+            continue
+        key = (-sum(cand[i][1] - cand[i][0] for i in pick), [-(i in pick) for i in idx])
+        if best is None or key < best[0]:
+            best = (key, pick)
+    return [cand[i] for i in best[1]] if best else []
+
+
+def test_best_path_segments_match_brute_force():
+    """Segment selection: hit-disjoint candidates of greatest summed length,
+    ties to the earlier candidate, against an exhaustive search on random hit lists."""
+    rng = np.random.default_rng(8)
+    for _ in range(3000):
+        nl = int(rng.integers(2, 7))
+        rules = [(int(rng.integers(nl)), int(rng.integers(nl)), int(rng.integers(2)))
+                 for _ in range(int(rng.integers(1, 6)))]
+        hits = sorted({(int(a), int(a) + int(rng.integers(0, 30)), int(rng.integers(nl)), 0)
+                       for a in rng.integers(0, 200, size=int(rng.integers(0, 11)))})
+        keep = bool(rng.integers(2))
+        got = ochop.segments(hits, rules, keep)
+        exp = _segments_brute(hits, rules, keep)
+        assert got == exp, (hits, rules, keep)
+
+
+def test_best_path_prefers_the_longer_of_overlapping_pairs():
+    # labels X=0, Y=1, Z=2; rules (X, Y) and (Y, Z): greedy pairing would take (X, Y)
+    rules = [(0, 1, 0), (1, 2, 1)]
+    hits = [(0, 10, 0, 0), (100, 110, 1, 0), (500, 510, 2, 0)]
+    assert ochop.segments(hits, rules, True) == [(100, 510, 1, 1)]
+    # equal lengths: the earlier candidate
+    hits = [(0, 10, 0, 0), (100, 110, 1, 0), (200, 210, 2, 0)]
+    assert ochop.segments(hits, rules, True) == [(0, 110, 0, 0)]
+    # disjoint candidates are all taken (the reference layout's fused reads)
+    primers, text = _ref_setup()
+    r = chop.parse_config(text, ["SP5", "SP27"])
+    hits = [(0, 58, 0, 3), (700, 758, 3, 2), (760, 818, 2, 1), (1500, 1558, 1, 4)]
+    assert ochop.segments(hits, r, True) == [(0, 758, 0, 0), (760, 1558, 1, 1)]
+
+
+def test_autotune_grid():
+    g = chop.autotune_cutoffs()
+    assert len(g) == 30 and g[0] == 0.1 and g[-1] == 0.6
+    assert g == ochop.autotune_cutoffs()
+
+
 def test_plan_rows_routes_in_input_order():
     nseg = np.array([0, 1, 2, 1, 0], np.uint32)
     segs = np.zeros(4, dtype=lib.CHOP_SEG_DTYPE)
@@ -172,7 +234,7 @@ def test_chop_hits_and_segments_match_oracle(ctx, cutoff, keep):
     assert S == eS
     assert np.bincount([h[0] for h in eH], minlength=len(seqs)).tolist() == nhit.tolist()
     assert np.bincount([s[0] for s in eS], minlength=len(seqs)).tolist() == nseg.tolist()
-    if cutoff <= 0.2:   # at 0.3 (k = 17 of 58) spurious hits break most reads' pairing
+    if cutoff <= 0.2:   # at 0.3 (k = 17 of 58) spurious hits break most reads' segments
         assert sum(1 for x in nseg if x == 1) > 0.5 * len(seqs)
 
 
