@@ -2056,6 +2056,13 @@ __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, 
 #ifndef DMX_WSCAN_WAVES
 #define DMX_WSCAN_WAVES 4
 #endif
+#ifndef DMX_SORT_GROUP
+#define DMX_SORT_GROUP 1024
+#endif
+constexpr int kSortGroup = DMX_SORT_GROUP;   // tasks ordered by length per block step
+constexpr int kSortBins = 64;                // counting-sort bins of 4 columns (last: >= 252)
+constexpr int kSortShift = 2;
+static_assert(kSortGroup % kScanBlock == 0, "sort group");
 template <bool BAND>
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_WSCAN_WAVES))) void wscan_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kPeqStride];
@@ -2092,29 +2099,77 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
 
     const int A = R.panel->n_adapters;
     if (R.screen) {   // the index screen's surviving (window piece, adapter) tasks
-      const uint32_t stride = gridDim.x * blockDim.x;
+      // A wave costs its longest task, and a FRONT panel's list mixes near pieces (a few
+      // columns, every adapter) with full windows (m + k + 1 + width columns): each block takes
+      // kSortGroup consecutive tasks at a time and runs them in order of their column count,
+      // so the 64 tasks of a wave have nearly equal lengths (tools/task_stats.py, round 1 of
+      // c2x24: wave max / mean 1.90 -> 1.09; window scan 4.8 -> 4.1 ms).  3' panels' tasks
+      // are already even (1.08), and there the sort only costs (2.4 -> 2.6 ms): not sorted.
+      const bool sorted = R.panel->where == kFront;
+      __shared__ uint32_t s_ord[kSortGroup];
+      __shared__ uint32_t s_bin[kSortBins];
+      __shared__ uint8_t s_mk[kMaxAdapters];
+      for (int a = threadIdx.x; a < A; a += blockDim.x)
+          s_mk[a] = (uint8_t)min(255, (int)R.panel->ad[a].m + (int)R.panel->ad[a].k + 1);
       {
         const Window* tl = R.tasks;
         const uint32_t nt = sm.total();
-        for (uint32_t base = blockIdx.x * blockDim.x; base < nt; base += stride) {
-            const uint32_t ti = base + threadIdx.x;
-            CandOut co;
-            TaskView tv{};
-            int sub = 0;
-            uint32_t item = 0;
-            if (ti < nt) {
-                const Window w = tl[sm.phys(ti)];
-                item = w.item;
-                wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, st, sink, co, tv,
-                                 sub);
+        for (uint32_t gb = blockIdx.x * kSortGroup; gb < nt; gb += gridDim.x * kSortGroup) {
+            const uint32_t gn = min((uint32_t)kSortGroup, nt - gb);
+            if (sorted) {   // block-uniform
+            if (threadIdx.x < kSortBins) s_bin[threadIdx.x] = 0;
+            __syncthreads();                       // (also: s_mk, and the last group's s_ord)
+            constexpr int PER = kSortGroup / kScanBlock;
+            uint32_t key[PER], pos[PER];
+#pragma unroll
+            for (int e = 0; e < PER; ++e) {
+                const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
+                key[e] = 0;
+                if (li < gn) {
+                    const Window* w = tl + sm.phys(gb + li);
+                    const int j1 = (int)w->j1, j2 = (int)w->j2, a = (int)w->info;
+                    const int cols = j2 - max(j1 - (int)s_mk[a], 0);
+                    key[e] = (uint32_t)min(max(cols, 0) >> kSortShift, kSortBins - 1);
+                    pos[e] = atomicAdd(&s_bin[key[e]], 1u);
+                }
             }
-            if constexpr (BAND) {
-                emit_cands(R, co, tv, item, sub, R.panel->ad[tv.a].m);
-                __builtin_amdgcn_wave_barrier();
-                if (sink.st[0].count() > DMX_WAVE_CAND_FLUSH) sink.st[0].flush();
-                if (sink.st[1].count() > DMX_WAVE_CAND_FLUSH) sink.st[1].flush();
-            } else {
-                if (stage_count(&s_clcnt) > kStageCap / 2) st.flush();
+            __syncthreads();
+            if (threadIdx.x == 0) {                // exclusive scan over the bins
+                uint32_t acc = 0;
+                for (int b = 0; b < kSortBins; ++b) {
+                    const uint32_t c = s_bin[b];
+                    s_bin[b] = acc;
+                    acc += c;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < PER; ++e) {
+                const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
+                if (li < gn) s_ord[s_bin[key[e]] + pos[e]] = li;
+            }
+            __syncthreads();
+            }
+            for (uint32_t sb = 0; sb < gn; sb += kScanBlock) {   // block-uniform
+                const uint32_t li = sb + threadIdx.x;
+                CandOut co;
+                TaskView tv{};
+                int sub = 0;
+                uint32_t item = 0;
+                if (li < gn) {
+                    const Window w = tl[sm.phys(gb + (sorted ? s_ord[li] : li))];
+                    item = w.item;
+                    wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, st, sink, co,
+                                     tv, sub);
+                }
+                if constexpr (BAND) {
+                    emit_cands(R, co, tv, item, sub, R.panel->ad[tv.a].m);
+                    __builtin_amdgcn_wave_barrier();
+                    if (sink.st[0].count() > DMX_WAVE_CAND_FLUSH) sink.st[0].flush();
+                    if (sink.st[1].count() > DMX_WAVE_CAND_FLUSH) sink.st[1].flush();
+                } else {
+                    if (stage_count(&s_clcnt) > kStageCap / 2) st.flush();
+                }
             }
         }
       }
@@ -2486,24 +2541,105 @@ __device__ __forceinline__ void band_dp2(const uint8_t* rm, const uint32_t* seq,
     score = ie - max(-origin, 0) - 2 * cost - v;
 }
 
+// 16 no-match bits -> the even bits of a word (bit k -> bit 2k), aligned with 2-bit codes.
+__device__ __forceinline__ uint32_t spread_even(uint32_t x) {
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    return (x | (x << 1)) & 0x55555555u;
+}
+
+// band_dp2 for a band inside the view (no column 0, no view end) and adapter rows of one code
+// each (A/C/G/T; the block checks its panel): every cell is ONE packed word
+//   S = cost << 9 | origin index << 3 | V
+// (origin index: the row-0 band cell the chosen path starts from; V: its vertical moves).
+// cutadapt's pointer rule — diagonal if the characters match or cost(diag) <= min(up, left),
+// else up if cost(up) <= cost(left), else left — is the lexicographic minimum of (cost,
+// preference) over the three moves with preference diagonal 0 < up 1 < left 2 (a matching
+// diagonal costs at most either other move, since neighbouring cells differ by <= 1).  So a cell
+// is one v_min3 over S_diag + mismatch << 9, S_up + (1 << 9 | 1 << 7 | 1) (an up move is one V)
+// and S_left + (1 << 9 | 2 << 7), with the preference bits cleared afterwards.  The three options
+// never tie in (cost, preference), so the low bits never decide.  V <= cost <= 7 on every path
+// that can reach the end cell (costs never fall along a path), so on those cells the 3-bit V
+// field cannot carry into the origin index; a cell of a larger cost is never chosen by one of a
+// smaller cost.  Mismatches for a whole row: the row's code replicated to every 2-bit field,
+// XORed with the 16 read codes; a field is nonzero where they differ (read N: never a match).
+template <int W>
+__device__ __forceinline__ void band_dp_fast(const uint8_t* rm, const uint32_t* seq,
+                                             const uint32_t* nmask, const TaskView& tv, int ie,
+                                             int je, int& cost, int& origin, int& score) {
+    static_assert(W <= 15, "origin index: 4 bits");
+    constexpr int H = W / 2;
+    constexpr uint32_t INF = 1u << 30;
+    constexpr uint32_t UP = (1u << 9) | (1u << 7) | 1u, LEFT = (1u << 9) | (2u << 7);
+    const int dx = je - ie;
+    uint32_t S[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) S[k] = (uint32_t)k << 3;   // row 0: free start, cost 0
+    int base = dx - H;
+    uint32_t w0, n0, w1, n1, w2, n2;
+    fetch16s(seq, nmask, tv, base, w0, n0);
+    fetch16s(seq, nmask, tv, base + 16, w1, n1);
+    fetch16s(seq, nmask, tv, base + 32, w2, n2);
+    n0 = spread_even(n0);
+    n1 = spread_even(n1);
+    int o = 0;
+    uint32_t rnext = rm[0];
+    for (int i = 1; i <= ie; ++i) {
+        if (o == 16) {                 // uniform: every lane advances one row per iteration
+            w0 = w1;
+            n0 = n1;
+            w1 = w2;
+            n1 = spread_even(n2);
+            base += 16;
+            fetch16s(seq, nmask, tv, base + 32, w2, n2);
+            o = 0;
+        }
+        const uint32_t codes = o ? __builtin_amdgcn_alignbit(w1, w0, 2 * o) : w0;
+        const uint32_t nbs = o ? __builtin_amdgcn_alignbit(n1, n0, 2 * o) : n0;
+        const uint32_t rb = rnext;
+        rnext = rm[min(i, 63) * kMaxAdapters];
+        const uint32_t x = codes ^ (((rb >> 4) & 3u) * 0x55555555u);
+        const uint32_t ne = x | (x >> 1) | nbs;   // bit 2k: cell k is a mismatch
+        uint32_t left = INF;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            const uint32_t d = S[k] + (__builtin_amdgcn_ubfe(ne, 2 * k, 1) << 9);
+            const uint32_t u = (k + 1 < W) ? S[k + 1] + UP : INF;
+            const uint32_t v = min(min(d, u), left + LEFT) & ~(3u << 7);
+            S[k] = v;
+            left = v;
+        }
+        ++o;
+    }
+    cost = (int)(S[H] >> 9);
+    origin = dx - H + (int)((S[H] >> 3) & 15u);
+    score = ie - 2 * cost - (int)(S[H] & 7u);
+}
+
 // The DP of one queued cell with the narrowest exact band for the wave: cells are sorted by cost
 // before a DP pass, so a wave's cells share a cost (or two neighbouring ones) and the wave runs
 // 2c + 1 diagonals for its largest cost c (wave-uniform branch; H >= c keeps the band exact).
 template <int C, int CMAX, bool EDGE>
-__device__ __forceinline__ void band_dp_cost(int wc, const uint8_t* rm, const uint32_t* seq,
-                                             const uint32_t* nmask, const TaskView& tv,
-                                             bool front, int ie, int je, int& cost, int& origin,
-                                             int& score) {
+__device__ __forceinline__ void band_dp_cost(int wc, bool fast, const uint8_t* rm,
+                                             const uint32_t* seq, const uint32_t* nmask,
+                                             const TaskView& tv, bool front, int ie, int je,
+                                             int& cost, int& origin, int& score) {
     if constexpr (C < CMAX) {
-        if (wc <= C) {
-            band_dp2<2 * C + 1, EDGE>(rm, seq, nmask, tv, front, ie, je, cost, origin, score);
+        if (wc > C) {
+            band_dp_cost<C + 1, CMAX, EDGE>(wc, fast, rm, seq, nmask, tv, front, ie, je, cost,
+                                             origin, score);
             return;
         }
-        band_dp_cost<C + 1, CMAX, EDGE>(wc, rm, seq, nmask, tv, front, ie, je, cost, origin,
-                                         score);
-    } else {
-        band_dp2<2 * C + 1, EDGE>(rm, seq, nmask, tv, front, ie, je, cost, origin, score);
     }
+    if constexpr (!EDGE) {
+        if (fast) {   // block-uniform
+            band_dp_fast<2 * C + 1>(rm, seq, nmask, tv, ie, je, cost, origin, score);
+            return;
+        }
+    }
+    band_dp2<2 * C + 1, EDGE>(rm, seq, nmask, tv, front, ie, je, cost, origin, score);
 }
 
 // Band kernel over one candidate list (costs CMIN..CMAX; cost-0 cells need no DP).  Every block
@@ -2527,11 +2663,17 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
     __shared__ uint32_t s_hist[8], s_nq[2], s_n;
     const DevPanel* P = R.panel;
     const int A = P->n_adapters;
+    // bits 0-3: codes adapter char i matches; bits 4-5: that code when it is exactly one
+    __shared__ uint32_t s_multi;   // some adapter char matches more or fewer than one code
+    if (threadIdx.x == 0) s_multi = 0;
+    __syncthreads();
     for (int x = threadIdx.x; x < 64 * A; x += blockDim.x) {
         const int a = x >> 6, i = x & 63;
         const DevAdapter& ad = P->ad[a];
         uint32_t r = 0;
         for (int c = 0; c < 4; ++c) r |= (uint32_t)((ad.peq[c] >> i) & 1ull) << c;
+        if (__popc(r) == 1) r |= (uint32_t)(__ffs(r) - 1) << 4;
+        else if (i < (int)ad.m) s_multi = 1u;
         s_rm[i * kMaxAdapters + a] = (uint8_t)r;
     }
     if (threadIdx.x == 0) {
@@ -2546,6 +2688,7 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
     const Cand* cl = R.cand[list];
     Outcome* outs = R.cand_out[list];
     const uint32_t wave = threadIdx.x >> 6;
+    const bool fast = s_multi == 0;                  // (read after sm.load's barrier)
 
     // One DP pass over the top `cnt` (<= 256) cells of queue e (block-uniform call).
     auto dp_pass = [&](int e, uint32_t cnt) {
@@ -2592,13 +2735,19 @@ __global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
                 tv.o = c.o;
                 tv.a = c.a;
                 int c2, origin, score;
+#ifdef DMX_BAND_SKIP_DP   // timing A/B only (results invalid): the band stage without its DPs
+                c2 = cst;
+                origin = (int)(c.j) - iend;
+                score = (int)wc;
+                if (false)
+#endif
                 if (e == 0)
                     band_dp_cost<CMIN == 0 ? 1 : CMIN, CMAX, false>(
-                        wc, s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend, j, c2,
+                        wc, fast, s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend, j, c2,
                         origin, score);
                 else
                     band_dp_cost<CMIN == 0 ? 1 : CMIN, CMAX, true>(
-                        wc, s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend, j, c2,
+                        wc, fast, s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend, j, c2,
                         origin, score);
                 if (c2 != cst) atomicOr(R.flags, 2u);    // band / scan disagreement: bug
                 const int lr = iend + (origin < 0 ? origin : 0);

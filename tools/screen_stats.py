@@ -53,6 +53,9 @@ def shape(w, ads, front: bool, rate: float):
     lanes = np.repeat(nch, q)
     n = len(lanes) // 64 * 64
     waves = lanes[:n].reshape(-1, 64)
+    # the same lanes sorted by chunk count inside each block iteration (256 lanes)
+    nb = len(lanes) // 256 * 256
+    srt = np.sort(lanes[:nb].reshape(-1, 256), axis=1).reshape(-1, 64)
     return {"windows": int(len(w)), "lanes": int(len(lanes)),
             "width_pcts": np.percentile(j2 - j1 + 1, [50, 90, 99, 99.9, 100]).tolist(),
             "chunks_lane_mean": float(lanes.mean()),
@@ -60,6 +63,8 @@ def shape(w, ads, front: bool, rate: float):
             "no_scan_frac": float((nch == 0).mean()),
             "wave_max_mean": float(waves.max(axis=1).mean()),
             "wave_max_over_mean": float(waves.max(axis=1).sum() / max(1, waves.mean(axis=1).sum())),
+            "wave_max_over_mean_block_sorted": float(srt.max(axis=1).sum() /
+                                                     max(1, srt.mean(axis=1).sum())),
             "lastcol_frac": float(lastc.mean()),
             "params": {"pre_len": pl, "filter_len": sl, "kf": kf, "jsplit": jsplit,
                        "index_len": [int(ls.min()), int(ls.max())]}}

@@ -27,7 +27,12 @@ def shape(t, m_of, k):
     width = t["j2"].astype(np.int64) - t["j1"].astype(np.int64) + 1
     n = len(cols) // 64 * 64
     waves = cols[:n].reshape(-1, 64)
-    return {"tasks": int(len(t)), "cols_mean": float(cols.mean()),
+    srt = {}
+    for blk in (256, 1024):   # sorted by column count inside groups of `blk` consecutive tasks
+        nb = len(cols) // blk * blk
+        sw = np.sort(cols[:nb].reshape(-1, blk), axis=1).reshape(-1, 64)
+        srt[blk] = float(sw.max(axis=1).sum() / max(1, sw.mean(axis=1).sum()))
+    return {"wave_max_over_mean_sorted_256": srt[256], "wave_max_over_mean_sorted_1024": srt[1024],"tasks": int(len(t)), "cols_mean": float(cols.mean()),
             "cols_pcts": np.percentile(cols, [50, 90, 99, 99.9, 100]).tolist(),
             "width_pcts": np.percentile(width, [50, 90, 99, 99.9, 100]).tolist(),
             "lastcol_frac": float((t["lastcol"] != 0).mean()),
