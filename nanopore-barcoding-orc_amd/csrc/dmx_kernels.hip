@@ -1752,6 +1752,14 @@ __device__ __forceinline__ uint32_t spread_bits_nib(uint32_t b) {
     return x << 3;
 }
 
+#ifndef DMX_SORT_GROUP
+#define DMX_SORT_GROUP 1024
+#endif
+constexpr int kSortGroup = DMX_SORT_GROUP;   // tasks ordered by length per block step
+constexpr int kSortBins = 64;                // counting-sort bins of 4 columns (last: >= 252)
+constexpr int kSortShift = 2;
+static_assert(kSortGroup % kScanBlock == 0, "sort group");
+
 constexpr int kScreenQuads = 8;             // adapters <= 32 (larger panels: iscreen_kernel)
 constexpr int kScreenRow = 8;               // u64 per code row (64 B)
 constexpr int kScreenCap = 128;             // per-wave task staging (4 pushes per lane per round)
@@ -1816,10 +1824,53 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     const int jsplit = front ? P->jsplit : 0;
     const bool pshared = P->pshared != 0;
 
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride) {
-        const uint32_t t = base + threadIdx.x;
-        const bool live = t < total;
+    // FRONT panels: a wave costs its longest lane, and near pieces (no scan) and wide windows
+    // share the list with the common ~3-chunk windows (tools/screen_stats.py: wave max / mean
+    // 1.37 on round 1 of c2x24); each block takes kSortGroup consecutive lanes at a time and runs
+    // them in order of their window's scan span.  3' panels' windows are even (1.04): unsorted.
+    const bool sorted = front;
+    __shared__ uint32_t s_ord[kSortGroup];
+    __shared__ uint32_t s_bin[kSortBins];
+    for (uint32_t gb = blockIdx.x * kSortGroup; gb < total; gb += gridDim.x * kSortGroup) {
+      const uint32_t gn = min((uint32_t)kSortGroup, total - gb);
+      if (sorted) {   // block-uniform
+        if (threadIdx.x < kSortBins) s_bin[threadIdx.x] = 0;
+        __syncthreads();                           // (also: the last group's s_ord)
+        constexpr int PER = kSortGroup / kScanBlock;
+        uint32_t key[PER], pos[PER];
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+            const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
+            key[e] = 0;
+            if (li < gn) {
+                const Window* w = wl + sm.phys((gb + li) / (uint32_t)Q);
+                const int j1 = (int)w->j1, j2 = (int)w->j2;
+                const int span = w->bmin != 255 ? j2 - max(j1, jsplit) : -1;
+                key[e] = span < 0 ? 0u : 1u + (uint32_t)min(span >> kSortShift, kSortBins - 2);
+                pos[e] = atomicAdd(&s_bin[key[e]], 1u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {                    // exclusive scan over the bins
+            uint32_t acc = 0;
+            for (int b = 0; b < kSortBins; ++b) {
+                const uint32_t c = s_bin[b];
+                s_bin[b] = acc;
+                acc += c;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+            const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
+            if (li < gn) s_ord[s_bin[key[e]] + pos[e]] = li;
+        }
+        __syncthreads();
+      }
+      for (uint32_t sb = 0; sb < gn; sb += kScanBlock) {   // block-uniform
+        const uint32_t li = sb + threadIdx.x;
+        const bool live = li < gn;
+        const uint32_t t = gb + (live ? (sorted ? s_ord[li] : li) : 0u);
         uint32_t near_m = 0, pass_m = 0, end_m = 0;   // per adapter k of the quad (bits 0..3)
         Window w{};
         int q = 0;
@@ -2010,6 +2061,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
         }
         __builtin_amdgcn_wave_barrier();
         if (st.count() > kScreenCap / 2) st.flush();
+      }
     }
     __builtin_amdgcn_wave_barrier();
     st.flush();
@@ -2056,13 +2108,6 @@ __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, 
 #ifndef DMX_WSCAN_WAVES
 #define DMX_WSCAN_WAVES 4
 #endif
-#ifndef DMX_SORT_GROUP
-#define DMX_SORT_GROUP 1024
-#endif
-constexpr int kSortGroup = DMX_SORT_GROUP;   // tasks ordered by length per block step
-constexpr int kSortBins = 64;                // counting-sort bins of 4 columns (last: >= 252)
-constexpr int kSortShift = 2;
-static_assert(kSortGroup % kScanBlock == 0, "sort group");
 template <bool BAND>
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_WSCAN_WAVES))) void wscan_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kPeqStride];
@@ -2651,7 +2696,19 @@ __device__ __forceinline__ void band_dp_cost(int wc, bool fast, const uint8_t* r
 // wave runs the narrowest band its cells allow (band_dp_cost).  The slot's best is the minimum
 // key over all its candidates (key order = locate's / best_match's / ReverseComplementer's order).
 template <int CMIN, int CMAX>
-__global__ __launch_bounds__(256) void band_cand_kernel(RoundArgs R, int list) {
+// Occupancy floors of list 0 (costs 1..3) and list 1 with kk <= 5: the DP passes wait on their
+// cells' loads, and 8 / 6 waves per SIMD (64 / 80 VGPRs) measured 8.44 -> 8.28 ms
+// per step on c2x24 against the compiler's 7 / 5 (list 0 then spills 2 VGPRs).  The kk <= 7
+// variant keeps its registers.
+#ifndef DMX_BAND_WAVES0
+#define DMX_BAND_WAVES0 8
+#endif
+#ifndef DMX_BAND_WAVES1
+#define DMX_BAND_WAVES1 6
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    CMAX <= 3 ? DMX_BAND_WAVES0 : (CMAX <= 5 ? DMX_BAND_WAVES1 : 1)))) void band_cand_kernel(
+    RoundArgs R, int list) {
     // s_rm[i * kMaxAdapters + a]: bit c = adapter a's char i matches read code c.  Row-major, so
     // the lanes of a wave (one row i, different adapters) read neighbouring bytes: no bank
     // conflicts (an adapter-major table put every adapter's row i in one of 4 banks).
