@@ -750,11 +750,114 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
     }
 }
 
+__device__ __forceinline__ uint32_t align32(uint32_t hi, uint32_t lo, uint32_t r) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> r);
+}
+
+__device__ __forceinline__ uint32_t bsel(uint32_t mask, uint32_t a, uint32_t b) {
+    return (a & mask) | (b & ~mask);      // mask ? a : b, bitwise (stays in registers)
+}
+
+// ---------------------------------------------------------------------------------------------
+// Consecutive 64-position stretches of a view, read as whole aligned 64-nt blocks of the packed
+// read (one 16-B code load + one 8-B mask load per block, instead of two 4-B gathers per 16
+// positions): the two blocks holding the current stretch and the next block in flight.  A lane's
+// stretches start 64 positions apart, so its bit alignment inside the blocks never changes and the
+// extraction is the filter's (seg_extract): word selects + funnel shifts, no indexed registers.
+// Strand 1 walks the global blocks downwards and reverses + complements each 16-position chunk.
+// ---------------------------------------------------------------------------------------------
+struct ViewBlocks {
+    uint32_t cw[12], nw[6];      // [0..7]/[0..3]: blocks B, B + 1 (ascending); [8..11]/[4..5]:
+                                 // the block in flight (B + 2 on strand 0, B - 1 on strand 1)
+    uint32_t m1, m2, r, r2;
+    const uint4* sp;
+    const uint2* np;
+    int64_t nxt;                 // the next block to load
+    bool rev;
+
+    __device__ __forceinline__ void load(int k, int64_t b) {
+        const uint4 c4 = sp[b];
+        cw[4 * k + 0] = c4.x;
+        cw[4 * k + 1] = c4.y;
+        cw[4 * k + 2] = c4.z;
+        cw[4 * k + 3] = c4.w;
+        const uint2 n2 = np[b];
+        nw[2 * k + 0] = n2.x;
+        nw[2 * k + 1] = n2.y;
+    }
+    // view positions [p, p + 64 * n_stretch) of the view (strand, start, n, off) of tv
+    __device__ __forceinline__ void init(const RoundArgs& R, const TaskView& tv, int p) {
+        rev = tv.strand != 0;
+        const int64_t g = rev ? (int64_t)tv.off + (int64_t)tv.n - 1 - tv.start - p - 63
+                              : (int64_t)tv.off + tv.start + p;
+        const int64_t blk = g >> 6;               // floor: the buffers carry guard words
+        const uint32_t sh = (uint32_t)(g & 63);
+        sp = reinterpret_cast<const uint4*>(R.seq);
+        np = reinterpret_cast<const uint2*>(R.nmask);
+        load(0, blk);
+        load(1, blk + 1);
+        nxt = rev ? blk - 1 : blk + 2;
+        load(2, nxt);
+        nxt += rev ? -1 : 1;
+        m1 = ((sh >> 4) & 1u) ? ~0u : 0u;
+        m2 = ((sh >> 5) & 1u) ? ~0u : 0u;
+        r = (2u * sh) & 31u;
+        r2 = sh & 31u;
+    }
+    // the current stretch as 4 chunks (view order), then slide by one block; `more`: a later
+    // stretch will be needed after the next one (load its block now)
+    __device__ __forceinline__ void extract(uint32_t vc[4], uint32_t vn[4], bool more) {
+        uint32_t a[7], t[5], asc[4], tn[3];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) a[k] = bsel(m1, cw[k + 1], cw[k]);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) t[k] = bsel(m2, a[k + 2], a[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) asc[k] = align32(t[k + 1], t[k], r);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) tn[k] = bsel(m2, nw[k + 1], nw[k]);
+        const uint32_t an[2] = {align32(tn[1], tn[0], r2), align32(tn[2], tn[1], r2)};
+        if (!rev) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                vc[c] = asc[c];
+                vn[c] = (an[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int d = 3 - c;
+                vc[c] = ~rev_pairs(asc[d]);                        // complement = 3 - code
+                vn[c] = __brev((an[d >> 1] >> (16 * (d & 1))) & 0xFFFFu) >> 16;
+            }
+        }
+        // slide: strand 0 (lo, hi, in flight) -> (hi, in flight, next);
+        //        strand 1 (lo, hi, in flight) -> (in flight, lo, next)
+        const uint32_t rm = rev ? ~0u : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t lo = cw[k], hi = cw[4 + k], fl = cw[8 + k];
+            cw[k] = bsel(rm, fl, hi);
+            cw[4 + k] = bsel(rm, lo, fl);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t lo = nw[k], hi = nw[2 + k], fl = nw[4 + k];
+            nw[k] = bsel(rm, fl, hi);
+            nw[2 + k] = bsel(rm, lo, fl);
+        }
+        if (more) {
+            load(2, nxt);
+            nxt += rev ? -1 : 1;
+        }
+    }
+};
+
 // ---------------------------------------------------------------------------------------------
 // filter: 32-bit Myers of the panel's shared suffix block (L rows) over every view, cut into
-// SEGMENTS of S = 256 - W view positions.  One lane per segment: lanes of a wave take
+// SEGMENTS of S = kSegSpan - W view positions.  One lane per segment: lanes of a wave take
 // consecutive segments of the same view, so their loads cover one contiguous stretch of the
-// packed read (each lane loads its 256 positions once, as five aligned 64-nt blocks).
+// packed read (each lane streams its positions once, as whole aligned 64-nt blocks).
 // A segment after the first starts W = L + kf columns early with the restricted-start column
 // D(i) = i: an alignment of the block with cost <= kf spans at most L + kf columns, so every
 // hit column of the segment (b(j) <= kf) is computed exactly.  Hit columns
@@ -766,7 +869,14 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
 #define DMX_SEG_VIEWS 512
 #endif
 constexpr uint32_t kSegViewsPerBlock = DMX_SEG_VIEWS;   // views per filter block (>= 256)
-constexpr int kSegSpan = 256;                 // view positions loaded per segment (S + W)
+// Segment span A/B with streamed blocks (c2x24, ms per step): 256 -> 52.38, 512 -> 52.41,
+// 768 -> 55.99 (the warm-up saved is lost to the longer idle tails of last segments)
+#ifndef DMX_SEG_SPAN
+#define DMX_SEG_SPAN 256
+#endif
+constexpr int kSegSpan = DMX_SEG_SPAN;        // view positions per segment (S + W)
+static_assert(kSegSpan % 256 == 0 && kSegSpan <= 1024, "segment span: whole 256-position buckets");
+constexpr int kStepsPerBucket = kSegSpan / 256;   // last segments grouped by 64-step count / this
 
 __device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskView& tv,
                                               uint32_t j1, uint32_t j2, int lastcol, int bmin) {
@@ -784,10 +894,6 @@ __device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskVi
     w.info = 0;
     w.off = tv.off;
     return w;
-}
-
-__device__ __forceinline__ uint32_t align32(uint32_t hi, uint32_t lo, uint32_t r) {
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> r);
 }
 
 struct SegState {
@@ -892,94 +998,20 @@ __device__ __forceinline__ void filter_chunk(uint32_t codes, uint32_t nb, uint32
     }
 }
 
-__device__ __forceinline__ uint32_t bsel(uint32_t mask, uint32_t a, uint32_t b) {
-    return (a & mask) | (b & ~mask);      // mask ? a : b, bitwise (stays in registers)
-}
-
-// The 5 aligned 64-nt blocks of a segment (ascending global nt; 4 code words + 2 mask words
-// per block) and the lane's bit offset into them.
-struct SegBlocks {
-    uint32_t cw[20], nw[10];
-    uint32_t m1, m2, mv1;      // word-offset select masks
-    uint32_t r, r2;            // bit offsets within a word (codes, mask)
-};
-
-// The next 64 view positions as 4 chunks (2-bit codes; 16 no-match bits each), then advance
-// the block window by one block (strand 0 up, strand 1 down).
-template <int STRAND>
-__device__ __forceinline__ void seg_extract(SegBlocks& B, uint32_t vc[4], uint32_t vn[4]) {
-    constexpr int b0 = STRAND == 0 ? 0 : 3;
-    uint32_t a[7], t[5], asc[4], tn[3];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) a[k] = bsel(B.m1, B.cw[4 * b0 + k + 1], B.cw[4 * b0 + k]);
-#pragma unroll
-    for (int k = 0; k < 5; ++k) t[k] = bsel(B.m2, a[k + 2], a[k]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) asc[k] = align32(t[k + 1], t[k], B.r);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) tn[k] = bsel(B.mv1, B.nw[2 * b0 + k + 1], B.nw[2 * b0 + k]);
-    const uint32_t an[2] = {align32(tn[1], tn[0], B.r2), align32(tn[2], tn[1], B.r2)};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        if constexpr (STRAND == 0) {
-            vc[c] = asc[c];
-            vn[c] = (an[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
-        } else {
-            const int d = 3 - c;
-            vc[c] = ~rev_pairs(asc[d]);                        // complement = 3 - code
-            vn[c] = __brev((an[d >> 1] >> (16 * (d & 1))) & 0xFFFFu) >> 16;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if constexpr (STRAND == 0) B.cw[k] = B.cw[k + 4];
-        else B.cw[19 - k] = B.cw[15 - k];
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        if constexpr (STRAND == 0) B.nw[k] = B.nw[k + 2];
-        else B.nw[9 - k] = B.nw[7 - k];
-    }
-}
-
-// Process view positions [P0, P1) (P1 - P0 <= kSegSpan) of one view.  Loaded: 256 positions
-// from the ascending global nt index g (strand 0: off + start + P0; strand 1: the lowest global
-// nt of the 256 positions, whose view order is descending).
+// Process view positions [P0, P1) (P1 - P0 <= kSegSpan) of one view, streaming the packed
+// read as whole aligned 64-nt blocks (ViewBlocks: two blocks held, the next one in flight).
 __device__ __forceinline__ void filter_segment(const RoundArgs& R, const TaskView& tv,
                                                uint32_t P0, uint32_t P1, SegState& S,
                                                const uint32_t* s_fpeq, const int8_t* s_thr,
                                                int kf_far, uint32_t gap, uint32_t hit_from,
                                                const WaveStage<Window, kWaveWinCap>& st,
                                                uint32_t item, int o) {
-    const bool rev = tv.strand != 0;
-    const int64_t g = rev ? (int64_t)tv.off + (int64_t)tv.n - 1 - tv.start - P0 - (kSegSpan - 1)
-                          : (int64_t)tv.off + tv.start + P0;
-    const int64_t blk = g >> 6;                   // floor: the buffers carry guard words
-    const uint32_t sh = (uint32_t)(g & 63);
-    const uint4* sp = reinterpret_cast<const uint4*>(R.seq) + blk;
-    const uint2* np = reinterpret_cast<const uint2*>(R.nmask) + blk;
-    SegBlocks B;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const uint4 c4 = sp[k];
-        B.cw[4 * k + 0] = c4.x;
-        B.cw[4 * k + 1] = c4.y;
-        B.cw[4 * k + 2] = c4.z;
-        B.cw[4 * k + 3] = c4.w;
-        const uint2 n2 = np[k];
-        B.nw[2 * k + 0] = n2.x;
-        B.nw[2 * k + 1] = n2.y;
-    }
-    B.m1 = ((sh >> 4) & 1u) ? ~0u : 0u;           // code-word offset sh / 16
-    B.m2 = ((sh >> 5) & 1u) ? ~0u : 0u;
-    B.mv1 = B.m2;                                 // mask-word offset sh / 32
-    B.r = (2u * sh) & 31u;
-    B.r2 = sh & 31u;
-
-    for (uint32_t p0 = P0; p0 < P1; p0 += 64) {
+    ViewBlocks B;
+    B.init(R, tv, (int)P0);
+    const uint32_t nsteps = (P1 - P0 + 63u) / 64u;
+    for (uint32_t s = 0, p0 = P0; p0 < P1; ++s, p0 += 64) {
         uint32_t vc[4], vn[4];
-        if (rev) seg_extract<1>(B, vc, vn);
-        else seg_extract<0>(B, vc, vn);
+        B.extract(vc, vn, s + 2u < nsteps);
         // per-column thresholds only near the view start (segment 0, grouped first in the
         // block's task order, so the branch is wave-uniform but for one wave); later segments
         // have threshold kf_far everywhere and mask their warm-up columns
@@ -1003,8 +1035,9 @@ __device__ __forceinline__ void filter_segment(const RoundArgs& R, const TaskVie
     }
 }
 
+// 5 waves per SIMD (96 VGPRs, one spilled) measured 52.41 -> 52.36 ms per step against 4
 #ifndef DMX_FILTER_WAVES
-#define DMX_FILTER_WAVES 4
+#define DMX_FILTER_WAVES 5
 #endif
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_FILTER_WAVES))) void filter_kernel(RoundArgs R) {
     __shared__ uint32_t s_fpeq[8];
@@ -1064,8 +1097,9 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             // an empty view of a 3' panel still gets its last-column window (one segment)
             cnt[e] = tv.len ? (tv.len + SEG - 1) / SEG : (P->where == kFront ? 0u : 1u);
             grp[e] = (int)tv.strand;
-            if (cnt[e] >= 2)   // last segment: positions [seg0 - W, len), in 64-position steps
-                bk[e] = (tv.len - (cnt[e] - 1u) * SEG + W + 63u) / 64u;
+            if (cnt[e] >= 2)   // last segment: positions [seg0 - W, len), in 64-position
+                bk[e] = ((tv.len - (cnt[e] - 1u) * SEG + W + 63u) / 64u + kStepsPerBucket - 1u) /
+                        kStepsPerBucket;   // steps, kStepsPerBucket per bucket (1..4)
         }
         const uint32_t f = cnt[e] ? 1u : 0u, l = cnt[e] >= 2 ? cnt[e] - 2u : 0u;
         if (grp[e]) {
@@ -1276,101 +1310,6 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
 }
 
 // ---------------------------------------------------------------------------------------------
-// Consecutive 64-position stretches of a view, read as whole aligned 64-nt blocks of the packed
-// read (one 16-B code load + one 8-B mask load per block, instead of two 4-B gathers per 16
-// positions): the two blocks holding the current stretch and the next block in flight.  A lane's
-// stretches start 64 positions apart, so its bit alignment inside the blocks never changes and the
-// extraction is the filter's (seg_extract): word selects + funnel shifts, no indexed registers.
-// Strand 1 walks the global blocks downwards and reverses + complements each 16-position chunk.
-// ---------------------------------------------------------------------------------------------
-struct ViewBlocks {
-    uint32_t cw[12], nw[6];      // [0..7]/[0..3]: blocks B, B + 1 (ascending); [8..11]/[4..5]:
-                                 // the block in flight (B + 2 on strand 0, B - 1 on strand 1)
-    uint32_t m1, m2, r, r2;
-    const uint4* sp;
-    const uint2* np;
-    int64_t nxt;                 // the next block to load
-    bool rev;
-
-    __device__ __forceinline__ void load(int k, int64_t b) {
-        const uint4 c4 = sp[b];
-        cw[4 * k + 0] = c4.x;
-        cw[4 * k + 1] = c4.y;
-        cw[4 * k + 2] = c4.z;
-        cw[4 * k + 3] = c4.w;
-        const uint2 n2 = np[b];
-        nw[2 * k + 0] = n2.x;
-        nw[2 * k + 1] = n2.y;
-    }
-    // view positions [p, p + 64 * n_stretch) of the view (strand, start, n, off) of tv
-    __device__ __forceinline__ void init(const RoundArgs& R, const TaskView& tv, int p) {
-        rev = tv.strand != 0;
-        const int64_t g = rev ? (int64_t)tv.off + (int64_t)tv.n - 1 - tv.start - p - 63
-                              : (int64_t)tv.off + tv.start + p;
-        const int64_t blk = g >> 6;               // floor: the buffers carry guard words
-        const uint32_t sh = (uint32_t)(g & 63);
-        sp = reinterpret_cast<const uint4*>(R.seq);
-        np = reinterpret_cast<const uint2*>(R.nmask);
-        load(0, blk);
-        load(1, blk + 1);
-        nxt = rev ? blk - 1 : blk + 2;
-        load(2, nxt);
-        nxt += rev ? -1 : 1;
-        m1 = ((sh >> 4) & 1u) ? ~0u : 0u;
-        m2 = ((sh >> 5) & 1u) ? ~0u : 0u;
-        r = (2u * sh) & 31u;
-        r2 = sh & 31u;
-    }
-    // the current stretch as 4 chunks (view order), then slide by one block; `more`: a later
-    // stretch will be needed after the next one (load its block now)
-    __device__ __forceinline__ void extract(uint32_t vc[4], uint32_t vn[4], bool more) {
-        uint32_t a[7], t[5], asc[4], tn[3];
-#pragma unroll
-        for (int k = 0; k < 7; ++k) a[k] = bsel(m1, cw[k + 1], cw[k]);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) t[k] = bsel(m2, a[k + 2], a[k]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) asc[k] = align32(t[k + 1], t[k], r);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) tn[k] = bsel(m2, nw[k + 1], nw[k]);
-        const uint32_t an[2] = {align32(tn[1], tn[0], r2), align32(tn[2], tn[1], r2)};
-        if (!rev) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                vc[c] = asc[c];
-                vn[c] = (an[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
-            }
-        } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int d = 3 - c;
-                vc[c] = ~rev_pairs(asc[d]);                        // complement = 3 - code
-                vn[c] = __brev((an[d >> 1] >> (16 * (d & 1))) & 0xFFFFu) >> 16;
-            }
-        }
-        // slide: strand 0 (lo, hi, in flight) -> (hi, in flight, next);
-        //        strand 1 (lo, hi, in flight) -> (in flight, lo, next)
-        const uint32_t rm = rev ? ~0u : 0u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t lo = cw[k], hi = cw[4 + k], fl = cw[8 + k];
-            cw[k] = bsel(rm, fl, hi);
-            cw[4 + k] = bsel(rm, lo, fl);
-        }
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t lo = nw[k], hi = nw[2 + k], fl = nw[4 + k];
-            nw[k] = bsel(rm, fl, hi);
-            nw[2 + k] = bsel(rm, lo, fl);
-        }
-        if (more) {
-            load(2, nxt);
-            nxt += rev ? -1 : 1;
-        }
-    }
-};
-
-// ---------------------------------------------------------------------------------------------
 // verify: one lane per filter window; 32-bit Myers of the shared PREFIX block over the columns
 // where the prefix of an alignment ending in the window would end.  Keeps the window only if
 //   (rows) some full alignment ending in [j1, j2] could cost <= kf: bmin + min D_pre <= kf
@@ -1380,6 +1319,14 @@ struct ViewBlocks {
 //          m_max - 1 - pre_len + kf columns of the end.
 // Survivors are compacted into the second window list for the window scan.
 // ---------------------------------------------------------------------------------------------
+#ifndef DMX_SORT_GROUP
+#define DMX_SORT_GROUP 1024
+#endif
+constexpr int kSortGroup = DMX_SORT_GROUP;   // tasks ordered by length per block step
+constexpr int kSortBins = 64;                // counting-sort bins of 4 columns (last: >= 252)
+constexpr int kSortShift = 2;
+static_assert(kSortGroup % kScanBlock == 0, "sort group");
+
 __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
     __shared__ Window s_w[kStageCap];
     __shared__ uint32_t s_wc, s_wb;
@@ -1399,10 +1346,54 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
     const bool front = P->where == kFront;
     const int L = P->pre_len, kf = P->kf;
     const uint32_t total = sm.total();
-    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
-        const uint32_t wi = base + threadIdx.x;
-        if (wi < total) {
-            Window w = R.win[sm.phys(wi)];
+    // FRONT panels: a wave costs its widest window (filter windows are ~11 columns wide, a few
+    // over 100), so each block takes kSortGroup consecutive windows at a time and runs them in
+    // order of their column range, as the screen and the window scan do.
+#ifndef DMX_VERIFY_SORT
+#define DMX_VERIFY_SORT 1
+#endif
+    const bool sorted = DMX_VERIFY_SORT && front;
+    __shared__ uint32_t s_ord[kSortGroup];
+    __shared__ uint32_t s_bin[kSortBins];
+    for (uint32_t gb = blockIdx.x * kSortGroup; gb < total; gb += gridDim.x * kSortGroup) {
+      const uint32_t gn = min((uint32_t)kSortGroup, total - gb);
+      if (sorted) {   // block-uniform
+        if (threadIdx.x < kSortBins) s_bin[threadIdx.x] = 0;
+        __syncthreads();                           // (also: the last group's s_ord)
+        constexpr int PER = kSortGroup / kScanBlock;
+        uint32_t key[PER], pos[PER];
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+            const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
+            key[e] = 0;
+            if (li < gn) {
+                const Window* w = R.win + sm.phys(gb + li);
+                const int span = (int)w->j2 - (int)w->j1;   // the rows range grows with it
+                key[e] = (uint32_t)min(max(span, 0) >> kSortShift, kSortBins - 1);
+                pos[e] = atomicAdd(&s_bin[key[e]], 1u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {                    // exclusive scan over the bins
+            uint32_t acc = 0;
+            for (int b = 0; b < kSortBins; ++b) {
+                const uint32_t c = s_bin[b];
+                s_bin[b] = acc;
+                acc += c;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+            const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
+            if (li < gn) s_ord[s_bin[key[e]] + pos[e]] = li;
+        }
+        __syncthreads();
+      }
+      for (uint32_t sb = 0; sb < gn; sb += kScanBlock) {   // block-uniform
+        const uint32_t li = sb + threadIdx.x;
+        if (li < gn) {
+            Window w = R.win[sm.phys(gb + (sorted ? s_ord[li] : li))];
             const int len = (int)w.len;
             const bool rows_free = (front && (int)w.j1 <= P->max_mk) || w.bmin == 255;
             // column ranges the prefix block must be evaluated on
@@ -1495,6 +1486,7 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
             if (keep) st.push(w);
         }
         if (stage_count(&s_wc) > kStageCap / 2) st.flush();
+      }
     }
     st.flush();
 }
@@ -1752,13 +1744,6 @@ __device__ __forceinline__ uint32_t spread_bits_nib(uint32_t b) {
     return x << 3;
 }
 
-#ifndef DMX_SORT_GROUP
-#define DMX_SORT_GROUP 1024
-#endif
-constexpr int kSortGroup = DMX_SORT_GROUP;   // tasks ordered by length per block step
-constexpr int kSortBins = 64;                // counting-sort bins of 4 columns (last: >= 252)
-constexpr int kSortShift = 2;
-static_assert(kSortGroup % kScanBlock == 0, "sort group");
 
 constexpr int kScreenQuads = 8;             // adapters <= 32 (larger panels: iscreen_kernel)
 constexpr int kScreenRow = 8;               // u64 per code row (64 B)
