@@ -209,12 +209,16 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
     }
 
     uint32_t p0 = js;
-    uint32_t ncodes, nnb;             // next chunk, prefetched one chunk ahead
+    uint32_t ncodes, nnb, ncodes2 = 0, nnb2 = 0;   // the next two chunks, in flight
     fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb);
+    if (p0 + 16 < jhi)
+        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes2, nnb2);
     for (; p0 + 16 <= jhi; p0 += 16) {
         const uint32_t codes = ncodes, nb = nnb;
-        if (p0 + 16 < jhi)
-            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes, nnb);
+        ncodes = ncodes2;
+        nnb = nnb2;
+        if (p0 + 32 < jhi)
+            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 32, ncodes2, nnb2);
 #pragma unroll
         for (int q = 0; q < 16; ++q) DMX_SCAN_STEP(q)
     }
@@ -554,12 +558,16 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
     };
 
     uint32_t p0 = js;
-    uint32_t ncodes, nnb;             // next chunk, prefetched one chunk ahead
+    uint32_t ncodes, nnb, ncodes2 = 0, nnb2 = 0;   // the next two chunks, in flight
     fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb);
+    if (p0 + 16 < jhi)
+        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes2, nnb2);
     for (; p0 + 16 <= jhi; p0 += 16) {
         const uint32_t codes = ncodes, nb = nnb;
-        if (p0 + 16 < jhi)
-            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes, nnb);
+        ncodes = ncodes2;
+        nnb = nnb2;
+        if (p0 + 32 < jhi)
+            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 32, ncodes2, nnb2);
         if (segset && p0 + 16 >= seg + 64) {   // this chunk could overflow the 64-bit segment
             flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
             segset = false;
