@@ -203,7 +203,7 @@ static_assert(sizeof(Cand) == 40, "Cand layout");
 struct Outcome {      // best cell found by the resolve lane of a cluster
     uint64_t key;     // ~0 = none
     int32_t origin;
-    int32_t pad;
+    int32_t pad;      // band_cand_kernel: the cell's winner slot (read by select_cand_kernel)
 };
 
 // 64-bit ordering key, smaller = better, matching cutadapt's selection order:

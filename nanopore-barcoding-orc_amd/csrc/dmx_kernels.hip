@@ -2805,7 +2805,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                     Outcome out;
                     out.key = make_key(score, c.o, cst, c.a, t);
                     out.origin = origin;
-                    out.pad = 0;
+                    out.pad = (int32_t)slot;             // select_cand needs no Cand reload
                     atomicMin(&R.winner[slot], (unsigned long long)out.key);
                     outs[cj] = out;
                 }
@@ -2838,6 +2838,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                     if (lr >= 0 && 0 <= (int)P->ad[c.a].acc[lr]) {
                         out.key = make_key(score, c.o, 0, c.a, t);
                         out.origin = origin;
+                        out.pad = (int32_t)slot;
                         atomicMin(&R.winner[slot], (unsigned long long)out.key);
                     }
                 } else {
@@ -2875,8 +2876,7 @@ __global__ void select_cand_kernel(RoundArgs R) {
             const uint32_t ci = sm.phys(ti);
             const Outcome o = R.cand_out[list][ci];
             if (o.key == ~0ull) continue;
-            const Cand c = R.cand[list][ci];
-            const uint32_t slot = slot_of(R, c.item, c.sub);
+            const uint32_t slot = (uint32_t)o.pad;   // band_cand_kernel stores the cell's slot
             if (R.winner[slot] == o.key) R.origin[slot] = o.origin;
         }
     }
