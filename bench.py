@@ -112,7 +112,23 @@ def _valu_ceiling() -> float:
         return 50.5e12
 
 
-VALU_CEILING = _valu_ceiling()   # independent v_bitop3 chains at full occupancy
+VALU_CEILING = _valu_ceiling()   # dependent v_bitop3 chain x4 per lane at full occupancy
+VALU_CEILING_WHAT = ("v_bitop3 dependency chains (each instruction uses the one before), four "
+                     "per lane, at full occupancy (" + os.path.relpath(VALU_CEILING_FILE, ROOT) +
+                     " 'bitop3_dependent_chain_t_lane_ops_per_s'); eight independent chains per "
+                     "lane reach less, 'bitop3_independent_t_lane_ops_per_s'")
+
+
+def survey_bytes_per_read(lengths: np.ndarray) -> np.ndarray:
+    """SURVEY.md §8(d) algorithmic HBM bytes per read: B(read) = ceil(L/4) (2-bit packed read)
+    + 8 (offset + length) + ceil(L/64) (N mask) + 24 (result record)."""
+    L = lengths.astype(np.float64)
+    return np.ceil(L / 4) + 8.0 + np.ceil(L / 64) + 24.0
+
+
+def survey_bytes(lengths: np.ndarray) -> float:
+    """Σ B(read) over the reads (views) one launch processes."""
+    return float(np.sum(survey_bytes_per_read(lengths)))
 
 
 def pmc_table(workload: str, reads: int):
@@ -170,11 +186,11 @@ def valu_roof(rate, clk_ghz, what: str):
     return out
 
 
-def filter_algorithmic_bytes(lengths: np.ndarray, n_windows: int) -> float:
-    """Algorithmic HBM bytes of one filter launch over these views: each read's
-    2-bit packed codes once (L/4 B) and its 1-bit no-match mask (L/8 B), its offset + length
-    (12 B), plus the 40-B window records the launch writes.  Both orientations of a read are
-    filtered from the same bytes."""
+def filter_layout_bytes(lengths: np.ndarray, n_windows: int) -> float:
+    """Bytes of one filter launch in this build's layout: each read's 2-bit
+    packed codes once (L/4 B) and its 1-bit no-match mask (L/8 B), its offset + length (12 B),
+    plus the 40-B window records the launch writes.  Both orientations of a read are filtered
+    from the same bytes.  Reported beside the §8(d) figure, never as roofline.achieved."""
     L = lengths.astype(np.float64)
     return float(np.sum(np.ceil(L / 4) + np.ceil(L / 8) + 12.0) + 40.0 * n_windows)
 
@@ -339,6 +355,7 @@ def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutof
                  "frac_of_measured_ceiling": (cols / (kern_ms / 1e3) * ops_col / VALU_CEILING
                                               if ops_col else None),
                  "measured_ceiling_lane_ops_per_s": VALU_CEILING,
+                 "measured_ceiling_what": VALU_CEILING_WHAT,
                  "source": "ops/column = SQ_INSTS_VALU x 64 of the PMC'd timed launch "
                            "(profiles/kernel_pmc.json 'chop:<reads>') / its Myers columns"},
         "stage_ms_per_step": {k: round(v / K, 3) for k, v in ms.items()},
@@ -357,10 +374,17 @@ def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, 
     m2 = res["bin1"] >= 0
     n2 = int(m2.sum())
     len2 = (lengths[m2] - res["m1_rstop"][m2]).astype(np.int64)
-    bytes0 = filter_algorithmic_bytes(lengths, int(windows_raw[0] / K))
-    bytes1 = filter_algorithmic_bytes(len2, int(windows_raw[1] / K))
-    alg_bytes = (bytes0 + bytes1) / 2
+    # roofline.achieved: SURVEY.md §8(d)'s B(read) over the views each filter launch scans
+    # (round 1: every read; round 2: the round-1-trimmed tails), averaged over the two launches
+    sb0, sb1 = survey_bytes(lengths), survey_bytes(len2)
+    alg_bytes = (sb0 + sb1) / 2
     achieved = alg_bytes / (filt_ms / 1e3) / 1e9
+    # this build's layout (1-bit mask, 40-B windows): a second figure, not the roofline's
+    lay0 = filter_layout_bytes(lengths, int(windows_raw[0] / K))
+    lay1 = filter_layout_bytes(len2, int(windows_raw[1] / K))
+    layout_bytes = (lay0 + lay1) / 2
+    step_ms = elapsed / K * 1e3
+    step_bytes = survey_bytes(lengths)   # §8(d): round 2 reuses the resident read
     traffic, traffic_src = pmc_traffic(args.workload, args.reads)
     A0, A1 = ctx.panel_sizes
     cols = float(lengths.sum()) * 2 + float(len2.sum()) * 2     # filter columns, both strands
@@ -382,6 +406,23 @@ def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, 
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": round(alg_bytes),
+                     "algorithmic_bytes_per_launch_r1_r2": [round(sb0), round(sb1)],
+                     "algorithmic_bytes_rule": "SURVEY.md §8(d) B(read) = ceil(L/4) + 8 + "
+                                               "ceil(L/64) + 24 over the launch's views, mean "
+                                               "of the round-1 and round-2 launches",
+                     "layout_bytes_per_launch": round(layout_bytes),
+                     "layout_bytes_rule": "this build's layout: ceil(L/4) + ceil(L/8) (1-bit "
+                                          "mask) + 12 per view + 40 B per emitted window",
+                     "traffic_over_algorithmic": (round(traffic / alg_bytes, 3)
+                                                  if traffic else None),
+                     "traffic_over_layout": (round(traffic / layout_bytes, 3)
+                                             if traffic else None),
+                     "per_step": {"bytes": round(step_bytes), "ms": round(step_ms, 3),
+                                  "achieved_gbs": round(step_bytes / (step_ms / 1e3) / 1e9, 3),
+                                  "frac": round(step_bytes / (step_ms / 1e3) / 1e9
+                                                / HBM_PEAK_GBS, 6),
+                                  "what": "§8(d) bytes of every read once per step (round 2 "
+                                          "reuses the resident read) / ms_per_step"},
                      "kernel": "dmx::filter_kernel", "avg_launch_ms": round(filt_ms, 3),
                      "share_of_step": round(2 * filt_ms / (elapsed / K * 1e3), 4),
                      "note": "the dominant kernel (largest share of the step, see 'kernels'); "
@@ -399,8 +440,8 @@ def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, 
                  "measured_ceiling_lane_ops_per_s": VALU_CEILING,
                  "nominal_peak_lane_ops_per_s": VALU_PEAK_TOPS * 1e12,
                  "source": "ops/column = SQ_INSTS_VALU x 64 of both PMC'd filter launches "
-                           "(profiles/kernel_pmc.json) / their columns; ceiling = independent "
-                           "v_bitop3 chains at full occupancy (profiles/r2_valu_ceiling.json)"},
+                           "(profiles/kernel_pmc.json) / their columns; ceiling = "
+                           + VALU_CEILING_WHAT},
         "kernels": kernel_table(args.workload, args.reads, stage, K, elapsed / K * 1e3),
         "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
         "clusters_per_step": (clusters / K).tolist(),
@@ -421,7 +462,8 @@ def linked_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen
     scan_ms = stage["scan0"] / K
     A0, _ = ctx.panel_sizes
     L = lengths.astype(np.float64)
-    alg_bytes = float(np.sum(np.ceil(L / 4) + np.ceil(L / 8) + 12.0))
+    alg_bytes = survey_bytes(lengths)   # SURVEY.md §8(d) B(read) over the consensuses
+    layout_bytes = float(np.sum(np.ceil(L / 4) + np.ceil(L / 8) + 12.0))
     achieved = alg_bytes / (scan_ms / 1e3) / 1e9
     traffic, traffic_src = pmc_traffic("c5", args.reads)
     vi = pmc_valu_insts("c5", args.reads, "scan_kernel<true>", first_only=True)
@@ -441,6 +483,11 @@ def linked_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": round(alg_bytes),
+                     "algorithmic_bytes_rule": "SURVEY.md §8(d) B(read) = ceil(L/4) + 8 + "
+                                               "ceil(L/64) + 24 over the launch's reads",
+                     "layout_bytes_per_launch": round(layout_bytes),
+                     "traffic_over_algorithmic": (round(traffic / alg_bytes, 3)
+                                                  if traffic else None),
                      "kernel": "dmx::scan_kernel<true>", "avg_launch_ms": round(scan_ms, 3),
                      "note": "VALU-bound bit-vector scan (DESIGN.md §5); the round-1 launch "
                              "(every front primer over every consensus)",

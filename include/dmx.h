@@ -176,7 +176,8 @@ int dmx_counts(dmx_ctx* ctx, uint64_t* out_counts, size_t n_out);
  * band DPs / tracebacks r0, r1, filter windows before prefix verification r0, r1, (window
  * piece, adapter) tasks passed by the index screen r0, r1}, and flags
  * (bit0 cluster overflow, bit1 exactness-check violation, bit2 filter-window overflow, bit3
- * candidate-cell overflow; must be 0). */
+ * candidate-cell overflow, bit4 filter step bucket out of range (a build-knob invariant, see
+ * kStepsPerBucket); must be 0). */
 int dmx_stats(dmx_ctx* ctx, float* stage_ms, int n_stage, uint64_t* counts, int n_counts,
               int* flags);
 

@@ -56,6 +56,12 @@ int dmx_io_abi_version(void);
 int dmx_io_gzip(const uint8_t* src, size_t n, int level, uint8_t* out, size_t cap,
                 size_t* out_len);
 
+/* Inflate a gzip stream held in memory (one or more members; tests and tools: the reader's
+ * own gzip path, parallel on `threads` unless DMX_SEQ_INFLATE=1) into out (cap bytes).
+ * 0 = OK (*out_len bytes), -2 = invalid / truncated stream or CRC mismatch, -3 = cap too small. */
+int dmx_io_inflate(const uint8_t* src, size_t n, int threads, uint8_t* out, size_t cap,
+                   size_t* out_len);
+
 /* path: a file (gzip detected by its magic bytes) or "-" for stdin. */
 int dmx_reader_open(const char* path, size_t batch_bytes, int threads, dmx_reader** out);
 /* Next batch in input order; *out = NULL at end of input. */
@@ -105,6 +111,12 @@ void dmx_sink_free(dmx_sink* s);
  * text from memory (no read, no inflate) and drops it.  Replaces: re-reading and inflating each
  * SP5 bin in the round-2 calls (scripts/02_cutadapt_loop.sh:91-103). */
 int dmx_sink_retain(dmx_sink* s, uint64_t max_bytes);
+/* Per output o: keep = 0 excludes it from retention (an output no later call reads back, e.g.
+ * the round-1 `unknown` bin that 02_cutadapt_loop.sh:79 skips); keep = 1 re-includes it before
+ * its first write.  Call after dmx_sink_retain. */
+int dmx_sink_retain_output(dmx_sink* s, int o, int keep);
+/* 1 if this reader takes its text from a retained sink output (no file read), else 0. */
+int dmx_reader_in_memory(const dmx_reader* r);
 /* Bytes of retained output text held in this process; drop all of it. */
 uint64_t dmx_io_retained_bytes(void);
 void dmx_io_drop_retained(void);

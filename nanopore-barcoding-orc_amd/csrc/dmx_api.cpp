@@ -1021,8 +1021,9 @@ int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const MaskSrc& nmask,
             int flags = 0;
             float ms[7];
             if ((rc = dmx_stats(c, ms, 7, cl, 8, &flags))) return rc;
-            if (flags & 2) {
-                c->err = "internal: traceback left the exact window (please report)";
+            if (flags & 18) {
+                c->err = (flags & 2) ? "internal: traceback left the exact window (please report)"
+                                     : "internal: filter step bucket out of range (please report)";
                 return DMX_E_STATE;
             }
             if (!(flags & 13)) break;
@@ -1073,21 +1074,29 @@ int run_impl(dmx_ctx* c, const uint32_t* seq2b, const MaskSrc& mask, const uint6
             c->err = "panels not set for this mode";
             return DMX_E_STATE;
         }
-        std::atomic<bool> bad{false};
+        // Every read must also sit at or after its chunk's base g0 = offsets[chunk lo] -
+        // DMX_PACK_PAD (+16, the guard any offset keeps): the device rebases offsets by g0, so
+        // a read below it (a permuted batch) would wrap.  Such a batch runs in one shot.
+        std::atomic<bool> bad{false}, permuted{false};
         parallel_ranges(n_reads, [&](size_t lo, size_t hi) {
-            for (size_t r = lo; r < hi; ++r)
+            for (size_t r = lo; r < hi; ++r) {
                 if (offsets[r] < 16 || (offsets[r] + lens[r] + 64) > (uint64_t)n_words * 16 ||
                     lens[r] >= (1u << 30)) {
                     bad = true;
                     return;
                 }
+                if (offsets[r] < offsets[r / per * per] - (uint64_t)DMX_PACK_PAD + 16u)
+                    permuted = true;
+            }
         });
         if (bad) {
             c->err = "read offsets/lengths do not fit the packed buffer (use dmx_pack)";
             return DMX_E_INVALID;
         }
-        return run_chunked(c, seq2b, mask, offsets, lens, n_words, n_reads, out, per);
+        chunkable = !permuted;
     }
+    if (chunkable)
+        return run_chunked(c, seq2b, mask, offsets, lens, n_words, n_reads, out, per);
     int rc = load_impl(c, seq2b, mask, offsets, lens, n_words, n_reads);
     if (rc) return rc;
     for (int attempt = 0; attempt < 8; ++attempt) {
@@ -1096,8 +1105,9 @@ int run_impl(dmx_ctx* c, const uint32_t* seq2b, const MaskSrc& mask, const uint6
         int flags = 0;
         float ms[7];
         if ((rc = dmx_stats(c, ms, 7, cl, 8, &flags))) return rc;
-        if (flags & 2) {
-            c->err = "internal: traceback left the exact window (please report)";
+        if (flags & 18) {
+            c->err = (flags & 2) ? "internal: traceback left the exact window (please report)"
+                                 : "internal: filter step bucket out of range (please report)";
             return DMX_E_STATE;
         }
         if (!(flags & 13)) return dmx_fetch(c, out);

@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "dmx_deflate.h"
+#include "dmx_inflate.h"
 #include "pack.h"
 
 // libdeflate (system library of the image; only the runtime .so is installed, so the few
@@ -410,6 +411,10 @@ struct GzSource : Source {
     }
 };
 
+// Any other gzip stream: parallel inflate (ParGzSource below), or zlib's sequential inflate
+// with DMX_SEQ_INFLATE=1.
+std::unique_ptr<Source> make_gz_source(std::unique_ptr<Source> raw, int threads);
+
 // gzip members that state their own size — our writer's "DX" extra subfield (compressed and
 // uncompressed member size) or BGZF's "BC" (bgzip, htslib) — are inflated in parallel, each
 // straight into its place in the batch buffer, and checked against the member's CRC-32 and
@@ -533,7 +538,7 @@ struct MemberGzSource : Source {
         pre->inner = std::move(raw);
         cbuf.clear();
         cpos = 0;
-        seq = std::make_unique<GzSource>(std::move(pre));
+        seq = make_gz_source(std::move(pre), threads);
     }
 
     long read(uint8_t* dst, size_t cap) override {
@@ -630,6 +635,369 @@ struct MemberGzSource : Source {
             }
         }
         return (long)got;
+    }
+};
+
+// Parallel inflate of gzip streams whose members do not state their size — an ordinary
+// single-member file such as 02_cutadapt_loop.sh's input `pychopped_<ds>.gz` (:15,28-34,71) —
+// on `threads` workers (dmx_inflate.h: speculative chunk decoding with a marker window, each
+// speculative start checked against the previous chunk's actual end, markers resolved against
+// the real window, CRC-32 / ISIZE of every member checked).  One round decodes up to `threads`
+// chunks of `chunk` compressed bytes; its output goes straight into the caller's buffer when
+// it fits.  DMX_INFLATE_CHUNK_KB sets the chunk size (tests use small chunks to put many chunk
+// edges into small files); DMX_SEQ_INFLATE=1 selects the sequential zlib path instead.
+struct ParGzSource : Source {
+    std::unique_ptr<Source> raw;
+    int threads = 1;
+    size_t chunk = 4u << 20;           // compressed bytes per chunk
+    size_t margin = 4u << 20;          // input held past the last chunk's nominal end
+    std::vector<uint8_t> cbuf;         // compressed input; cn valid bytes, then >= 64 zero bytes
+    size_t cn = 0;
+    bool raw_eof = false;
+    uint64_t pos = 0;                  // bit position in cbuf of the next decode
+    bool at_member = true, done = false;
+    std::vector<uint8_t> win;          // the last <= 32 KiB of output
+    bool in_member = false;            // CRC-32 / size of the current member's output so far
+    uint32_t mcrc = 0;
+    uint64_t msize = 0;
+    Bytes pend;                        // decoded output not yet delivered
+    size_t ppos = 0;
+
+    struct Chunk {
+        uint64_t nominal = 0, stop = 0, start = 0, end = 0;
+        bool found = false, bytes = false, atm_in = false, atm_out = false;
+        dmxi::Stop st = dmxi::Stop::kError;
+        dmxi::Buf<uint8_t> b8;
+        dmxi::Buf<uint16_t> b16, scratch;
+        std::vector<dmxi::Event> ev;
+        std::vector<uint8_t> w0;       // the real window before this chunk (resolve)
+        uint64_t n = 0, out = 0;       // output elements, offset in the round's output
+        std::vector<std::pair<uint64_t, uint32_t>> seg;   // (length, CRC-32) between events
+    };
+    std::vector<Chunk> ch;
+
+    explicit ParGzSource(std::unique_ptr<Source> r, int nth) : raw(std::move(r)), threads(nth) {
+        if (const char* e = getenv("DMX_INFLATE_CHUNK_KB")) {
+            const long kb = atol(e);
+            if (kb > 0) chunk = (size_t)kb << 10;
+        }
+        margin = std::max<size_t>(4u << 20, chunk);
+    }
+    size_t chunk_hint() const override { return 1u << 30; }
+
+    bool fill(size_t need) {   // cbuf holds >= need bytes from pos / 8 (or all of the input)
+        const size_t from = (size_t)(pos >> 3);
+        if (from > (64u << 20) && from * 2 > cn) {   // drop consumed input
+            cbuf.erase(cbuf.begin(), cbuf.begin() + (ptrdiff_t)from);
+            cn -= from;
+            pos -= (uint64_t)from * 8;
+        }
+        const size_t at = (size_t)(pos >> 3);
+        while (!raw_eof && cn - at < need) {
+            const size_t want = std::max<size_t>(need - (cn - at), 16u << 20);
+            cbuf.resize(cn + want + 64);
+            const long n = raw->read(cbuf.data() + cn, want);
+            if (n < 0) {
+                err = raw->err;
+                return false;
+            }
+            cn += (size_t)n;
+            if (n == 0) raw_eof = true;
+        }
+        cbuf.resize(cn + 64);
+        memset(cbuf.data() + cn, 0, 64);
+        return true;
+    }
+
+    // Decode chunk c from `from` with the real window `w` into bytes.
+    static dmxi::Stop decode_bytes(const dmxi::In& in, Chunk& c, uint64_t from, bool atm,
+                                   const std::vector<uint8_t>& w) {
+        // output estimate: ~3.5x the compressed bytes up to the stop (FASTQ), grown on demand
+        const uint64_t lim = std::min<uint64_t>(c.stop, in.end_bits());
+        c.b8.reserve(dmxi::kWin + (size_t)(lim > from ? (lim - from) / 8 * 7 / 2 : 0) + (1u << 16));
+        memset(c.b8.p, 0, dmxi::kWin - w.size());
+        memcpy(c.b8.p + dmxi::kWin - w.size(), w.data(), w.size());
+        c.b8.n = dmxi::kWin;
+        c.ev.clear();
+        c.start = from;
+        c.end = from;
+        c.atm_in = atm;
+        c.atm_out = atm;
+        c.bytes = true;
+        c.w0 = w;
+        c.st = dmxi::inflate_run<uint8_t>(in, c.end, c.atm_out, c.b8, dmxi::kWin - w.size(), c.stop,
+                                          c.ev);
+        c.n = c.b8.n - dmxi::kWin;
+        return c.st;
+    }
+
+    // The last <= 32 KiB of (w followed by chunk c's resolved output).
+    static bool tail_after(const std::vector<uint8_t>& w, const Chunk& c, std::vector<uint8_t>& t) {
+        const size_t keep = (size_t)std::min<uint64_t>(c.n, dmxi::kWin);
+        const size_t from_w = std::min<size_t>(w.size(), (size_t)dmxi::kWin - keep);
+        // a member starting inside the chunk resets the history: the window is then the output
+        // since that start, but the markers never reach before it, so keeping w is harmless
+        t.assign(w.end() - (ptrdiff_t)from_w, w.end());
+        const size_t o = t.size();
+        t.resize(o + keep);
+        if (c.bytes) {
+            memcpy(t.data() + o, c.b8.p + dmxi::kWin + (c.n - keep), keep);
+            return true;
+        }
+        const uint16_t* s = c.b16.p + dmxi::kWin + (c.n - keep);
+        const size_t wmiss = dmxi::kWin - w.size();   // markers below this index are undefined
+        for (size_t i = 0; i < keep; ++i) {
+            const uint16_t v = s[i];
+            if (v < 256) {
+                t[o + i] = (uint8_t)v;
+            } else {
+                const size_t wi = v - 256u;
+                if (wi < wmiss) return false;
+                t[o + i] = w[wi - wmiss];
+            }
+        }
+        return true;
+    }
+
+    // One round; 1 = done (output appended), 0 = retry with more input, -1 = error.
+    int round(uint8_t* dst, size_t cap, size_t& wrote) {
+        const int nth = std::max(1, threads);
+        if (!fill((size_t)nth * chunk + margin)) return -1;
+        const dmxi::In in{cbuf.data(), cn, raw_eof};
+        const uint64_t p0 = pos;
+        const size_t b0 = (size_t)(p0 >> 3);
+        const size_t avail = cn - b0;
+        // chunks of `chunk` bytes; at the end of the input the rest is split evenly (chunks of
+        // at least chunk / 4) so the last round keeps the threads busy too
+        size_t nch = 1, cs = chunk;
+        if (nth > 1) {
+            const size_t usable = raw_eof ? avail : (avail > margin ? avail - margin : 0);
+            const size_t minc = std::max<size_t>(chunk / 4, 64u << 10);
+            nch = std::max<size_t>(1, std::min<size_t>((size_t)nth, (usable + minc - 1) / minc));
+            if (raw_eof) cs = std::max<size_t>(minc, (usable + nch - 1) / nch);
+            nch = std::max<size_t>(1, std::min(nch, usable / std::max<size_t>(cs, 1) +
+                                                        (raw_eof ? 1 : 0)));
+        }
+        if (ch.size() < nch) ch.resize(nch);
+        for (size_t k = 0; k < nch; ++k) {
+            Chunk& c = ch[k];
+            c.nominal = k == 0 ? p0 : (uint64_t)(b0 + k * cs) * 8;
+            const uint64_t e = (uint64_t)(b0 + (k + 1) * cs) * 8;
+            c.stop = k + 1 < nch ? e : (raw_eof && e >= (uint64_t)cn * 8 ? UINT64_MAX : e);
+            c.found = false;
+            c.bytes = false;
+        }
+        const double t0 = kIoDebug ? now_s() : 0;
+        std::vector<double> tfind(nch, 0.0), tdec(nch, 0.0);
+        std::atomic<size_t> next{1};
+        parallel((int)nch, [&](int t) {
+            if (t == 0) {
+                decode_bytes(in, ch[0], p0, at_member, win);
+                ch[0].found = true;
+            }
+            for (size_t k; (k = next.fetch_add(1)) < nch;) {
+                Chunk& c = ch[k];
+                uint64_t s = 0;
+                const double tf = kIoDebug ? now_s() : 0;
+                const bool fnd = dmxi::find_block(in, c.nominal,
+                                                  c.stop == UINT64_MAX ? in.end_bits() : c.stop, s,
+                                                  c.scratch);
+                if (kIoDebug) tfind[k] = now_s() - tf;
+                if (!fnd) continue;
+                c.found = true;
+                c.start = s;
+                c.end = s;
+                c.atm_in = c.atm_out = false;
+                c.ev.clear();
+                const uint64_t lim = std::min<uint64_t>(c.stop, in.end_bits());
+                c.b16.reserve(dmxi::kWin + (size_t)(lim > s ? (lim - s) / 8 * 7 / 2 : 0) + (1u << 16));
+                for (int i = 0; i < dmxi::kWin; ++i) c.b16.p[i] = (uint16_t)(256 + i);
+                c.b16.n = dmxi::kWin;
+                c.st = dmxi::inflate_run<uint16_t>(in, c.end, c.atm_out, c.b16, 0, c.stop, c.ev);
+                c.n = c.b16.n - dmxi::kWin;
+                if (kIoDebug) tdec[k] = now_s() - tf - tfind[k];
+            }
+        });
+        const double t1 = kIoDebug ? now_s() : 0;
+        // stitch: accept a speculative chunk only where it starts at its predecessor's end,
+        // else decode it again from there with the real window
+        std::vector<uint8_t> w = win;
+        uint64_t total = 0;
+        for (size_t k = 0; k < nch; ++k) {
+            Chunk& c = ch[k];
+            if (k > 0) {
+                const Chunk& p = ch[k - 1];
+                if (p.st == dmxi::Stop::kEnd) {   // the stream ended before this chunk
+                    nch = k;
+                    break;
+                }
+                const bool ok = c.found && !c.bytes && c.start == p.end && !p.atm_out &&
+                                (c.st == dmxi::Stop::kBoundary || c.st == dmxi::Stop::kEnd);
+                if (!ok) decode_bytes(in, c, p.end, p.atm_out, w);
+                else c.w0 = w;
+            }
+            if (c.st == dmxi::Stop::kNeedMore) {
+                if (raw_eof) {
+                    err = "truncated gzip input";
+                    return -1;
+                }
+                margin *= 2;
+                return 0;
+            }
+            if (c.st == dmxi::Stop::kError) {   // near the end of the input: truncation
+                err = raw_eof && c.end + 512 >= in.end_bits() ? "truncated gzip input"
+                                                              : "gzip: invalid compressed data";
+                return -1;
+            }
+            std::vector<uint8_t> t;
+            if (!tail_after(w, c, t)) {
+                err = "gzip: invalid compressed data (distance too far back)";
+                return -1;
+            }
+            w.swap(t);
+            c.out = total;
+            total += c.n;
+        }
+        // resolve / copy into the destination and CRC the pieces between member events
+        const double t2 = kIoDebug ? now_s() : 0;
+        uint8_t* out = dst;
+        if (total > cap) {
+            pend.resize(total);
+            ppos = 0;
+            out = pend.data();
+        }
+        std::atomic<bool> bad{false};
+        std::atomic<size_t> nk{0};
+        parallel((int)std::min<size_t>(nch, (size_t)nth), [&](int) {
+            for (size_t k; (k = nk.fetch_add(1)) < nch;) {
+                Chunk& c = ch[k];
+                uint8_t* o = out + c.out;
+                if (c.bytes) {
+                    memcpy(o, c.b8.p + dmxi::kWin, c.n);
+                } else {
+                    const uint16_t* s = c.b16.p + dmxi::kWin;
+                    const size_t wmiss = dmxi::kWin - c.w0.size();
+                    const uint8_t* w0 = c.w0.data();
+                    bool fail = false;
+                    for (uint64_t i = 0; i < c.n; ++i) {
+                        const uint32_t v = s[i];
+                        if (v < 256) {
+                            o[i] = (uint8_t)v;
+                        } else if (v - 256u >= wmiss) {
+                            o[i] = w0[v - 256u - wmiss];
+                        } else {
+                            fail = true;
+                            o[i] = 0;
+                        }
+                    }
+                    if (fail) bad = true;
+                }
+                c.seg.clear();
+                uint64_t a = 0;
+                for (const auto& e : c.ev) {
+                    c.seg.emplace_back(e.out - a, libdeflate_crc32(0u, o + a, e.out - a));
+                    a = e.out;
+                }
+                c.seg.emplace_back(c.n - a, libdeflate_crc32(0u, o + a, c.n - a));
+            }
+        });
+        if (bad) {
+            err = "gzip: invalid compressed data (distance too far back)";
+            return -1;
+        }
+        for (size_t k = 0; k < nch; ++k) {
+            const Chunk& c = ch[k];
+            for (size_t s = 0; s < c.seg.size(); ++s) {
+                const uint64_t len = c.seg[s].first;
+                if (len) {
+                    if (!in_member) {
+                        err = "gzip: data outside a member";
+                        return -1;
+                    }
+                    mcrc = (uint32_t)crc32_combine(mcrc, c.seg[s].second, (z_off_t)len);
+                    msize += len;
+                }
+                if (s < c.ev.size()) {
+                    const dmxi::Event& e = c.ev[s];
+                    if (e.kind == 0) {
+                        in_member = true;
+                        mcrc = 0;
+                        msize = 0;
+                    } else {
+                        if (!in_member || e.crc != mcrc || e.isize != (uint32_t)msize) {
+                            err = "gzip: CRC-32 or length mismatch";
+                            return -1;
+                        }
+                        in_member = false;
+                    }
+                }
+            }
+        }
+        if (kIoDebug) {
+            double mf = 0, md = 0;
+            int redo = 0;
+            for (size_t k = 0; k < nch; ++k) {
+                mf = std::max(mf, tfind[k]);
+                md = std::max(md, tdec[k]);
+                redo += k > 0 && ch[k].bytes;
+            }
+            fprintf(stderr, "[pinflate] chunks %zu out %.1f MB: decode %.3f s (max find %.3f, "
+                    "max dec %.3f), stitch %.3f s, resolve+crc %.3f s, redone %d\n", nch,
+                    total / 1e6, t1 - t0, mf, md, t2 - t1, now_s() - t2, redo);
+        }
+        const Chunk& last = ch[nch - 1];
+        pos = last.end;
+        at_member = last.atm_out;
+        done = last.st == dmxi::Stop::kEnd;
+        if (done && in_member) {
+            err = "truncated gzip input";
+            return -1;
+        }
+        win.swap(w);
+        wrote = total > cap ? cap : (size_t)total;
+        if (total > cap) {
+            memcpy(dst, pend.data(), cap);
+            ppos = cap;
+        }
+        return 1;
+    }
+
+    long read(uint8_t* dst, size_t cap) override {
+        size_t got = 0;
+        if (ppos < pend.size()) {
+            got = std::min(cap, pend.size() - ppos);
+            memcpy(dst, pend.data() + ppos, got);
+            ppos += got;
+            if (ppos == pend.size()) {
+                pend.clear();
+                ppos = 0;
+            }
+        }
+        while (got < cap && !done) {
+            size_t w = 0;
+            const int r = round(dst + got, cap - got, w);
+            if (r < 0) return -1;
+            got += w;
+        }
+        return (long)got;
+    }
+};
+
+std::unique_ptr<Source> make_gz_source(std::unique_ptr<Source> raw, int threads) {
+    const char* e = getenv("DMX_SEQ_INFLATE");
+    if (e && atoi(e)) return std::make_unique<GzSource>(std::move(raw));
+    return std::make_unique<ParGzSource>(std::move(raw), threads);
+}
+
+// A memory range as a source (dmx_io_inflate).
+struct SpanSource : Source {
+    const uint8_t* p = nullptr;
+    size_t n = 0, at = 0;
+    long read(uint8_t* dst, size_t cap) override {
+        const size_t k = std::min(cap, n - at);
+        memcpy(dst, p + at, k);
+        at += k;
+        return (long)k;
     }
 };
 
@@ -908,6 +1276,7 @@ struct dmx_reader {
     size_t batch_bytes = 256u << 20;
     int threads = 1;
     int format = 0;   // 1 FASTQ, 2 FASTA
+    bool in_memory = false;   // the text comes from a retained sink output (no file read)
     Bytes carry;
     bool src_eof = false;
 
@@ -1083,6 +1452,7 @@ int dmx_reader_open(const char* path, size_t batch_bytes, int threads, dmx_reade
             m->pieces = std::move(ret.pieces);
             m->threads = clamp_threads(threads);
             r->src = std::move(m);
+            r->in_memory = true;
             r->batch_bytes = std::max<size_t>(batch_bytes, 1u << 16);
             r->threads = clamp_threads(threads);
             r->th = std::thread([r] { r->produce(); });
@@ -1116,7 +1486,7 @@ int dmx_reader_open(const char* path, size_t batch_bytes, int threads, dmx_reade
         m->threads = clamp_threads(threads);
         r->src = std::move(m);
     } else if (gz) {
-        r->src = std::make_unique<GzSource>(std::move(pre));
+        r->src = make_gz_source(std::move(pre), clamp_threads(threads));
     } else {
         r->src = std::move(pre);
     }
@@ -1146,6 +1516,33 @@ int dmx_reader_next(dmx_reader* r, dmx_batch** out) {
 }
 
 const char* dmx_reader_error(dmx_reader* r) { return r ? r->api_err.c_str() : "null reader"; }
+
+int dmx_reader_in_memory(const dmx_reader* r) { return r && r->in_memory ? 1 : 0; }
+
+int dmx_io_inflate(const uint8_t* src, size_t n, int threads, uint8_t* out, size_t cap,
+                   size_t* out_len) {
+    if ((!src && n) || (!out && cap) || !out_len) return -1;
+    auto sp = std::make_unique<SpanSource>();
+    sp->p = src;
+    sp->n = n;
+    auto gz = make_gz_source(std::move(sp), clamp_threads(threads));
+    size_t got = 0;
+    for (;;) {
+        const long k = gz->read(out + got, cap - got);
+        if (k < 0) return -2;
+        got += (size_t)k;
+        if (k == 0) break;
+        if (got == cap) {   // full: is there more?
+            uint8_t extra;
+            const long m = gz->read(&extra, 1);
+            if (m < 0) return -2;
+            if (m > 0) return -3;
+            break;
+        }
+    }
+    *out_len = got;
+    return 0;
+}
 
 void dmx_reader_close(dmx_reader* r) {
     if (!r) return;
@@ -1721,6 +2118,25 @@ int dmx_sink_retain(dmx_sink* s, uint64_t max_bytes) {
     s->cv.wait(lk, [&] { return !s->busy; });
     s->retain_cap = max_bytes;
     for (auto& f : s->outs) f.keep = max_bytes > 0 && f.gz && f.path != "-" && f.n == 0;
+    return 0;
+}
+
+int dmx_sink_retain_output(dmx_sink* s, int o, int keep) {
+    if (!s || o < 0 || o >= (int)s->outs.size()) return -1;
+    std::unique_lock<std::mutex> lk(s->mu);
+    s->cv.wait(lk, [&] { return !s->busy; });
+    Out& f = s->outs[o];
+    if (!keep) {   // never retained from here on; release what it already holds
+        if (f.kept_bytes) {
+            std::lock_guard<std::mutex> g(g_ret_mu);
+            g_ret_bytes -= f.kept_bytes;
+        }
+        f.kept_bytes = 0;
+        f.keep = false;
+        std::vector<Bytes>().swap(f.kept);
+    } else if (f.n == 0) {
+        f.keep = s->retain_cap > 0 && f.gz && f.path != "-";
+    }
     return 0;
 }
 

@@ -883,8 +883,19 @@ constexpr uint32_t kSegViewsPerBlock = DMX_SEG_VIEWS;   // views per filter bloc
 #define DMX_SEG_SPAN 256
 #endif
 constexpr int kSegSpan = DMX_SEG_SPAN;        // view positions per segment (S + W)
-static_assert(kSegSpan % 256 == 0 && kSegSpan <= 1024, "segment span: whole 256-position buckets");
-constexpr int kStepsPerBucket = kSegSpan / 256;   // last segments grouped by 64-step count / this
+// A view's last segment spans at most kSegSpan positions, i.e. ceil(kSegSpan / 64) 64-position
+// steps; the block prologue groups last segments into FOUR step buckets (16-bit fields of
+// s_tot / s_totl, LB[g][0..4]).  A span-384 A/B build with kStepsPerBucket = kSegSpan / 256 = 1
+// put 6-step segments in buckets 5..6: LB[g][5] read past the array, s_lastv written outside
+// its region, and the run died with an illegal memory access (round 3).  The bucket width is
+// therefore derived from the span so that the invariant below holds for every span; the kernel
+// also flags (bit 16) any bucket outside 1..4 instead of indexing with it.
+constexpr int kStepsPerBucket = (kSegSpan + 255) / 256;   // 64-position steps per bucket
+constexpr int kLastBuckets = 4;
+static_assert(kSegSpan >= 128 && kSegSpan <= 1024 && kSegSpan % 64 == 0,
+              "segment span: 128..1024 positions, whole 64-position steps");
+static_assert(kLastBuckets * kStepsPerBucket * 64 >= kSegSpan,
+              "every last segment's step count must fall into one of the four step buckets");
 
 __device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskView& tv,
                                               uint32_t j1, uint32_t j2, int lastcol, int bmin) {
@@ -1105,9 +1116,14 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             // an empty view of a 3' panel still gets its last-column window (one segment)
             cnt[e] = tv.len ? (tv.len + SEG - 1) / SEG : (P->where == kFront ? 0u : 1u);
             grp[e] = (int)tv.strand;
-            if (cnt[e] >= 2)   // last segment: positions [seg0 - W, len), in 64-position
+            if (cnt[e] >= 2) {   // last segment: positions [seg0 - W, len), in 64-position
                 bk[e] = ((tv.len - (cnt[e] - 1u) * SEG + W + 63u) / 64u + kStepsPerBucket - 1u) /
                         kStepsPerBucket;   // steps, kStepsPerBucket per bucket (1..4)
+                if (bk[e] < 1u || bk[e] > (uint32_t)kLastBuckets) {   // excluded statically
+                    atomicOr(R.flags, 16u);
+                    bk[e] = 0;
+                }
+            }
         }
         const uint32_t f = cnt[e] ? 1u : 0u, l = cnt[e] >= 2 ? cnt[e] - 2u : 0u;
         if (grp[e]) {

@@ -180,14 +180,23 @@ def run(argv=None, keep_contexts: bool = False) -> int:
     t0 = time.perf_counter()
     a1 = len(ads) if linked else 0
     totals = np.zeros((len(ads) + 1, a1 + 1), dtype=np.int64)
+    reader = nio.Reader(args.input, _batch_bytes(args), threads=args.cores)
     # the resident server keeps gzip outputs' text for the script's next calls, which read the
-    # round-1 bins back (02_cutadapt_loop.sh:91-103): DMX_RETAIN_MB caps it (0 disables)
-    retain = (int(os.environ.get("DMX_RETAIN_MB", "8192")) << 20) if keep_contexts else 0
-    sink = nio.Sink(paths, fasta_out, level, threads=args.cores, retain_bytes=retain)
+    # round-1 bins back (02_cutadapt_loop.sh:91-103); retain_plan says which outputs
+    untrimmed = len(names) if demux and not args.discard_untrimmed else None
+    retain, keep = retain_plan(paths, untrimmed, reader.in_memory, keep_contexts)
+    try:
+        sink = nio.Sink(paths, fasta_out, level, threads=args.cores, retain_bytes=retain)
+    except BaseException:
+        reader.close()
+        raise
+    for o, k in enumerate(keep):
+        if retain and not k:
+            sink.retain_output(o, False)
     _phase("sink", marks)
     tw = [0.0, 0.0, 0.0]   # read wait, GPU, plan + write enqueue
     try:
-        with nio.Reader(args.input, _batch_bytes(args), threads=args.cores) as reader:
+        with reader:
             _phase("reader", marks)
             t = time.perf_counter()
             for batch in reader:
@@ -234,6 +243,27 @@ def run(argv=None, keep_contexts: bool = False) -> int:
         print("dmx cli phases: " + " ".join(f"{k}={v:.3f}" for k, v in marks) +
               f" exec_to_import={_EXEC_TO_IMPORT:.2f}", file=sys.stderr)
     return 0
+
+
+def retain_plan(paths, untrimmed, input_in_memory: bool, resident: bool):
+    """(cap in bytes, keep flag per output) of the round-2 cache for one call; `untrimmed` is
+    the index of the demultiplexed `unknown` output, or None.
+
+    Only outputs a later call reads back are kept: in 02_cutadapt_loop.sh those are round 1's
+    SP5 bins (read by the round-2 calls, :91-103).  Not kept: the `unknown` bin (the identifier
+    scan at :79 skips it), every output of a call whose input itself came from the cache (a
+    round-2 call: its SP27 bins are never read again), and everything outside the resident
+    server.  The cap is nio.default_retain_bytes(): DMX_RETAIN_MB, else a quarter of the memory
+    still available to the job, at most 8 GiB."""
+    if not resident or input_in_memory:
+        return 0, [False] * len(paths)
+    cap = nio.default_retain_bytes()
+    if cap <= 0:
+        return 0, [False] * len(paths)
+    keep = [p.endswith(".gz") for p in paths]
+    if untrimmed is not None:   # the demultiplexed untrimmed bin ({name} -> "unknown")
+        keep[untrimmed] = False
+    return cap, keep
 
 
 def _batch_bytes(args) -> int:

@@ -10,9 +10,9 @@ stderr and exit status. The first call starts the server; it exits after `idle` 
 without a request. `DMX_DAEMON=0` makes every call run in its own process (the behaviour is
 the same either way; tests cover both).
 
-Isolation: one server per (user, checkout, SLURM job, GPU visibility). The socket name hashes
-SLURM_JOB_ID and the GPU-visibility variables (HIP/ROCR/CUDA_VISIBLE_DEVICES,
-GPU_DEVICE_ORDINAL), so a job never talks to another job's server (which would use the other
+Isolation: one server per (user, checkout, SLURM job, GPU visibility, library build). The socket
+name hashes SLURM_JOB_ID, the GPU-visibility variables (HIP/ROCR/CUDA_VISIBLE_DEVICES,
+GPU_DEVICE_ORDINAL) and the library selectors (DMX_LIBDMX, DMX_LIBDIR), so a job never talks to another job's server (which would use the other
 job's GPUs and die with it, `04_cleaning_primers.sh:4,7` is a 96-task array), and the server,
 spawned by its first client, sees exactly the devices its callers see. A request is served
 with only its own DMX_* variables; contexts are cached per (devices, dmx_open-time switches).
@@ -41,6 +41,10 @@ PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # variables that decide which GPUs a process sees (and so which server may serve it)
 VISIBILITY_ENV = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
                   "GPU_DEVICE_ORDINAL")
+# variables that decide which libdmx / libdmx_io build a process loads (read once at import by
+# dmx/lib.py and dmx/nio.py, so a server cannot switch them per request): a call that sets them
+# (A/B or sanitizer builds) gets a server of its own
+LIBRARY_ENV = ("DMX_LIBDMX", "DMX_LIBDIR")
 
 
 def socket_path(env=None) -> str:
@@ -56,7 +60,7 @@ def socket_path(env=None) -> str:
             tmp = d
             break
     scope = "|".join([PKG, env.get("SLURM_JOB_ID", "")] +
-                     [f"{k}={env.get(k, '<unset>')}" for k in VISIBILITY_ENV])
+                     [f"{k}={env.get(k, '<unset>')}" for k in VISIBILITY_ENV + LIBRARY_ENV])
     return os.path.join(tmp, f"dmx-{os.getuid()}-{zlib.crc32(scope.encode()):08x}.sock")
 
 
@@ -133,6 +137,19 @@ def _handle(conn) -> bool:
     return fatal
 
 
+def _admit(busy, state) -> bool:
+    """Take the one-call lock for an accepted connection.  One call runs at a time; others are
+    answered "busy" and run in-process.  So is a call accepted after a worker hit a GPU error
+    (state["fatal"], set just before that worker released the lock): it must not run on contexts
+    that may hold a sticky HIP error, and the accept loop exits right after."""
+    if not busy.acquire(blocking=False):
+        return False
+    if state["fatal"]:
+        busy.release()
+        return False
+    return True
+
+
 def serve(path: str, idle: float):
     srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
     try:
@@ -168,7 +185,7 @@ def serve(path: str, idle: float):
                 if not busy.locked() and time.monotonic() - state["last"] > idle:
                     break
                 continue
-            if not busy.acquire(blocking=False):   # one call at a time; others run in-process
+            if not _admit(busy, state):
                 with conn:
                     try:   # take the request off the wire first, so the client sees the reply
                         conn.settimeout(2.0)

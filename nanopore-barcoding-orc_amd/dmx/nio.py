@@ -22,7 +22,8 @@ IO_EXPORTS = ["dmx_io_abi_version", "dmx_reader_open", "dmx_reader_next", "dmx_r
               "dmx_reader_close", "dmx_batch_free", "dmx_sink_open", "dmx_sink_write",
               "dmx_sink_close", "dmx_sink_error", "dmx_sink_free", "dmx_sink_write_rows",
               "dmx_batch_mean_qual", "dmx_io_gzip", "dmx_sink_retain", "dmx_io_retained_bytes",
-              "dmx_io_drop_retained"]
+              "dmx_io_drop_retained", "dmx_sink_retain_output", "dmx_reader_in_memory",
+              "dmx_io_inflate"]
 
 
 class _CBatch(ctypes.Structure):
@@ -69,6 +70,11 @@ def load() -> ctypes.CDLL:
     L.dmx_sink_retain.argtypes = [P, ctypes.c_uint64]
     L.dmx_io_retained_bytes.restype = ctypes.c_uint64
     L.dmx_io_drop_retained.restype = None
+    L.dmx_sink_retain_output.argtypes = [P, c_int, c_int]
+    L.dmx_reader_in_memory.argtypes = [P]
+    L.dmx_reader_in_memory.restype = c_int
+    L.dmx_io_inflate.argtypes = [ctypes.c_char_p, c_size, c_int, P, c_size, P]
+    L.dmx_io_inflate.restype = c_int
     if L.dmx_io_abi_version() != 1:
         raise DmxError("libdmx_io ABI mismatch")
     _io = L
@@ -157,6 +163,11 @@ class Reader:
         self._h = h
         self.path = path
 
+    @property
+    def in_memory(self) -> bool:
+        """The text comes from a retained sink output of this process (dmx_reader_in_memory)."""
+        return bool(self._h) and bool(self._L.dmx_reader_in_memory(self._h))
+
     def __iter__(self):
         while True:
             b = self.next()
@@ -196,6 +207,52 @@ def drop_retained():
     load().dmx_io_drop_retained()
 
 
+def _read_int(path: str):
+    try:
+        with open(path) as fh:
+            v = fh.read().strip()
+        return None if v in ("", "max") else int(v)
+    except (OSError, ValueError):
+        return None
+
+
+def available_memory_bytes():
+    """Memory this process can still take: the smaller of MemAvailable (/proc/meminfo) and the
+    cgroup's limit minus its usage (v2 memory.max / memory.current, or v1 limit / usage; a
+    SLURM job's --mem lands there).  None when neither is readable."""
+    cands = []
+    try:
+        with open("/proc/meminfo") as fh:
+            for line in fh:
+                if line.startswith("MemAvailable:"):
+                    cands.append(int(line.split()[1]) * 1024)
+                    break
+    except (OSError, ValueError, IndexError):
+        pass
+    for lim, cur in (("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory.current"),
+                     ("/sys/fs/cgroup/memory/memory.limit_in_bytes",
+                      "/sys/fs/cgroup/memory/memory.usage_in_bytes")):
+        limit, used = _read_int(lim), _read_int(cur)
+        if limit is not None and used is not None and limit < (1 << 60):
+            cands.append(max(0, limit - used))
+            break
+    return min(cands) if cands else None
+
+
+def default_retain_bytes(cap_mb=None) -> int:
+    """The resident server's round-2 cache cap: DMX_RETAIN_MB when set (0 disables), else a
+    quarter of the memory still available to the process (cgroup limit or MemAvailable) and
+    at most 8 GiB.  02_cutadapt_loop.sh runs under `#SBATCH --mem=4G`: retaining more than the
+    job can hold would get the server OOM-killed in the middle of the loop."""
+    env = os.environ.get("DMX_RETAIN_MB", "").strip() if cap_mb is None else str(cap_mb)
+    if env:
+        return max(0, int(env)) << 20
+    avail = available_memory_bytes()
+    if avail is None:
+        return 0
+    return int(min(8 << 30, avail // 4))
+
+
 class Sink:
     """Outputs (created now) receiving records in input order; '.gz' paths are gzip members."""
 
@@ -218,6 +275,11 @@ class Sink:
         self.n_written = self.bp_written = None
         if retain_bytes > 0:
             self._L.dmx_sink_retain(self._h, int(retain_bytes))
+
+    def retain_output(self, o: int, keep: bool):
+        """Include or exclude output o from retention (dmx_sink_retain_output)."""
+        if self._L.dmx_sink_retain_output(self._h, int(o), int(bool(keep))) != 0:
+            raise ValueError(f"no output {o}")
 
     def write(self, batch: NativeBatch, out_idx, start, stop, rc, n_rc):
         n = len(batch)

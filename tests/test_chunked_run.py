@@ -153,3 +153,25 @@ def test_sparse_mask_run_matches_dense(c2x24, chunk, monkeypatch):
         again = ctx.run(p)
     assert sparse.tobytes() == dense.tobytes() == again.tobytes()
     assert c_sparse.sum() > 0
+
+
+def test_permuted_batch_runs_one_shot(c2x24, monkeypatch):
+    """A dmx_pack batch whose reads are reordered (every offset aligned, but some below their
+    chunk's first offset) must not be chunked: the device rebase by the chunk base would wrap.
+    It runs in one shot and its results are the unpermuted run's, permuted."""
+    d, p = c2x24
+    perm = np.random.default_rng(7).permutation(p.n_reads)
+    q = lib.Packed(p.seq2b, p.nmask, p.offsets[perm].copy(), p.lengths[perm].copy())
+    monkeypatch.setenv("DMX_RUN_CHUNK", "3000")
+    with lib.Context(0) as ctx:
+        _setup(ctx, d)
+        got = ctx.run(q)
+        got_counts = ctx.counts()
+        ctx.fetch()          # a one-shot run leaves its results fetchable (not chunked)
+    monkeypatch.setenv("DMX_RUN_CHUNK", "0")
+    with lib.Context(0) as ctx:
+        _setup(ctx, d)
+        exp = ctx.run(p)
+        exp_counts = ctx.counts()
+    assert got.tobytes() == exp[perm].tobytes()
+    assert got_counts.tolist() == exp_counts.tolist()

@@ -32,7 +32,7 @@ def _client_module():
 
 def _scoped(monkeypatch, **env):
     monkeypatch.delenv("DMX_DAEMON_SOCK", raising=False)
-    for k in daemon.VISIBILITY_ENV + ("SLURM_JOB_ID",):
+    for k in daemon.VISIBILITY_ENV + daemon.LIBRARY_ENV + ("SLURM_JOB_ID",):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -46,7 +46,10 @@ def test_socket_scope_by_gpu_visibility_and_job(monkeypatch):
                       "rocr1": {"ROCR_VISIBLE_DEVICES": "1"},
                       "job7": {"SLURM_JOB_ID": "7"},
                       "job8": {"SLURM_JOB_ID": "8"},
-                      "job7_hip1": {"SLURM_JOB_ID": "7", "HIP_VISIBLE_DEVICES": "1"}}.items():
+                      "job7_hip1": {"SLURM_JOB_ID": "7", "HIP_VISIBLE_DEVICES": "1"},
+                      # another libdmx / libdmx_io build (A/B, sanitizers): its own server
+                      "libdmx_ab": {"DMX_LIBDMX": "/x/libdmx_ab.so"},
+                      "libdir_asan": {"DMX_LIBDIR": "/x/build/asan"}}.items():
         _scoped(monkeypatch, **env)
         paths[name] = client._sock_path()
         assert paths[name] == daemon.socket_path(), "client and server disagree on the socket"
@@ -146,6 +149,19 @@ def test_gpu_error_ends_the_server(server):
     th.join(10)
     assert not th.is_alive()
     assert not os.path.exists(path)
+
+
+def test_call_after_a_gpu_error_is_not_admitted():
+    """a connection accepted between a worker's GPU error and the accept loop's exit
+    gets the lock but must be answered "busy" (run in-process), not served."""
+    busy = threading.Lock()
+    state = {"fatal": False}
+    assert daemon._admit(busy, state)
+    assert not daemon._admit(busy, state)     # a call is running
+    busy.release()
+    state["fatal"] = True                     # the worker's GPU error, lock released after it
+    assert not daemon._admit(busy, state)
+    assert not busy.locked()                  # the lock is not leaked
 
 
 def test_server_unlinks_only_its_own_socket(tmp_path, monkeypatch):

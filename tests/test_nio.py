@@ -303,3 +303,216 @@ def test_retained_outputs_read_back_without_the_file(tmp_path):
     write_bins(1 << 30)
     nio.drop_retained()
     assert nio.retained_bytes() == base
+
+
+def test_retain_plan_keeps_only_bins_read_back(tmp_path, monkeypatch):
+    """the resident server retains only outputs a later call reads back — round 1's
+    bins, not its `unknown` bin (02_cutadapt_loop.sh:79 skips it) and nothing of a call whose
+    input came from the cache (round 2) — under a cap that fits the job's memory."""
+    from dmx import cli
+    recs, text = _records(3000, seed=6)
+    src = tmp_path / "in.fastq"
+    src.write_text(text)
+    r1 = [str(tmp_path / f"SP5_{i}.fastq.gz") for i in range(2)] + [str(tmp_path / "unknown.fastq.gz")]
+    nio.drop_retained()
+    base = nio.retained_bytes()
+    monkeypatch.setenv("DMX_RETAIN_MB", "64")
+
+    def call(inp, outs, untrimmed):
+        with nio.Reader(inp, 64 << 10, threads=4) as r:
+            cap, keep = cli.retain_plan(outs, untrimmed, r.in_memory, True)
+            s = nio.Sink(outs, False, 1, threads=4, retain_bytes=cap)
+            for o, k in enumerate(keep):
+                if cap and not k:
+                    s.retain_output(o, False)
+            sizes = np.zeros(len(outs), np.int64)
+            for b in r:
+                k = len(b)
+                idx = (np.arange(k) % len(outs)).astype(np.int32)
+                for o in range(len(outs)):
+                    sel = idx == o
+                    sizes[o] += sum(len(b.header(i)) + 2 * int(b.lens[i]) + 6
+                                    for i in np.nonzero(sel)[0])
+                s.write(b, idx, np.zeros(k, np.int32), b.lens.astype(np.int32),
+                        np.zeros(k, np.uint8), np.zeros(k, np.uint8))
+                b.free()
+            s.close()
+            return cap, keep, sizes, r.in_memory
+
+    cap, keep, sizes, mem = call(str(src), r1, 2)          # round 1
+    assert cap == 64 << 20 and keep == [True, True, False] and not mem
+    held = nio.retained_bytes() - base
+    assert held == sizes[0] + sizes[1]                       # the unknown bin is not held
+    r2 = [str(tmp_path / f"SP27_{i}.fastq.gz") for i in range(3)]
+    cap, keep, _, mem = call(r1[0], r2, 2)                   # round 2 reads SP5_0 from memory
+    assert mem and cap == 0 and keep == [False] * 3
+    assert nio.retained_bytes() - base == sizes[1]           # SP5_0 dropped, nothing new held
+    nio.drop_retained()
+    assert nio.retained_bytes() == base
+    # outside the resident server nothing is retained; DMX_RETAIN_MB=0 disables
+    assert cli.retain_plan(r1, 2, False, False)[0] == 0
+    monkeypatch.setenv("DMX_RETAIN_MB", "0")
+    assert cli.retain_plan(r1, 2, False, True)[0] == 0
+
+
+def test_default_retain_cap_follows_available_memory(monkeypatch):
+    monkeypatch.delenv("DMX_RETAIN_MB", raising=False)
+    monkeypatch.setattr(nio, "available_memory_bytes", lambda: 4 << 30)   # e.g. --mem=4G
+    assert nio.default_retain_bytes() == 1 << 30
+    monkeypatch.setattr(nio, "available_memory_bytes", lambda: 1 << 40)
+    assert nio.default_retain_bytes() == 8 << 30
+    monkeypatch.setattr(nio, "available_memory_bytes", lambda: None)
+    assert nio.default_retain_bytes() == 0
+    monkeypatch.setenv("DMX_RETAIN_MB", "100")
+    assert nio.default_retain_bytes() == 100 << 20
+    monkeypatch.undo()
+    avail = nio.available_memory_bytes()      # this container: MemAvailable and/or the cgroup
+    assert avail is None or avail > 0
+
+
+# ---------------------------------------------------------------------------------------------
+# Parallel inflate of ordinary (unsized) gzip streams (csrc/dmx_inflate.h, ParGzSource): the
+# input of 02_cutadapt_loop.sh is a single-member `pychopped_<ds>.gz` (:15,28-34,71).  Output
+# must be byte-identical to zlib's inflate for stored, fixed and dynamic blocks, several members
+# (members straddling chunk edges, empty members, zero padding), every header field, and chunk
+# sizes small enough to put dozens of chunk edges into a few MB; corrupt input must fail.
+
+def _inflate(data, threads, cap=None):
+    import ctypes
+    L = nio.load()
+    cap = cap if cap is not None else max(1024, len(data) * 30 + (8 << 20))
+    out = np.empty(cap, np.uint8)
+    n = ctypes.c_size_t()
+    r = L.dmx_io_inflate(data, len(data), threads, out.ctypes.data, cap, ctypes.byref(n))
+    return r, out[:n.value].tobytes()
+
+
+def _zcompress(text, level=6, strategy=0, sync_every=0, wbits=31):
+    c = zlib.compressobj(level, zlib.DEFLATED, wbits, 9, strategy)
+    if not sync_every:
+        return c.compress(text) + c.flush()
+    parts = []
+    for i in range(0, len(text), sync_every):
+        parts.append(c.compress(text[i:i + sync_every]))
+        parts.append(c.flush(zlib.Z_SYNC_FLUSH if (i // sync_every) % 2 else zlib.Z_FULL_FLUSH))
+    parts.append(c.flush())
+    return b"".join(parts)
+
+
+def _gzip_with_header_fields(text):
+    """A member with FTEXT, FHCRC, FEXTRA, FNAME and FCOMMENT set (RFC 1952)."""
+    import struct
+    raw = zlib.compressobj(6, zlib.DEFLATED, -15)
+    body = raw.compress(text) + raw.flush()
+    extra = b"AB" + struct.pack("<H", 3) + b"xyz"
+    hdr = bytes([0x1f, 0x8b, 8, 1 | 2 | 4 | 8 | 16, 0, 0, 0, 0, 0, 3])
+    hdr += struct.pack("<H", len(extra)) + extra + b"name.fq\0" + b"a comment\0"
+    hdr += struct.pack("<H", zlib.crc32(hdr) & 0xFFFF)
+    return hdr + body + struct.pack("<II", zlib.crc32(text), len(text) & 0xFFFFFFFF)
+
+
+@pytest.fixture(scope="module")
+def fq_text():
+    return _records(6000, seed=11)[1].encode()
+
+
+@pytest.mark.parametrize("chunk_kb", ["16", "64", "4096"])
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_parallel_inflate_single_member_levels(fq_text, monkeypatch, chunk_kb, threads):
+    monkeypatch.setenv("DMX_INFLATE_CHUNK_KB", chunk_kb)
+    for level in (1, 6, 9):
+        gz = gzip.compress(fq_text, compresslevel=level)
+        r, out = _inflate(gz, threads)
+        assert r == 0 and out == fq_text, (level, r, len(out))
+
+
+@pytest.mark.parametrize("kind", ["fixed", "stored", "huffman", "rle", "sync", "random_bytes",
+                                  "header_fields", "text_mixed"])
+def test_parallel_inflate_block_kinds(fq_text, monkeypatch, kind):
+    monkeypatch.setenv("DMX_INFLATE_CHUNK_KB", "16")
+    text = fq_text
+    if kind == "fixed":
+        gz = _zcompress(text, 6, zlib.Z_FIXED)
+    elif kind == "stored":
+        gz = _zcompress(text, 0)
+    elif kind == "huffman":
+        gz = _zcompress(text, 6, zlib.Z_HUFFMAN_ONLY)
+    elif kind == "rle":
+        gz = _zcompress(text, 6, zlib.Z_RLE)
+    elif kind == "sync":             # empty stored blocks (sync / full flush) every 50 KB
+        gz = _zcompress(text, 6, 0, sync_every=50000)
+    elif kind == "random_bytes":     # incompressible: zlib falls back to stored blocks
+        text = np.random.default_rng(3).integers(0, 256, 600000, dtype=np.uint8).tobytes()
+        text = text + fq_text[:300000] + text[:100000]
+        gz = _zcompress(text, 6)
+    elif kind == "header_fields":
+        gz = _gzip_with_header_fields(text)
+    else:                            # long repeats (distances up to 32 KiB, lengths 258)
+        rep = fq_text[:40000]
+        text = rep * 8 + fq_text + b"A" * 100000 + rep
+        gz = _zcompress(text, 9)
+    assert gzip.decompress(gz) == text
+    for threads in (1, 4, 8):
+        r, out = _inflate(gz, threads)
+        assert r == 0 and out == text, (kind, threads, r, len(out), len(text))
+
+
+@pytest.mark.parametrize("threads", [1, 5])
+def test_parallel_inflate_members_straddle_chunks(fq_text, monkeypatch, threads):
+    """Unsized members of random sizes (empty ones too), some separated by zero padding, so
+    member boundaries fall anywhere relative to the 16 KiB chunk edges."""
+    monkeypatch.setenv("DMX_INFLATE_CHUNK_KB", "16")
+    rng = np.random.default_rng(9)
+    cuts = np.sort(rng.integers(0, len(fq_text), 40))
+    pieces = np.split(np.frombuffer(fq_text, np.uint8), cuts)
+    gz = b""
+    for i, p in enumerate(pieces + [np.zeros(0, np.uint8)]):
+        gz += gzip.compress(p.tobytes(), compresslevel=int(rng.integers(1, 10)))
+        if i % 7 == 3:
+            gz += b"\0" * int(rng.integers(1, 20))
+    r, out = _inflate(gz, threads)
+    assert r == 0 and out == fq_text
+
+
+def test_parallel_inflate_rejects_corrupt_input(fq_text, monkeypatch):
+    monkeypatch.setenv("DMX_INFLATE_CHUNK_KB", "16")
+    gz = bytearray(gzip.compress(fq_text, 6))
+    bad_crc = bytes(gz[:-8]) + bytes([gz[-8] ^ 1]) + bytes(gz[-7:])
+    bad_len = bytes(gz[:-4]) + bytes([gz[-4] ^ 1]) + bytes(gz[-3:])
+    for data in (bad_crc, bad_len, bytes(gz[:len(gz) // 2]), bytes(gz[:-3]),
+                 bytes(gz) + b"garbage!"):
+        for threads in (1, 6):
+            r, _ = _inflate(data, threads)
+            assert r == -2, (threads, len(data))
+    flipped = bytearray(gz)                    # a flipped bit inside the data
+    flipped[len(gz) // 3] ^= 0x10
+    for threads in (1, 6):
+        assert _inflate(bytes(flipped), threads)[0] == -2
+    # too small an output buffer is reported as such
+    assert _inflate(bytes(gz), 4, cap=len(fq_text) - 1)[0] == -3
+    # empty input and an empty member
+    assert _inflate(b"", 4) == (0, b"")
+    assert _inflate(gzip.compress(b""), 4) == (0, b"")
+
+
+def test_reader_single_member_gzip_records(tmp_path, monkeypatch):
+    """The reader's records from a Python-gzip single-member file equal the plain file's, with
+    chunk edges every 16 KiB (parallel inflate) and with DMX_SEQ_INFLATE=1 (zlib)."""
+    recs, text = _records(5000, seed=12)
+    plain = tmp_path / "r.fastq"
+    plain.write_text(text)
+    gz = tmp_path / "r.fastq.gz"
+    gz.write_bytes(gzip.compress(text.encode(), 6))
+
+    def read_all(path):
+        got = []
+        with nio.Reader(str(path), 256 << 10, threads=4) as r:
+            for b in r:
+                got += [(b.header(i), b.sequence(i), b.quality(i)) for i in range(len(b))]
+                b.free()
+        return got
+    ref = read_all(plain)
+    monkeypatch.setenv("DMX_INFLATE_CHUNK_KB", "16")
+    assert read_all(gz) == ref
+    monkeypatch.setenv("DMX_SEQ_INFLATE", "1")
+    assert read_all(gz) == ref

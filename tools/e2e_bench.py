@@ -6,7 +6,8 @@ workload (default c2: 12x12 panel, lognormal ~1.2 kb) with random qualities, wri
 FASTQ.gz (level 1, parallel members, via libdmx_io), then times
   fused : bin/dmx-demux-loop IN       (one pass, both rounds; what 02_cutadapt_loop.sh leaves)
           on plain FASTQ (01_pychopper.sh:57 writes *_pass.fastq uncompressed), on our
-          multi-member .gz (parallel inflate) and on a single-member .gz (sequential inflate)
+          multi-member .gz (member-parallel inflate) and on an ordinary single-member .gz
+          (speculative chunk-parallel inflate; DMX_E2E_SEQ_A_B=1 adds zlib's sequential path)
   calls : the 13 bin/cutadapt calls of 02_cutadapt_loop.sh:64-103 (per-call drop-in)
   pychopper (--pychopper): bin/pychopper with 01_pychopper.sh:45-57's flags on the .gz input
 and prints one JSON line with reads/s for each.  Usage:
@@ -88,6 +89,12 @@ def main():
     ap.add_argument("--skip-fused", action="store_true")
     ap.add_argument("--pychopper", action="store_true")
     ap.add_argument("--workdir", default=None)
+    ap.add_argument("--single-level", type=int, default=1,
+                    help="zlib level of the single-member .gz (default strategy: LZ77 + "
+                         "dynamic Huffman blocks, as `gzip -N` writes)")
+    ap.add_argument("--calls-input", choices=["single", "members"], default="single",
+                    help="round-1 input of the 13 calls: the single-member .gz (what "
+                         "02_cutadapt_loop.sh reads, pychopped_<ds>.gz) or our multi-member .gz")
     a = ap.parse_args()
     wd = a.workdir or tempfile.mkdtemp(prefix="dmx_e2e_")
     pych = os.path.join(wd, "pychopped")
@@ -98,11 +105,12 @@ def main():
     gz = plain + ".gz"
     write_fastq(plain, d, seed=5)
     gzip_native(plain, gz, a.threads)
-    # a single-member gzip (Python gzip / pigz-like): only sequential inflate is possible
+    # an ordinary single-member gzip (`gzip -1`-like: LZ77 + dynamic blocks, no size fields):
+    # the reader inflates it in speculative parallel chunks (csrc/dmx_inflate.h)
     gz1 = os.path.join(wd, "single", "pychopped_e2e.fastq.gz")
     os.makedirs(os.path.dirname(gz1), exist_ok=True)
     with open(plain, "rb") as fi, open(gz1, "wb") as fo:
-        c = zlib.compressobj(1, zlib.DEFLATED, 31, 8, zlib.Z_HUFFMAN_ONLY)
+        c = zlib.compressobj(a.single_level, zlib.DEFLATED, 31, 8, zlib.Z_DEFAULT_STRATEGY)
         while True:
             chunk = fi.read(64 << 20)
             if not chunk:
@@ -129,13 +137,19 @@ def main():
         res["pychopper_gz_s"] = round(ps, 3)
         res["pychopper_gz_reads_per_s"] = round(a.reads / ps, 1)
         res["pychopper_report"] = p.stderr.strip().splitlines()[-1] if p.stderr.strip() else ""
-    for tag, path in ((() if a.skip_fused else (("fused_plain", plain),
-                                                  ("fused_gz_members", gz),
-                                                  ("fused_gz_single", gz1)))):
+    res["input_gz_single_bytes"] = os.path.getsize(gz1)
+    res["input_gz_single_level"] = a.single_level
+    fused = [("fused_plain", plain), ("fused_gz_members", gz), ("fused_gz_single", gz1)]
+    if os.environ.get("DMX_E2E_SEQ_A_B") == "1":   # the same file through zlib's sequential path
+        fused.append(("fused_gz_single_seq_inflate", gz1))
+    for tag, path in (() if a.skip_fused else fused):
         t = time.perf_counter()
+        fenv = dict(env, DMX_PROFILE_IO="1")
+        if tag.endswith("_seq_inflate"):
+            fenv["DMX_SEQ_INFLATE"] = "1"
         p = subprocess.run([os.path.join(PKG, "bin", "dmx-demux-loop"), path, "-j",
                             str(a.threads), "--outdir", os.path.join(wd, tag)], check=True,
-                           env=dict(env, DMX_PROFILE_IO="1"), stdout=subprocess.DEVNULL,
+                           env=fenv, stdout=subprocess.DEVNULL,
                            stderr=subprocess.PIPE, text=True)
         fs = time.perf_counter() - t
         res[f"{tag}_s"] = round(fs, 3)
@@ -165,7 +179,9 @@ def main():
         t = time.perf_counter()
         call([cli, "--action=trim", "-e", "0.1", "-j", j, "--rc",
               "-g", f"file:{panel.SP5_FASTA}", "-o", f"{out}/SP5/{{name}}_e2e.fastq.gz",
-              gz, f"--json={out}/SP5/cutadapt_SP5_e2e.json"])
+              gz1 if a.calls_input == "single" else gz,
+              f"--json={out}/SP5/cutadapt_SP5_e2e.json"])
+        res["calls_input"] = a.calls_input
         ids = sorted(os.path.basename(f)[:-len("_e2e.fastq.gz")]
                      for f in glob.glob(f"{out}/SP5/*_e2e.fastq.gz") if "unknown" not in f)
         for ident in ids:
