@@ -730,10 +730,19 @@ def main():
             cores, how = args.cpu_threads, f"--cpu-threads {args.cpu_threads}; detected: {how}"
         out["cpu_baseline"] = cpu_baseline(args.workload, cores, how)
     if rank == 0:
+        out["provenance"] = run_provenance()
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def run_provenance():
+    """Which code produced this line (tools/provenance.py: commit of the build, SHA-256 of the
+    loaded libraries and of the sources)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from provenance import provenance
+    return provenance()
 
 
 def chop_main(args, ctx, packed, tune, lengths, gen_s, world, rank, dist, on_gpu):

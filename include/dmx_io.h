@@ -51,7 +51,7 @@ typedef struct dmx_sink dmx_sink;
 
 int dmx_io_abi_version(void);
 /* One gzip member of src[0, n) in the writers' format (RFC 1952 with a "DX" size subfield;
- * level 1 = Huffman-only DEFLATE, other levels zlib): written to out (cap bytes, at least
+ * level 1 = Huffman-only DEFLATE, other levels libdeflate at that level): written to out (cap bytes, at least
  * 2 n + 4096), its length to *out_len.  0 on success, negative if cap is too small. */
 int dmx_io_gzip(const uint8_t* src, size_t n, int level, uint8_t* out, size_t cap,
                 size_t* out_len);
@@ -93,6 +93,23 @@ int dmx_sink_write(dmx_sink* s, dmx_batch* b, const int32_t* out_idx, const int3
 int dmx_sink_write_rows(dmx_sink* s, dmx_batch* b, size_t n_rows, const uint32_t* read,
                         const int32_t* out_idx, const int32_t* start, const int32_t* stop,
                         const uint8_t* rc, const uint8_t* name_mode);
+/* Rows named as segments with their own " rc" suffixes (the fused 01 -> 02 loop): row r writes
+ * read[r][start[r]:stop[r]] (reverse-complemented if rc[r]) named
+ * "{name_start}:{name_stop}|{id} strand=+|-{comment}" (strand from name_strand) followed by
+ * n_rc[r] x " rc".  Asynchronous like dmx_sink_write. */
+int dmx_sink_write_rows2(dmx_sink* s, dmx_batch* b, size_t n_rows, const uint32_t* read,
+                         const int32_t* out_idx, const int32_t* start, const int32_t* stop,
+                         const uint8_t* rc, const int32_t* name_start, const int32_t* name_stop,
+                         const uint8_t* name_strand, const uint8_t* n_rc);
+/* Pack views of a batch's reads into the libdmx device layout (include/dmx.h, as dmx_pack
+ * lays out reads): view i = read[i][start[i]:stop[i]], reverse-complemented if rc[i] — the
+ * records pychopper writes for segments (scripts/01_pychopper.sh) handed to the demultiplexer
+ * without rendering or re-reading them.  n_words >= dmx_pack_words(sum of lengths, n_views).
+ * 0 = OK, -2 = a view outside its read, -3 = n_words too small. */
+int dmx_batch_pack_views(const dmx_batch* b, size_t n_views, const uint32_t* read,
+                         const int32_t* start, const int32_t* stop, const uint8_t* rc,
+                         int threads, uint32_t* out_seq2b, uint32_t* out_nmask,
+                         uint64_t* out_offsets, uint32_t* out_lens, size_t n_words);
 int dmx_sink_close(dmx_sink* s, uint64_t* n_written, uint64_t* bp_written);
 const char* dmx_sink_error(dmx_sink* s);
 

@@ -51,6 +51,12 @@ void libdeflate_free_decompressor(libdeflate_decompressor* d);
 int libdeflate_deflate_decompress(libdeflate_decompressor* d, const void* in, size_t in_nbytes,
                                   void* out, size_t out_nbytes_avail, size_t* actual_out_nbytes);
 uint32_t libdeflate_crc32(uint32_t crc, const void* buffer, size_t len);
+struct libdeflate_compressor;
+libdeflate_compressor* libdeflate_alloc_compressor(int compression_level);
+size_t libdeflate_deflate_compress(libdeflate_compressor* c, const void* in, size_t in_nbytes,
+                                   void* out, size_t out_nbytes_avail);
+size_t libdeflate_deflate_compress_bound(libdeflate_compressor* c, size_t in_nbytes);
+void libdeflate_free_compressor(libdeflate_compressor* c);
 }
 
 namespace {
@@ -1597,6 +1603,10 @@ struct Job {
     bool rows = false;
     std::vector<uint32_t> rread;
     std::vector<uint8_t> mode;
+    // mode 2 (dmx_sink_write_rows2): the name is the segment's "{ns}:{ne}|{id} strand=..." of
+    // (nstart, nstop, nstrand) followed by nrc " rc" suffixes; start/stop/rc give the sequence
+    std::vector<int32_t> nstart, nstop;
+    std::vector<uint8_t> nstrand;
 };
 
 inline uint32_t ndigits(uint32_t v) {
@@ -1631,10 +1641,11 @@ inline void put32(uint8_t* p, uint32_t v) {
 // One gzip member (RFC 1952) whose header carries a "DX" extra subfield with the member's
 // compressed and uncompressed size, so that our reader (and any reader that skips unknown
 // subfields, i.e. all of them) can find member boundaries and inflate members in parallel.
-// Level 1 is Huffman-only deflate: on FASTQ (2-bit-entropy bases, skewed qualities) zlib's
-// level-1 LZ77 finds little and costs most of the time — zlib's Huffman-only strategy measured
-// 2.6x faster and 4 % smaller here, and the table-driven encoder of dmx_deflate.h is several
-// times faster again (same kind of stream).  Other levels use zlib.  Appends to `out`.
+// Level 1 (`-Z`) is Huffman-only deflate: on FASTQ (2-bit-entropy bases, skewed qualities)
+// zlib's level-1 LZ77 finds little and costs most of the time — zlib's Huffman-only strategy
+// measured 2.6x faster and 4 % smaller here, and the table-driven encoder of dmx_deflate.h is
+// several times faster again (same kind of stream).  Other levels use libdeflate.  Appends to
+// `out`.
 bool gzip_member(const uint8_t* src, size_t n, int level, Bytes& out) {
     if (level == 1) {
         const size_t base = out.size();
@@ -1656,27 +1667,34 @@ bool gzip_member(const uint8_t* src, size_t n, int level, Bytes& out) {
         out.resize(base + total);
         return true;
     }
-    z_stream zs{};
-    const int strategy = level == 1 ? Z_HUFFMAN_ONLY : Z_DEFAULT_STRATEGY;
-    if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, strategy) != Z_OK) return false;
+    // other levels: libdeflate's compressor at the same level (one per thread and level);
+    // its output at a zlib level is about zlib's size at that level, at several times zlib's
+    // speed.  cutadapt's default is level 5 (dmx/cli.py --compression-level).
+    struct Comp {
+        libdeflate_compressor* c[13] = {nullptr};
+        ~Comp() {
+            for (auto* x : c)
+                if (x) libdeflate_free_compressor(x);
+        }
+    };
+    thread_local Comp comp;
+    if (level < 0 || level > 12) return false;
+    if (!comp.c[level]) comp.c[level] = libdeflate_alloc_compressor(level);
+    libdeflate_compressor* lc = comp.c[level];
+    if (!lc) return false;
     const size_t base = out.size();
     const size_t hdr = 24;
-    out.resize(base + hdr + deflateBound(&zs, (uLong)n) + 16);
+    const size_t bound = libdeflate_deflate_compress_bound(lc, n);
+    out.resize(base + hdr + bound + 16);
     uint8_t* h = out.data() + base;
-    const uint8_t fixed[12] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, (uint8_t)(level == 1 ? 4 : level == 9 ? 2 : 0), 3, 12, 0};
+    const uint8_t fixed[12] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, (uint8_t)(level >= 9 ? 2 : 0), 3, 12, 0};
     memcpy(h, fixed, 12);
     h[12] = 'D';
     h[13] = 'X';
     h[14] = 8;
     h[15] = 0;
-    zs.next_in = const_cast<uint8_t*>(src);
-    zs.avail_in = (uInt)n;
-    zs.next_out = h + hdr;
-    zs.avail_out = (uInt)(out.size() - base - hdr);
-    const int ret = deflate(&zs, Z_FINISH);
-    const size_t clen = zs.total_out;
-    deflateEnd(&zs);
-    if (ret != Z_STREAM_END) return false;
+    const size_t clen = libdeflate_deflate_compress(lc, src, n, h + hdr, bound);
+    if (clen == 0) return false;
     const size_t total = hdr + clen + 8;
     put32(h + 16, (uint32_t)total);
     put32(h + 20, (uint32_t)n);
@@ -1740,9 +1758,18 @@ bool dmx_sink::process(Job& j, std::string& e) {
             }
             const uint64_t L = (uint64_t)(j.stop[r] - j.start[r]);
             const uint64_t hl = b->head_v[2 * ri + 1] - b->head_v[2 * ri];
+            if (j.rows && j.mode[r] == 2 &&
+                (j.nstart[r] < 0 || j.nstop[r] < j.nstart[r] ||
+                 (uint32_t)j.nstop[r] > b->lens_v[ri])) {
+                range_bad = true;
+                continue;
+            }
             const uint64_t h = (j.rows && j.mode[r] == 1)
                                    ? hl + ndigits((uint32_t)j.start[r]) +
                                          ndigits((uint32_t)j.stop[r]) + 2 + 9
+                               : (j.rows && j.mode[r] == 2)
+                                   ? hl + ndigits((uint32_t)j.nstart[r]) +
+                                         ndigits((uint32_t)j.nstop[r]) + 2 + 9 + 3ull * j.nrc[r]
                                    : hl + 3ull * j.nrc[r];
             sz[t][o] += 1 + h + 1 + L + 1 + (fq ? 2 + L + 1 : 0);
             cnt[t][o] += 1;
@@ -1771,19 +1798,25 @@ bool dmx_sink::process(Job& j, std::string& e) {
             uint8_t* p = w[o];
             *p++ = fq ? '@' : '>';
             const uint64_t hs = b->head_v[2 * ri], he = b->head_v[2 * ri + 1];
-            if (j.rows && j.mode[r] == 1) {   // segment of a read: "start:stop|id strand=+ ..."
-                p = put_u32(p, (uint32_t)j.start[r]);
+            if (j.rows && j.mode[r] >= 1) {   // segment of a read: "start:stop|id strand=+ ..."
+                const bool m2 = j.mode[r] == 2;
+                p = put_u32(p, (uint32_t)(m2 ? j.nstart[r] : j.start[r]));
                 *p++ = ':';
-                p = put_u32(p, (uint32_t)j.stop[r]);
+                p = put_u32(p, (uint32_t)(m2 ? j.nstop[r] : j.stop[r]));
                 *p++ = '|';
                 uint64_t cut = hs;
                 while (cut < he && tx[cut] != ' ' && tx[cut] != '\t') ++cut;
                 memcpy(p, tx + hs, cut - hs);
                 p += cut - hs;
-                memcpy(p, j.rc[r] ? " strand=-" : " strand=+", 9);
+                memcpy(p, (m2 ? j.nstrand[r] : j.rc[r]) ? " strand=-" : " strand=+", 9);
                 p += 9;
                 memcpy(p, tx + cut, he - cut);
                 p += he - cut;
+                if (m2)
+                    for (int k = 0; k < j.nrc[r]; ++k) {
+                        memcpy(p, " rc", 3);
+                        p += 3;
+                    }
             } else {
                 memcpy(p, tx + hs, he - hs);
                 p += he - hs;
@@ -2014,8 +2047,70 @@ int dmx_sink_write_rows(dmx_sink* s, dmx_batch* bp, size_t n_rows, const uint32_
     j->stop.assign(stop, stop + n_rows);
     j->rc.assign(rc, rc + n_rows);
     j->mode.assign(name_mode, name_mode + n_rows);
+    for (uint8_t m : j->mode)
+        if (m > 1) return -1;   // mode 2 needs the segment names (dmx_sink_write_rows2)
     j->nrc.assign(n_rows, 0);
     return sink_enqueue(s, b, std::move(j));
+}
+
+int dmx_sink_write_rows2(dmx_sink* s, dmx_batch* bp, size_t n_rows, const uint32_t* read,
+                         const int32_t* out_idx, const int32_t* start, const int32_t* stop,
+                         const uint8_t* rc, const int32_t* name_start, const int32_t* name_stop,
+                         const uint8_t* name_strand, const uint8_t* n_rc) {
+    if (!s || !bp || s->closed || !s->th.joinable()) return -1;
+    if (n_rows && (!read || !out_idx || !start || !stop || !rc || !name_start || !name_stop ||
+                   !name_strand || !n_rc))
+        return -1;
+    Batch* b = static_cast<Batch*>(bp);
+    auto j = std::make_unique<Job>();
+    j->rows = true;
+    j->rread.assign(read, read + n_rows);
+    j->idx.assign(out_idx, out_idx + n_rows);
+    j->start.assign(start, start + n_rows);
+    j->stop.assign(stop, stop + n_rows);
+    j->rc.assign(rc, rc + n_rows);
+    j->mode.assign(n_rows, 2);
+    j->nstart.assign(name_start, name_start + n_rows);
+    j->nstop.assign(name_stop, name_stop + n_rows);
+    j->nstrand.assign(name_strand, name_strand + n_rows);
+    j->nrc.assign(n_rc, n_rc + n_rows);
+    return sink_enqueue(s, b, std::move(j));
+}
+
+int dmx_batch_pack_views(const dmx_batch* bp, size_t n_views, const uint32_t* read,
+                         const int32_t* start, const int32_t* stop, const uint8_t* rc,
+                         int threads, uint32_t* out_seq2b, uint32_t* out_nmask,
+                         uint64_t* out_offsets, uint32_t* out_lens, size_t n_words) {
+    if (!bp || (n_views && (!read || !start || !stop || !rc || !out_offsets || !out_lens)) ||
+        !out_seq2b || !out_nmask)
+        return -1;
+    const Batch* b = static_cast<const Batch*>(bp);
+    uint64_t g = kPad, total = 0;
+    for (size_t i = 0; i < n_views; ++i) {
+        if (read[i] >= b->n_reads || start[i] < 0 || stop[i] < start[i] ||
+            (uint32_t)stop[i] > b->lens_v[read[i]])
+            return -2;
+        out_offsets[i] = g;
+        out_lens[i] = (uint32_t)(stop[i] - start[i]);
+        g += ((uint64_t)out_lens[i] + dmx::kPackAlign - 1) / dmx::kPackAlign * dmx::kPackAlign;
+        total += out_lens[i];
+    }
+    // the same word count as dmx_pack_words(total, n_views) (include/dmx.h)
+    const uint64_t nt = 2 * kPad + total + (uint64_t)dmx::kPackAlign * n_views;
+    if (n_words < (size_t)((nt + 31) / 32 * 2 + 4)) return -3;
+    memset(out_seq2b, 0, n_words * sizeof(uint32_t));
+    memset(out_nmask, 0, n_words * sizeof(uint32_t));
+    const uint8_t* st = b->fasta ? b->seqtext_v.data() : b->text_v.data();
+    const int nth = (int)std::min<size_t>(clamp_threads(threads), std::max<size_t>(1, n_views / 1024));
+    parallel(nth, [&](int t) {
+        const size_t lo = n_views * t / nth, hi = n_views * (t + 1) / nth;
+        for (size_t i = lo; i < hi; ++i) {
+            const uint8_t* src = st + b->seq_v[2 * read[i]] + start[i];
+            if (rc[i]) dmx::pack_one_rc(src, out_lens[i], out_offsets[i], out_seq2b, out_nmask);
+            else dmx::pack_one(src, out_lens[i], out_offsets[i], out_seq2b, out_nmask);
+        }
+    });
+    return 0;
 }
 
 int dmx_batch_mean_qual(const dmx_batch* bp, double* out) {

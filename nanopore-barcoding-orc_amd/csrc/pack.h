@@ -56,6 +56,31 @@ inline void pack_one(const uint8_t* src, uint32_t n, uint64_t g0, uint32_t* seq,
     }
 }
 
+// The reverse complement of the n nt at src, packed like pack_one: nt y is the complement of
+// src[n - 1 - y] (code ^ 3: A<->T, C<->G); a non-ACGT byte stays no-match (code 0, mask bit),
+// exactly what pack_one gives for the reverse-complemented text.
+inline void pack_one_rc(const uint8_t* src, uint32_t n, uint64_t g0, uint32_t* seq,
+                        uint32_t* nmask) {
+    const PackTables& T = pack_tables();
+    uint32_t* sw = seq + g0 / 16;
+    uint32_t* nw = nmask + g0 / 32;
+    for (uint32_t x = 0; x < n; x += 32) {
+        const uint32_t cnt = n - x < 32u ? n - x : 32u;
+        uint32_t w0 = 0, w1 = 0, nb = 0;
+        for (uint32_t y = 0; y < cnt; ++y) {
+            const uint8_t ch = src[n - 1 - (x + y)];
+            const uint32_t nf = T.nflag[ch];
+            const uint32_t cd = nf ? 0u : (T.code[ch] ^ 3u);
+            if (y < 16) w0 |= cd << (2 * y);
+            else w1 |= cd << (2 * (y - 16));
+            nb |= nf << y;
+        }
+        sw[x / 16] = w0;
+        sw[x / 16 + 1] = w1;
+        nw[x / 32] = nb;
+    }
+}
+
 inline void pack_range(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens,
                        size_t lo, size_t hi, const uint64_t* out_offsets, uint32_t* seq,
                        uint32_t* nmask) {

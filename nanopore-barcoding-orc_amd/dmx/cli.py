@@ -54,8 +54,12 @@ def build_parser():
     p.add_argument("--discard-untrimmed", "--trimmed-only", dest="discard_untrimmed",
                    action="store_true")
     p.add_argument("--json")
+    # cutadapt 4.9: --compression-level defaults to 5; -Z selects level 1 (here Huffman-only
+    # DEFLATE, the fastest stream any inflater reads).  DMX_COMPRESSION_LEVEL changes the
+    # default for an unchanged calling script.
     p.add_argument("-Z", dest="zlevel1", action="store_true")
-    p.add_argument("--compression-level", type=int, default=1)
+    p.add_argument("--compression-level", type=int,
+                   default=int(os.environ.get("DMX_COMPRESSION_LEVEL", "5") or 5))
     p.add_argument("--quiet", action="store_true")
     p.add_argument("--report", default="full")
     p.add_argument("--no-indels", action="store_true")

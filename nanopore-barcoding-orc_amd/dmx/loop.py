@@ -1,4 +1,5 @@
-"""Fused replacement for scripts/02_cutadapt_loop.sh: both demultiplexing rounds in one pass.
+"""Fused replacement for scripts/02_cutadapt_loop.sh: both demultiplexing rounds in one pass
+(and, with --reorient, scripts/01_pychopper.sh's pychopper step in front of them).
 
 The reference runs cutadapt 13 times per sample (round 1 `-g file:SP5 --rc` at :64-72, then one
 `-a file:SP27rc --rc` call per SP5 bin at :91-103), re-reading and re-compressing every read,
@@ -12,7 +13,12 @@ view of every read, no host round trip) and writes the files the script leaves b
   demuxed/SP27/{SP5_i}_{dataset}.json               round-2 report per SP5 bin (:102)
 
 with the same record content and order as the 13 cutadapt calls (tests/test_cli_gpu.py checks
-it against the per-call CLI and the oracle).  `--no-cleanup` also writes the `unknown` and
+it against the per-call CLI and the oracle).  `--reorient` takes the RAW reads instead: per
+batch it finds the primer segments on the GPU (bin/pychopper's semantics, dmx/chop.py), writes
+pychopper's outputs (pychopped/<base>_{pass,rescued,unclass,short}.fastq, <base>_stats.out;
+01_pychopper.sh:45-57) and demultiplexes the PASS records straight from the resident batch —
+packed from the batch as oriented views (dmx_batch_pack_views), never written and read back —
+with the same outputs as bin/pychopper followed by this loop on its PASS file.  `--no-cleanup` also writes the `unknown` and
 SP27_009..012 files the script deletes.  Options mirror the script's variables (e_rate,
 threads, adapter FASTAs); GPUs as in the CLI (DMX_GPUS / DMX_DEVICE, default all visible).
 """
@@ -55,10 +61,50 @@ def build_parser():
     p.add_argument("--outdir", default=None, help="default: $(dirname $(dirname IN))/demuxed")
     p.add_argument("--no-cleanup", action="store_true",
                    help="keep the unknown and SP27_009..012 outputs (:107-119 delete them)")
-    p.add_argument("--compression-level", type=int, default=1)
+    # cutadapt's defaults (the script's calls pass neither): level 5; -Z = level 1
+    p.add_argument("--compression-level", type=int,
+                   default=int(os.environ.get("DMX_COMPRESSION_LEVEL", "5") or 5))
+    p.add_argument("-Z", dest="zlevel1", action="store_true")
     p.add_argument("--batch-mb", type=int, default=int(os.environ.get("DMX_BATCH_MB", "256")))
     p.add_argument("--device", type=int, default=None)
+    # 01 -> 02 fused: INFILE is the raw reads; reorient them as 01_pychopper.sh does, write its
+    # outputs, and demultiplex its PASS records straight from the resident batch
+    p.add_argument("--reorient", action="store_true",
+                   help="INFILE = raw reads: run 01_pychopper.sh's pychopper step first (its "
+                        "outputs in --pychopper-dir) and demultiplex its PASS records")
+    p.add_argument("--pychopper-dir", default=None, help="default: $(dirname IN)/pychopped")
+    p.add_argument("--primers", default=None, help="pychopper -b (M13_seqs_for_pychopper.fa)")
+    p.add_argument("--layout", default=None, help="pychopper -c (M13_config_for_pychopper.txt)")
+    p.add_argument("-Q", dest="min_qual", type=float, default=10.0, help="pychopper -Q (:17)")
+    p.add_argument("-z", dest="min_len", type=int, default=50, help="pychopper -z")
+    p.add_argument("-q", dest="cutoff", type=float, default=None, help="pychopper -q")
+    p.add_argument("-Y", dest="autotune_n", type=int, default=10000, help="pychopper -Y")
+    p.add_argument("-L", dest="autotune_samples", type=int, default=None, help="pychopper -L")
+    p.add_argument("--no-keep-primers", action="store_true", help="pychopper without -p")
     return p
+
+
+def view_coords(vs, ve, vst, a, b, o):
+    """Sub-range [a, b) of orient(P, o), P = orient(read[vs:ve], vst) (a pychopper segment), as
+    (start, stop, orientation) on the read itself: with t = vst ^ o, orient(read[vs:ve], t)[a:b]
+    is read[vs + a : vs + b] (t = 0) or the reverse complement of read[ve - b : ve - a]."""
+    t = (vst.astype(np.uint8) ^ o.astype(np.uint8)).astype(np.uint8)
+    vs, ve = vs.astype(np.int64), ve.astype(np.int64)
+    a, b = a.astype(np.int64), b.astype(np.int64)
+    return np.where(t == 1, ve - b, vs + a), np.where(t == 1, ve - a, vs + b), t
+
+
+def base_name(infile: str) -> str:
+    """01_pychopper.sh:21-26: the input's file name without .gz, then .fastq / .fq."""
+    b = os.path.basename(infile)
+    for suf in (".gz",):
+        if b.endswith(suf):
+            b = b[:-len(suf)]
+    for suf in (".fastq", ".fq"):
+        if b.endswith(suf):
+            b = b[:-len(suf)]
+            break
+    return b
 
 
 def plan_rounds(res, lens):
@@ -83,15 +129,29 @@ def run(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     args = build_parser().parse_args(argv)
     infile = args.infile
-    ds = dataset_name(infile)
-    outdir = args.outdir or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(infile))),
-                                         "demuxed")
+    if args.reorient:   # 01_pychopper.sh:21-31 names; 02 reads pychopped/pychopped_<base>
+        base = base_name(infile)
+        pych_dir = args.pychopper_dir or os.path.join(os.path.dirname(os.path.abspath(infile)),
+                                                      "pychopped")
+        ds = base
+        demux_in = os.path.join(pych_dir, f"pychopped_{base}.gz")
+    else:
+        ds = dataset_name(infile)
+        demux_in = infile
+    outdir = args.outdir or os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(demux_in))), "demuxed")
     print("=========================================")
     print(f"Processing: {infile}")
     print(f"Dataset name: {ds}")
     print(f"Output directory: {outdir}")
     print("=========================================")
-    for f in (infile, args.sp5, args.sp27):
+    chop_files = ()
+    if args.reorient:
+        from . import chop
+        args.primers = args.primers or chop.PRIMERS_FASTA
+        args.layout = args.layout or chop.CONFIG_FILE
+        chop_files = (args.primers, args.layout)
+    for f in (infile, args.sp5, args.sp27) + chop_files:
         if not os.path.isfile(f):
             print(f"Error: Required file not found: {f}")
             return 1
@@ -131,11 +191,15 @@ def run(argv=None) -> int:
         s = Stats(ads2)
         s.rc_mode = True
         st2.append(s)
+    reo = None
+    if args.reorient:
+        reo = Reorienter(args, pych_dir, base)
     t0 = time.perf_counter()
     print("Round 1: Demultiplexing with SP5 adapters...")
     print("Round 2: Demultiplexing with SP27 adapters (fused with round 1)...")
-    sink1 = nio.Sink(p1, False, args.compression_level, threads=args.threads)
-    sink2 = nio.Sink(p2, False, args.compression_level, threads=args.threads)
+    level = 1 if args.zlevel1 else args.compression_level
+    sink1 = nio.Sink(p1, False, level, threads=args.threads)
+    sink2 = nio.Sink(p2, False, level, threads=args.threads)
     bp2_out = np.zeros(len(n1), np.int64)
     prof = dict(read_wait=0.0, gpu=0.0, plan_write=0.0, drain=0.0)
     n2_out = np.zeros(len(n1), np.int64)
@@ -152,11 +216,20 @@ def run(argv=None) -> int:
                     if not len(batch):
                         continue
                     tw = time.perf_counter()
-                    res, cnt = lib.run_batch(ctxs, batch.packed)
+                    views = None
+                    packed, lens = batch.packed, batch.lens
+                    if reo is not None:   # the PASS records of 01_pychopper.sh, as views
+                        views = reo.batch(batch)
+                        packed = batch.pack_views(views[0], views[1], views[2], views[3],
+                                                  threads=args.threads)
+                        lens = packed.lengths
+                        if not len(lens):
+                            continue
+                    res, cnt = lib.run_batch(ctxs, packed)
                     totals += lib.bin_totals(cnt, len(n1), len(n2))
                     prof["gpu"] += time.perf_counter() - tw
                     tw = time.perf_counter()
-                    (s1, e1, o1), (s2, e2, o2, nrc2) = plan_rounds(res, batch.lens)
+                    (s1, e1, o1), (s2, e2, o2, nrc2) = plan_rounds(res, lens)
                     b1 = res["bin1"].astype(np.int64)
                     b2 = res["bin2"].astype(np.int64)
                     m1 = b1 >= 0
@@ -164,7 +237,12 @@ def run(argv=None) -> int:
                     # unmatched in round 1 is written untrimmed to unknown (--no-cleanup only)
                     s1w = np.where(m1, s1, 0)
                     o1w = o1.astype(np.uint8)   # an unmatched read may still be taken RC'd
-                    sink1.write(batch, idx1, s1w, e1, o1w, o1w)
+                    if views is None:
+                        sink1.write(batch, idx1, s1w, e1, o1w, o1w)
+                    else:
+                        x, y, t = view_coords(views[1], views[2], views[3], s1w, e1, o1w)
+                        sink1.write_rows2(batch, views[0], idx1, x, y, t, views[1], views[2],
+                                          views[3], o1w)
                     idx2 = np.where(m1, out2[np.maximum(b1, 0), b2 + 1], -1)
                     # round-2 unknown: the round-1 output record, untrimmed by round 2
                     m2 = b2 >= 0
@@ -175,9 +253,14 @@ def run(argv=None) -> int:
                     e2w = np.where(m2, e2, np.where(u2rc, e1 - s1, e1))
                     o2w = np.where(m2, o2, np.where(u2rc, 1 - o1, o1)).astype(np.uint8)
                     n2w = np.where(m2, nrc2, o1 + u2rc).astype(np.uint8)
-                    sink2.write(batch, idx2, s2w, e2w, o2w, n2w)
-                    _round_stats(st1, st2, res, batch.lens, m1, m2, b1, b2, s1, s2w, e2w,
-                                 bp2_out, n2_out, batch.packed)
+                    if views is None:
+                        sink2.write(batch, idx2, s2w, e2w, o2w, n2w)
+                    else:
+                        x, y, t = view_coords(views[1], views[2], views[3], s2w, e2w, o2w)
+                        sink2.write_rows2(batch, views[0], idx2, x, y, t, views[1], views[2],
+                                          views[3], n2w)
+                    _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w,
+                                 bp2_out, n2_out, packed)
                     prof["plan_write"] += time.perf_counter() - tw
                 finally:
                     batch.free()
@@ -185,6 +268,8 @@ def run(argv=None) -> int:
         tw = time.perf_counter()
         sink1.close()
         sink2.close()
+        if reo is not None:
+            reo.close()
         prof["drain"] += time.perf_counter() - tw
     if os.environ.get("DMX_PROFILE_IO"):
         print("io profile (s): " + ", ".join(f"{k} {v:.3f}" for k, v in prof.items()),
@@ -198,7 +283,7 @@ def run(argv=None) -> int:
     for i, s in enumerate(st2):
         s.n_out, s.bp_out = int(n2_out[i]), int(bp2_out[i])
     st1.write_json(f"{outdir}/SP5/cutadapt_SP5_{ds}.json", argv=["dmx-demux-loop"] + argv,
-                   cores=args.threads, in_path=infile, error_rate=args.e_rate)
+                   cores=args.threads, in_path=demux_in, error_rate=args.e_rate)
     print(f"Found {len(n1)} identifiers from SP5 demultiplexing")
     for i, ident in enumerate(n1):
         st2[i].write_json(f"{outdir}/SP27/{ident}_{ds}.json",
@@ -212,6 +297,71 @@ def run(argv=None) -> int:
     print("Pipeline complete!")
     print(f"Results in: {outdir}")
     return 0
+
+
+class Reorienter:
+    """The pychopper step of 01_pychopper.sh:45-57 inside the fused loop (dmx/chop.py semantics,
+    its own device context): per batch, primer hits and segments on the GPU, pychopper's five
+    outputs written, and the PASS records (one segment, QC pass, >= -z nt) returned as views
+    (read, start, stop, strand) for the demultiplexer."""
+
+    def __init__(self, args, pych_dir: str, base: str):
+        from . import chop
+        self.chop = chop
+        self.args = args
+        os.makedirs(pych_dir, exist_ok=True)
+        primers = chop.load_primers(args.primers)
+        with open(args.layout) as fh:
+            rules = chop.parse_config(fh.read(), [p[0] for p in primers])
+        dev = args.device if args.device is not None else int(os.environ.get("DMX_DEVICE", "0")
+                                                               or 0)
+        self.ctx = lib.Context(dev)
+        self.ch = chop.Chopper(self.ctx, primers, rules, not args.no_keep_primers)
+        # 01_pychopper.sh:47-57: -w rescued, -u unclass, -l short, -S stats, PASS to stdout
+        self.paths = [os.path.join(pych_dir, f"{base}_{k}.fastq")
+                      for k in ("pass", "rescued", "unclass", "short")]
+        self.stats_path = os.path.join(pych_dir, f"{base}_stats.out")
+        self.outs = [0, 1, 2, 3, -1]   # PASS, RESCUED, UNCLASS, SHORT, QCFAIL (no -K)
+        self.sink = None
+        self.stats = chop.ChopStats()
+        self.cutoff = args.cutoff
+        self.t0 = time.perf_counter()
+
+    def batch(self, b):
+        chop, a = self.chop, self.args
+        if self.sink is None:
+            self.sink = nio.Sink(self.paths, b.fasta, 1, threads=a.threads)
+        n = len(b)
+        qc_ok = np.ones(n, dtype=bool) if b.fasta else b.mean_qual() >= a.min_qual
+        if self.cutoff is None:   # tuned on the first -Y QC-passing reads (bin/pychopper's rule)
+            self.ctx.load(chop.sample_packed(b.packed, np.nonzero(qc_ok)[0][:a.autotune_n]))
+            self.cutoff = self.ch.autotune(np.arange(self.ctx._n_loaded),
+                                           a.autotune_samples or chop.AUTOTUNE_SAMPLES)
+        self.ctx.load(b.packed)
+        self.ch.set_cutoff(self.cutoff)
+        nseg, segs = self.ch.run()
+        self.sink.write_rows(b, *chop.plan_rows(nseg, segs, b.lens, qc_ok, a.min_len, self.outs))
+        self.stats.add(nseg, segs, qc_ok, a.min_len)
+        sread = segs["read"].astype(np.int64)
+        sstart = segs["start"].astype(np.int64)
+        sstop = segs["stop"].astype(np.int64)
+        ok = (qc_ok[sread] & (nseg.astype(np.int64)[sread] == 1) & (sstop - sstart >= a.min_len))
+        # plan_rows's PASS rows, in read order (segments come in read order)
+        return (sread[ok].astype(np.uint32), sstart[ok].astype(np.int32),
+                sstop[ok].astype(np.int32), segs["strand"][ok].astype(np.uint8))
+
+    def close(self):
+        if self.sink is None:   # empty input: the outputs still exist
+            self.sink = nio.Sink(self.paths, False, 1, threads=self.args.threads)
+        self.sink.close()
+        self.stats.cutoff = self.cutoff
+        self.stats.write(self.stats_path)
+        s = self.stats
+        print(f"pychopper (dmx {__version__}, MI355X, fused): {s.n_in} reads in "
+              f"{time.perf_counter() - self.t0:.3f} s, cutoff {self.cutoff}: {s.n_found} with "
+              f"primers, {s.n_rescue} rescued, {s.n_unclass} unclassified, {s.n_qcfail} QC fail",
+              file=sys.stderr)
+        self.ctx.close()
 
 
 def _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w, bp2_out, n2_out,

@@ -23,7 +23,7 @@ IO_EXPORTS = ["dmx_io_abi_version", "dmx_reader_open", "dmx_reader_next", "dmx_r
               "dmx_sink_close", "dmx_sink_error", "dmx_sink_free", "dmx_sink_write_rows",
               "dmx_batch_mean_qual", "dmx_io_gzip", "dmx_sink_retain", "dmx_io_retained_bytes",
               "dmx_io_drop_retained", "dmx_sink_retain_output", "dmx_reader_in_memory",
-              "dmx_io_inflate"]
+              "dmx_io_inflate", "dmx_sink_write_rows2", "dmx_batch_pack_views"]
 
 
 class _CBatch(ctypes.Structure):
@@ -75,6 +75,9 @@ def load() -> ctypes.CDLL:
     L.dmx_reader_in_memory.restype = c_int
     L.dmx_io_inflate.argtypes = [ctypes.c_char_p, c_size, c_int, P, c_size, P]
     L.dmx_io_inflate.restype = c_int
+    L.dmx_sink_write_rows2.argtypes = [P, ctypes.POINTER(_CBatch), c_size] + [P] * 9
+    L.dmx_batch_pack_views.argtypes = [ctypes.POINTER(_CBatch), c_size, P, P, P, P, c_int,
+                                       P, P, P, P, c_size]
     if L.dmx_io_abi_version() != 1:
         raise DmxError("libdmx_io ABI mismatch")
     _io = L
@@ -142,6 +145,29 @@ class NativeBatch:
         if rc != 0:
             raise ValueError("mean quality needs FASTQ input")
         return out
+
+    def pack_views(self, read, start, stop, rc, threads: int = 0) -> Packed:
+        """Views read[i][start[i]:stop[i]] (reverse-complemented where rc[i]) packed into the
+        device layout as reads of their own (dmx_batch_pack_views): segments handed to the
+        demultiplexer without rendering them."""
+        from .lib import load as load_dmx
+        arrs = [np.ascontiguousarray(read, np.uint32), np.ascontiguousarray(start, np.int32),
+                np.ascontiguousarray(stop, np.int32), np.ascontiguousarray(rc, np.uint8)]
+        n = len(arrs[0])
+        if any(len(a) != n for a in arrs):
+            raise ValueError("view arrays must have equal lengths")
+        total = int((arrs[2].astype(np.int64) - arrs[1]).sum()) if n else 0
+        words = int(load_dmx().dmx_pack_words(total, n))
+        seq = np.empty(words, np.uint32)
+        nm = np.empty(words, np.uint32)
+        offs = np.empty(n, np.uint64)
+        lens = np.empty(n, np.uint32)
+        r = load().dmx_batch_pack_views(self._ptr, n, *[a.ctypes.data for a in arrs],
+                                        int(threads), seq.ctypes.data, nm.ctypes.data,
+                                        offs.ctypes.data, lens.ctypes.data, words)
+        if r != 0:
+            raise ValueError(f"dmx_batch_pack_views failed ({r})")
+        return Packed(seq, nm, offs, lens)
 
     def free(self):
         if self._ptr is not None:
@@ -304,6 +330,23 @@ class Sink:
         if any(len(a) != n for a in arrs):
             raise ValueError("row arrays must have equal lengths")
         r = self._L.dmx_sink_write_rows(self._h, batch._ptr, n, *[a.ctypes.data for a in arrs])
+        if r != 0:
+            raise OSError(self._L.dmx_sink_error(self._h).decode())
+
+    def write_rows2(self, batch: NativeBatch, read, out_idx, start, stop, rc, name_start,
+                    name_stop, name_strand, n_rc):
+        """Rows named as segments "{name_start}:{name_stop}|id strand=..." plus n_rc " rc"
+        suffixes (dmx_sink_write_rows2); the sequence is read[start:stop], reverse-complemented
+        if rc (positions on the read as given)."""
+        arrs = [np.ascontiguousarray(read, np.uint32), np.ascontiguousarray(out_idx, np.int32),
+                np.ascontiguousarray(start, np.int32), np.ascontiguousarray(stop, np.int32),
+                np.ascontiguousarray(rc, np.uint8), np.ascontiguousarray(name_start, np.int32),
+                np.ascontiguousarray(name_stop, np.int32),
+                np.ascontiguousarray(name_strand, np.uint8), np.ascontiguousarray(n_rc, np.uint8)]
+        n = len(arrs[0])
+        if any(len(a) != n for a in arrs):
+            raise ValueError("row arrays must have equal lengths")
+        r = self._L.dmx_sink_write_rows2(self._h, batch._ptr, n, *[a.ctypes.data for a in arrs])
         if r != 0:
             raise OSError(self._L.dmx_sink_error(self._h).decode())
 

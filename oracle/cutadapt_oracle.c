@@ -154,6 +154,12 @@ static int aligner_locate(const orc_aligner* al, const char* query, int n, int o
     }
 
     int best_ref_stop = m, best_query_stop = n, best_cost = m + n + 1, best_origin = 0;
+    /* [UNVERIFIED] the initial best score.  INT_MIN accepts any acceptable cell, also one whose
+     * score is <= 0.  If cutadapt's _align.pyx seeds its best match with score 0 (and keeps the
+     * "score > best or (equal and cost lower)" update), accepted cells scoring < 0 would be
+     * refused there.  Such cells exist only under an absolute -e or a small -O (DESIGN.md §8c
+     * finding 1); at the reference's -e 0.1 -O 3 every accepted cell scores > 0, so the two
+     * readings agree.  tools/parity_vs_cutadapt.sh case "negscore" separates them. */
     int best_score = INT_MIN;
 
     /* Ukkonen's trick: index of the last cell that is at most k */

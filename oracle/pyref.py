@@ -23,6 +23,36 @@ _IUPAC = {"A": 1, "C": 2, "G": 4, "T": 8, "U": 8, "R": 5, "Y": 10, "S": 6, "W": 
 _COMP = str.maketrans("ACGTUMRWSYKVHDBNacgtumrwsykvhdbn", "TGCAAKYWSRMBDHVNtgcaakywsrmbdhvn")
 
 
+# The readings this restatement takes of the rules marked [UNVERIFIED] (cutadapt 4.9 source is
+# not available here).  tests/test_oracle.py switches them to the alternative readings to show
+# that every case of tools/unverified_cases.py (run against a real cutadapt 4.9 by
+# tools/parity_vs_cutadapt.sh) tells the two readings apart.
+DEFAULT_RULES = {
+    "best_init": "none",         # locate's first best: any acceptable cell  | "zero": score 0
+    "tie": "lower_cost",         # locate, equal score: lower cost wins     | "first": keep first
+    "col0": "minus2i",           # BACK column 0: score -2 i                | "zero": score 0
+    "besttie": "fewer_errors",   # best_match, equal score: fewer errors    | "first": file order
+    "rc": "strict",              # --rc: reverse complement iff score >     | "geq": iff >=
+    "linked": "both",            # -g F...R: both parts required            | "front": front alone
+}
+RULES = dict(DEFAULT_RULES)
+
+
+class rules:
+    """with rules(tie="first"): ... — evaluate under an alternative reading."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        self.saved = dict(RULES)
+        RULES.update(self.kw)
+
+    def __exit__(self, *exc):
+        RULES.clear()
+        RULES.update(self.saved)
+
+
 def revcomp(s: str) -> str:
     return s.translate(_COMP)[::-1]
 
@@ -57,7 +87,8 @@ def locate(ref: str, query: str, max_error_rate: float, flags: int, min_overlap:
     # cell = (cost, score, origin)
     C = [[None] * (n + 1) for _ in range(m + 1)]
     for i in range(m + 1):
-        C[i][0] = (0, 0, -i) if start_ref else (i, -2 * i, 0)
+        C[i][0] = (0, 0, -i) if start_ref else (i, -2 * i if RULES["col0"] == "minus2i" else 0,
+                                                    0)
     for j in range(1, n + 1):
         C[0][j] = (0, 0, j)
         for i in range(1, m + 1):
@@ -78,18 +109,25 @@ def locate(ref: str, query: str, max_error_rate: float, flags: int, min_overlap:
             eff = length - n_counts[length] if length < m else eff_len
         return length >= min_overlap and cell[0] <= eff * max_error_rate
 
+    # [UNVERIFIED] no initial score: any acceptable cell can win, also one scoring <= 0 (see
+    # cutadapt_oracle.c "the initial best score"; tools/parity_vs_cutadapt.sh case "negscore")
     best = None  # (score, cost, origin, ref_stop, q_stop)
+    if RULES["best_init"] == "zero":
+        best = (0, m + n + 1, 0, m, n)
+    lower_cost = RULES["tie"] == "lower_cost"
+
+    def better(cell):
+        return best is None or cell[1] > best[0] or (lower_cost and cell[1] == best[0]
+                                                     and cell[0] < best[1])
     for j in range(1, n + 1):
         cell = C[m][j]
-        if acceptable(m, cell) and (best is None or cell[1] > best[0]
-                                    or (cell[1] == best[0] and cell[0] < best[1])):
+        if acceptable(m, cell) and better(cell):
             best = (cell[1], cell[0], cell[2], m, j)
     for i in range(0 if stop_ref else m, m + 1):
         cell = C[i][n]
-        if acceptable(i, cell) and (best is None or cell[1] > best[0]
-                                    or (cell[1] == best[0] and cell[0] < best[1])):
+        if acceptable(i, cell) and better(cell):
             best = (cell[1], cell[0], cell[2], i, n)
-    if best is None:
+    if best is None or best[1] == m + n + 1:   # (the "zero" reading's seed: no match)
         return None
     score, cost, origin, rstop, qstop = best
     if origin >= 0:
@@ -105,7 +143,8 @@ def best_match(adapters, where, seq, e=0.1, min_overlap=3):
         mt = locate(ad, seq, rate, where[a], min_overlap)
         if mt is None:
             continue
-        if bm is None or mt[4] > bm[4] or (mt[4] == bm[4] and mt[5] < bm[5]):
+        if bm is None or mt[4] > bm[4] or (RULES["besttie"] == "fewer_errors" and
+                                           mt[4] == bm[4] and mt[5] < bm[5]):
             best, bm = a, mt
     return best, bm
 
@@ -119,7 +158,7 @@ def demux_round(adapters, where, seq, use_rc=True, e=0.1, min_overlap=3):
         ar, mr = best_match(adapters, where, rc, e, min_overlap)
     fs = mf[4] if mf else 0
     rs = mr[4] if mr else 0
-    if use_rc and rs > fs:
+    if use_rc and (rs > fs or (RULES["rc"] == "geq" and mr is not None and rs == fs)):
         a, mt, src, is_rc = ar, mr, rc, True
     else:
         a, mt, src, is_rc = af, mf, seq, False
@@ -150,10 +189,15 @@ def linked(fronts, backs, seq, e=0.1):
         rest = seq[mf[3]:]
         mb = locate(r, rest, e / len(r) if e >= 1 else e, BACK)
         if mb is None:
-            continue
-        s, er = mf[4] + mb[4], mf[5] + mb[5]
+            if RULES["linked"] != "front":
+                continue
+            s, er = mf[4], mf[5]
+        else:
+            s, er = mf[4] + mb[4], mf[5] + mb[5]
         if best < 0 or s > bs or (s == bs and er < be):
             best, bf, bb, bs, be = a, mf, mb, s, er
     if best < 0:
         return -1, None, None, seq
+    if bb is None:   # the "front" reading: the front part alone
+        return best, bf, None, seq[bf[3]:]
     return best, bf, bb, seq[bf[3]:][:bb[2]]

@@ -405,3 +405,67 @@ def test_pychopper_fasta_and_empty_inputs(tmp_path):
     assert os.path.getsize(tmp_path / "e_pass.fastq") == 0
     assert os.path.exists(tmp_path / "e_unclass.fastq")
     assert "Parameters\tcutoff\tNA" in stats.read_text()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", ["0.2", None])
+def test_fused_reorient_loop_equals_pychopper_then_loop(tmp_path, q):
+    """01 -> 02 fused on the GPU (`dmx-demux-loop --reorient RAW`): pychopper's outputs and every
+    02 output (records and reports) equal bin/pychopper (01_pychopper.sh:45-57) followed by
+    dmx-demux-loop on its PASS file (02_cutadapt_loop.sh) — the PASS records are demultiplexed
+    from the resident batch as oriented views, never written and read back.  Small batches put
+    different batch edges in the two paths."""
+    import glob
+    import gzip
+    import json
+    import shutil
+    from helpers import LOOP
+    names, seqs, quals = _records(np.random.default_rng(32), 1500)
+    two, fused = tmp_path / "two", tmp_path / "fused"
+    for d in (two, fused):
+        d.mkdir()
+        write_fastq(str(d / "sample.fastq.gz"), names, seqs, quals)
+    pych = two / "pychopped"
+    pych.mkdir()
+    cmd = [BIN, "-b", chop.PRIMERS_FASTA, "-c", chop.CONFIG_FILE, "-k", "LSK114", "-Q", "10",
+           "-w", str(pych / "sample_rescued.fastq"), "-u", str(pych / "sample_unclass.fastq"),
+           "-l", str(pych / "sample_short.fastq"), "-S", str(pych / "sample_stats.out"),
+           "-p", "-t", "4", "-m", "edlib", "--batch-mb", "1", str(two / "sample.fastq.gz")]
+    if q:
+        cmd[1:1] = ["-q", q]
+    with open(pych / "sample_pass.fastq", "wb") as fh:
+        subprocess.run(cmd, stdout=fh, check=True)
+    shutil.copy(pych / "sample_pass.fastq", pych / "pychopped_sample.fastq")   # 02's input
+    subprocess.run([LOOP, str(pych / "pychopped_sample.fastq"), "-j", "4", "--batch-mb", "1"],
+                   check=True, stdout=subprocess.DEVNULL)
+    # with -q given the fused run takes other batch edges; the autotune (no -q) samples the
+    # first batch's QC-passing reads (up to -Y), so there both runs read 1 MB batches
+    fcmd = [LOOP, "--reorient", str(fused / "sample.fastq.gz"), "-j", "4", "--batch-mb",
+            "2" if q else "1"]
+    if q:
+        fcmd += ["-q", q]
+    subprocess.run(fcmd, check=True, stdout=subprocess.DEVNULL)
+    for k in ("pass", "rescued", "unclass", "short"):
+        a = (pych / f"sample_{k}.fastq").read_bytes()
+        assert a == (fused / "pychopped" / f"sample_{k}.fastq").read_bytes(), k
+    assert (pych / "sample_stats.out").read_text() == \
+        (fused / "pychopped" / "sample_stats.out").read_text()
+    outs = sorted(os.path.relpath(p, two / "demuxed")
+                  for p in glob.glob(str(two / "demuxed" / "*" / "*")))
+    assert outs == sorted(os.path.relpath(p, fused / "demuxed")
+                          for p in glob.glob(str(fused / "demuxed" / "*" / "*")))
+    assert sum(o.endswith(".fastq.gz") for o in outs) == 12 + 12 * 8
+    n_rec = 0
+    for o in outs:
+        a, b = two / "demuxed" / o, fused / "demuxed" / o
+        if o.endswith(".gz"):
+            ta, tb = gzip.decompress(a.read_bytes()), gzip.decompress(b.read_bytes())
+            assert ta == tb, o
+            n_rec += ta.count(b"\n+\n")
+        else:
+            ja, jb = json.loads(a.read_text()), json.loads(b.read_text())
+            for j in (ja, jb):
+                j.pop("command_line_arguments")
+                j.pop("input")
+            assert ja == jb, o
+    assert n_rec > 0.5 * len(seqs)

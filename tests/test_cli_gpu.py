@@ -145,3 +145,51 @@ def test_04_linked_primers_dropin(tmp_path):
     assert len(trimmed) > 0.6 * len(seqs) and len(untrimmed) > 0
     assert _read_fasta(str(out)) == trimmed
     assert _read_fasta(str(unt)) == untrimmed
+
+
+def test_unverified_rule_cases_match_the_oracle(tmp_path):
+    """The cases tools/parity_vs_cutadapt.sh runs against a real cutadapt 4.9 for every rule the
+    oracle marks [UNVERIFIED] (tools/unverified_cases.py): the drop-in's outputs equal the
+    restatement's (oracle/pyref.py, default readings) record for record."""
+    import importlib.util
+    import pyref
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location(
+        "unverified_cases", os.path.join(root, "tools", "unverified_cases.py"))
+    uc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(uc)
+    cases = tmp_path / "cases"
+    uc.write(str(cases))
+    out = tmp_path / "out"
+    out.mkdir()
+    env = dict(os.environ, DMX_DAEMON="0")
+    for c in uc.CASES:
+        row = [r for r in open(cases / "cases.tsv").read().splitlines()
+               if r.split("\t")[0] == c["name"]][0]
+        _, inp, outs, opts = row.split("\t")
+        subprocess.run([CLI] + opts.split() + outs.replace("@OUT@", str(out)).split() + [inp],
+                       check=True, env=env, cwd=str(cases), stdout=subprocess.DEVNULL)
+        name = c["name"]
+        if c["where"] == "linked":
+            f, r = c["adapters"][0][1].split("...")
+            trimmed, untrimmed = [], []
+            for i, s in enumerate(c["reads"]):
+                a, _, _, tr = pyref.linked([f], [r], s, c["e"])
+                (trimmed if a >= 0 else untrimmed).append((f"{name}{i}", tr, None))
+            assert _read_fasta(str(out / f"{name}.fasta")) == trimmed, name
+            assert _read_fasta(str(out / f"{name}_untrimmed.fasta")) == untrimmed, name
+            continue
+        seqs = [x for _, x in c["adapters"]]
+        w = [pyref.BACK if c["where"] == "back" else pyref.FRONT] * len(seqs)
+        per, ordered = {}, []
+        for i, s in enumerate(c["reads"]):
+            a, rc, _, tr = pyref.demux_round(seqs, w, s, c["rc"], c["e"], c["O"])
+            rec = (f"@{name}{i}" + (" rc" if rc else ""), tr, "I" * len(tr))
+            per.setdefault(a, []).append(rec)
+            ordered.append(rec)
+        if len(seqs) == 1:   # trimmed and untrimmed reads share the one output
+            assert read_fastq(str(out / f"{name}.fastq")) == ordered, name
+        else:
+            for k, (an, _) in enumerate(c["adapters"]):
+                assert read_fastq(str(out / f"{name}_{an}.fastq")) == per.get(k, []), (name, an)
+            assert read_fastq(str(out / f"{name}_unknown.fastq")) == per.get(-1, []), name

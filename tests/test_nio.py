@@ -113,8 +113,11 @@ def test_reader_empty_and_errors(tmp_path):
         nio.Reader(str(tmp_path / "missing.fq"))
 
 
+@pytest.mark.parametrize("level", [1, 5, 9])
 @pytest.mark.parametrize("fasta_out", [False, True])
-def test_sink_matches_python_render(tmp_path, fasta_out):
+def test_sink_matches_python_render(tmp_path, fasta_out, level):
+    """Rendered records, inflated by Python's gzip (zlib) at -Z (1: Huffman-only members) and at
+    cutadapt's default level 5 (libdeflate members), and at 9."""
     recs, text = _records(2500, seed=2)
     (tmp_path / "in.fq").write_text(text)
     rng = np.random.default_rng(5)
@@ -123,7 +126,7 @@ def test_sink_matches_python_render(tmp_path, fasta_out):
     paths = [str(tmp_path / f"o{k}{ext}.gz") if k % 2 == 0 else str(tmp_path / f"o{k}{ext}")
              for k in range(n_out)]
     expect = [[] for _ in range(n_out)]
-    sink = nio.Sink(paths, fasta_out, level=1, threads=4)
+    sink = nio.Sink(paths, fasta_out, level=level, threads=4)
     pyb = list(fastx.read_batches(str(tmp_path / "in.fq"), batch_bytes=1 << 28))
     assert len(pyb) == 1
     pb = pyb[0]
@@ -153,6 +156,24 @@ def test_sink_matches_python_render(tmp_path, fasta_out):
         assert raw == b"".join(expect[k]), k
         assert int(sink.n_written[k]) == len(expect[k])
     assert len(expect[-1]) == 0 and gzip.decompress(open(paths[-1], "rb").read()) == b""
+    # the member header says which compressor wrote it (XFL 4 = fastest, 2 = best)
+    assert open(paths[0], "rb").read()[8] == {1: 4, 5: 0, 9: 2}[level]
+
+
+def test_default_level_is_cutadapts_and_smaller_than_z(tmp_path):
+    """cutadapt 4.9's --compression-level default (5) is the drop-in's default; -Z (level 1) is
+    Huffman-only.  At 5 the members are within a few percent of zlib's level 5 on the same
+    1 MiB pieces (libdeflate), and smaller than at -Z."""
+    from dmx import cli
+    args = cli.build_parser().parse_args(["-g", "ACGT", "-o", "x.fq.gz", "in.fq"])
+    assert args.compression_level == 5 and not args.zlevel1
+    text = _records(3000, seed=8)[1].encode()
+    pieces = [text[i:i + (1 << 20)] for i in range(0, len(text), 1 << 20)]
+    z5 = sum(len(zlib.compress(p, 5)) for p in pieces)
+    d5 = sum(len(nio.gzip_member(p, 5)) for p in pieces)
+    d1 = sum(len(nio.gzip_member(p, 1)) for p in pieces)
+    assert abs(d5 - z5) / z5 < 0.05
+    assert d5 < d1
 
 
 def test_sink_rejects_bad_coordinates(tmp_path):
@@ -516,3 +537,75 @@ def test_reader_single_member_gzip_records(tmp_path, monkeypatch):
     assert read_all(gz) == ref
     monkeypatch.setenv("DMX_SEQ_INFLATE", "1")
     assert read_all(gz) == ref
+
+
+def _revcomp(s: bytes) -> bytes:
+    return s.translate(bytes.maketrans(b"ACGTUMRWSYKVHDBNacgtumrwsykvhdbn",
+                                       b"TGCAAKYWSRMBDHVNtgcaakywsrmbdhvn"))[::-1]
+
+
+def test_pack_views_equals_packing_the_oriented_text(tmp_path):
+    """dmx_batch_pack_views (segments handed to the demultiplexer, the fused 01 -> 02 loop):
+    the packed words, mask, offsets and lengths equal dmx_pack of the oriented view texts."""
+    recs, text = _records(800, seed=21)
+    rng = np.random.default_rng(4)
+    lines = text.split("\n")   # some N in the sequence lines (line 2 of each record)
+    for k in range(1, len(lines), 4):
+        lines[k] = "".join("N" if rng.random() < 0.01 else c for c in lines[k])
+    text = "\n".join(lines)
+    (tmp_path / "in.fq").write_text(text)
+    with nio.Reader(str(tmp_path / "in.fq"), 64 << 20, threads=4) as r:
+        b = r.next()
+        n = len(b)
+        lens = b.lens.astype(np.int64)
+        read = rng.integers(0, n, 1500)
+        a = (rng.random(1500) * (lens[read] + 1)).astype(np.int64)
+        z = a + (rng.random(1500) * (lens[read] - a + 1)).astype(np.int64)
+        rc = rng.integers(0, 2, 1500).astype(np.uint8)
+        got = b.pack_views(read, a, z, rc, threads=4)
+        views = []
+        for i in range(1500):
+            s = b.sequence(int(read[i]))[a[i]:z[i]]
+            views.append(_revcomp(s) if rc[i] else s)
+        b.free()
+    blob = np.frombuffer(b"".join(views), np.uint8)
+    offs = np.concatenate([[0], np.cumsum([len(v) for v in views])[:-1]]).astype(np.uint64)
+    exp = lib.pack(blob, offs, np.array([len(v) for v in views], np.uint32))
+    assert got.offsets.tolist() == exp.offsets.tolist()
+    assert got.lengths.tolist() == exp.lengths.tolist()
+    assert np.array_equal(got.seq2b, exp.seq2b) and np.array_equal(got.nmask, exp.nmask)
+
+
+def test_rows2_segment_names_with_rc_suffixes(tmp_path):
+    """dmx_sink_write_rows2: the segment name of (name_start, name_stop, name_strand), n_rc " rc"
+    suffixes, and read[start:stop] oriented by rc — the fused 01 -> 02 records."""
+    recs, text = _records(300, seed=22)
+    (tmp_path / "in.fq").write_text(text)
+    out = str(tmp_path / "o.fq")
+    rng = np.random.default_rng(5)
+    s = nio.Sink([out], False, 1, threads=2)
+    exp = []
+    with nio.Reader(str(tmp_path / "in.fq")) as r:
+        b = r.next()
+        n = len(b)
+        lens = b.lens.astype(np.int64)
+        ns = (rng.random(n) * (lens + 1)).astype(np.int64)
+        ne = ns + (rng.random(n) * (lens - ns + 1)).astype(np.int64)
+        a = ns + (rng.random(n) * (ne - ns + 1)).astype(np.int64)
+        z = a + (rng.random(n) * (ne - a + 1)).astype(np.int64)
+        rc = rng.integers(0, 2, n).astype(np.uint8)
+        nst = rng.integers(0, 2, n).astype(np.uint8)
+        nrc = rng.integers(0, 3, n).astype(np.uint8)
+        s.write_rows2(b, np.arange(n), np.zeros(n), a, z, rc, ns, ne, nst, nrc)
+        for i in range(n):
+            h = b.header(i).decode()
+            rid, _, com = h.partition(" ")
+            name = (f"{ns[i]}:{ne[i]}|{rid} strand={'-' if nst[i] else '+'}" +
+                    (" " + com if com else "") + " rc" * int(nrc[i]))
+            seq, q = b.sequence(i)[a[i]:z[i]], b.quality(i)[a[i]:z[i]]
+            if rc[i]:
+                seq, q = _revcomp(seq), q[::-1]
+            exp.append(f"@{name}\n{seq.decode()}\n+\n{q.decode()}\n")
+        b.free()
+    s.close()
+    assert open(out).read() == "".join(exp)

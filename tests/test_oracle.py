@@ -3,12 +3,15 @@ alignment semantics, and agreement of its two independent formulations (one-colu
 in C vs full-matrix Python).  PARITY UNPINNED: the reference holds no fixtures for this path
 (SURVEY.md §4/§8c); the KATs below are chosen so their answer is the same under every
 plausible tie rule, except where a test name says `tie_rule`."""
+import os
 import random
 
 import pytest
 
 import oracle
 import pyref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SP5_001 = "CATGTAATGCACGTACTTTCAGGGTGAGCGTCTAATCGTAATTGTAAAACGACGGCCAG"
 SP27_001 = "GTCATAGCTGTTTCCTGTTAACCAGGCACGGAGGAGTCGTCGCAGCCTCACCTGATC"
@@ -159,3 +162,36 @@ def test_linked_c_oracle_equals_full_matrix():
             assert (res["m2_rstart"][i], res["m2_rstop"][i], res["m2_score"][i],
                     res["m2_errors"][i]) == (mb[2], mb[3], mb[4], mb[5])
     assert hits > 30
+
+
+def test_unverified_rule_cases_tell_the_readings_apart():
+    """Every [UNVERIFIED] rule of the restatement has a case in tools/unverified_cases.py (run
+    against a real cutadapt 4.9 by tools/parity_vs_cutadapt.sh) whose outputs differ between
+    the restatement's reading and the alternative one (pyref.rules)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "unverified_cases", os.path.join(ROOT, "tools", "unverified_cases.py"))
+    uc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(uc)
+    assert {c["rule"] for c in uc.CASES} == set(pyref.DEFAULT_RULES)
+
+    def outputs(c):
+        res = []
+        for s in c["reads"]:
+            if c["where"] == "linked":
+                f, r = c["adapters"][0][1].split("...")
+                a, _, _, tr = pyref.linked([f], [r], s, c["e"])
+                res.append((a, tr))
+            else:
+                seqs = [x for _, x in c["adapters"]]
+                w = [pyref.BACK if c["where"] == "back" else pyref.FRONT] * len(seqs)
+                a, rc, _, tr = pyref.demux_round(seqs, w, s, c["rc"], c["e"], c["O"])
+                res.append((a, rc, tr))
+        return res
+
+    for c in uc.CASES:
+        base = outputs(c)
+        with pyref.rules(**{c["rule"]: c["alt"]}):
+            alt = outputs(c)
+        assert base != alt, c["name"]
+        assert pyref.RULES == pyref.DEFAULT_RULES

@@ -31,6 +31,9 @@ from dmx import chop, lib, synth  # noqa: E402
 IUPAC = list("RYSWKMBDHVN")
 
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from provenance import provenance  # noqa: E402
+
 def rand_primer(rng, n, iupac_share):
     return "".join(rng.choice(IUPAC) if rng.random() < iupac_share else "ACGT"[rng.integers(4)]
                    for _ in range(n))
@@ -139,7 +142,8 @@ def main():
             print(f"{cases} cases, {reads} reads, {hits} hits, {len(bad)} mismatching",
                   flush=True)
     res = {"seed": a.seed, "seconds": round(time.time() - t0, 1), "cases": cases, "reads": reads,
-           "hits": hits, "mismatching_cases": len(bad), "mismatches": bad[:20]}
+           "hits": hits, "mismatching_cases": len(bad), "mismatches": bad[:20],
+           "provenance": provenance()}
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as fh:
         json.dump(res, fh, indent=1)

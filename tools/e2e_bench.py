@@ -139,16 +139,19 @@ def main():
         res["pychopper_report"] = p.stderr.strip().splitlines()[-1] if p.stderr.strip() else ""
     res["input_gz_single_bytes"] = os.path.getsize(gz1)
     res["input_gz_single_level"] = a.single_level
-    fused = [("fused_plain", plain), ("fused_gz_members", gz), ("fused_gz_single", gz1)]
+    # outputs at cutadapt's default level 5 (libdeflate members) and at -Z (Huffman-only)
+    fused = [("fused_plain", plain), ("fused_plain_Z", plain), ("fused_gz_members_Z", gz),
+             ("fused_gz_single", gz1), ("fused_gz_single_Z", gz1)]
     if os.environ.get("DMX_E2E_SEQ_A_B") == "1":   # the same file through zlib's sequential path
-        fused.append(("fused_gz_single_seq_inflate", gz1))
+        fused.append(("fused_gz_single_Z_seq_inflate", gz1))
     for tag, path in (() if a.skip_fused else fused):
         t = time.perf_counter()
         fenv = dict(env, DMX_PROFILE_IO="1")
         if tag.endswith("_seq_inflate"):
             fenv["DMX_SEQ_INFLATE"] = "1"
+        zflag = ["-Z"] if "_Z" in tag else []
         p = subprocess.run([os.path.join(PKG, "bin", "dmx-demux-loop"), path, "-j",
-                            str(a.threads), "--outdir", os.path.join(wd, tag)], check=True,
+                            str(a.threads), "--outdir", os.path.join(wd, tag)] + zflag, check=True,
                            env=fenv, stdout=subprocess.DEVNULL,
                            stderr=subprocess.PIPE, text=True)
         fs = time.perf_counter() - t

@@ -29,6 +29,9 @@ from dmx import lib, synth  # noqa: E402
 ALPH = np.array(list("ACGT"))
 
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from provenance import provenance  # noqa: E402
+
 def rand_seq(rng, n):
     return "".join(ALPH[rng.integers(0, 4, size=n)])
 
@@ -206,7 +209,7 @@ def main():
                 print(f"{time.time() - t0:.0f}s: {cases} cases, {reads} reads, "
                       f"{len(bad)} mismatching cases", flush=True)
     res = dict(seed=a.seed, seconds=round(time.time() - t0, 1), cases=cases, reads=reads,
-               mismatching_cases=len(bad), mismatches=bad)
+               mismatching_cases=len(bad), mismatches=bad, provenance=provenance())
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as fh:
         json.dump(res, fh, indent=1)
