@@ -794,6 +794,7 @@ def chop_main(args, ctx, packed, tune, lengths, gen_s, world, rank, dist, on_gpu
             cores, how = args.cpu_threads, f"--cpu-threads {args.cpu_threads}; detected: {how}"
         out["cpu_baseline"] = chop_cpu_baseline(cores, how, cutoff)
     if rank == 0:
+        out["provenance"] = run_provenance()
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:

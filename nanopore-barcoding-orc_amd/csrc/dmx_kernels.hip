@@ -2078,40 +2078,6 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     if (threadIdx.x == 0 && s_nend) atomicAdd(&R.diag[3], s_nend);     // by 3' cells only
 }
 
-// In-place exclusive scan of s[0, n) (n <= 2 * kScanBlock * 4) by the whole block; s_wsum
-// holds one word per wave.  Ends with a barrier.
-__device__ __forceinline__ void block_exclusive_scan(uint32_t* s, int n, uint32_t* s_wsum) {
-    const int per = (n + kScanBlock - 1) / kScanBlock;   // consecutive bins per thread
-    const int b0 = (int)threadIdx.x * per;
-    uint32_t loc = 0;
-    for (int i = 0; i < per; ++i)
-        if (b0 + i < n) loc += s[b0 + i];
-    const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
-    uint32_t inc = loc;   // inclusive wave scan
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += y;
-    }
-    if (lane == 63) s_wsum[wv] = inc;
-    __syncthreads();
-    uint32_t off = inc - loc;
-    for (int w = 0; w < wv; ++w) off += s_wsum[w];
-    for (int i = 0; i < per; ++i)
-        if (b0 + i < n) {
-            const uint32_t c = s[b0 + i];
-            s[b0 + i] = off;
-            off += c;
-        }
-    __syncthreads();
-}
-
-// A/B knob: group the 3' (round-2) window-scan tasks by adapter group too
-#ifndef DMX_WSCAN_SORT_BACK
-#define DMX_WSCAN_SORT_BACK 1
-#endif
-constexpr bool kWscanSortBack = DMX_WSCAN_SORT_BACK != 0;
-
 // Window scan: one lane per (window, adapter) — or, after the index screen, per surviving
 // (piece, adapter) — in a block-uniform grid stride over the device-side count, so that the
 // block can flush its staged records between strides.
@@ -2193,23 +2159,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
       // so the 64 tasks of a wave have nearly equal lengths (tools/task_stats.py, round 1 of
       // c2x24: wave max / mean 1.90 -> 1.09; window scan 4.8 -> 4.1 ms).  3' panels' tasks
       // are already even (1.08), and there the sort only costs (2.4 -> 2.6 ms): not sorted.
-      //
-      // The sort key also groups the tasks by ADAPTER GROUP (8 consecutive adapters) ahead of
-      // the column count: a lane's match-vector read is s_peq[code * kPeqStride + a], whose
-      // dword bank is (2 * kPeqStride * code + 2a) mod 64 = (48 code + 2a) mod 64, so within one
-      // group of 8 adapters every (code, adapter) pair reads its own two banks (4 ACGT codes x 8
-      // adapters x 2 dwords = 64 banks) and the 32 lanes of a ds_read_b64 half never conflict;
-      // lanes of one (code, adapter) broadcast.  Random adapters per wave cost 1.9-2.0 extra LDS
-      // cycles per instruction.  3' panels (even lengths) sort by group only.
-      const bool front_p = R.panel->where == kFront;
-      const int n_groups = (A + 7) >> 3;
-      const int nbc = front_p ? kSortBins : 1;          // column bins per adapter group
-      const bool sorted = front_p || (n_groups > 1 && kWscanSortBack);
+      const bool sorted = R.panel->where == kFront;
       __shared__ uint32_t s_ord[kSortGroup];
-      __shared__ uint32_t s_bin[kSortBins * (kMaxAdapters / 8)];
-      __shared__ uint32_t s_wsum[kScanBlock / 64];
+      __shared__ uint32_t s_bin[kSortBins];
       __shared__ uint8_t s_mk[kMaxAdapters];
-      const int nbins = n_groups * nbc;
       for (int a = threadIdx.x; a < A; a += blockDim.x)
           s_mk[a] = (uint8_t)min(255, (int)R.panel->ad[a].m + (int)R.panel->ad[a].k + 1);
       {
@@ -2218,7 +2171,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
         for (uint32_t gb = blockIdx.x * kSortGroup; gb < nt; gb += gridDim.x * kSortGroup) {
             const uint32_t gn = min((uint32_t)kSortGroup, nt - gb);
             if (sorted) {   // block-uniform
-            for (int b = threadIdx.x; b < nbins; b += kScanBlock) s_bin[b] = 0;
+            if (threadIdx.x < kSortBins) s_bin[threadIdx.x] = 0;
             __syncthreads();                       // (also: s_mk, and the last group's s_ord)
             constexpr int PER = kSortGroup / kScanBlock;
             uint32_t key[PER], pos[PER];
@@ -2229,17 +2182,21 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                 if (li < gn) {
                     const Window* w = tl + sm.phys(gb + li);
                     const int j1 = (int)w->j1, j2 = (int)w->j2, a = (int)w->info;
-                    uint32_t cb = 0;
-                    if (front_p) {
-                        const int cols = j2 - max(j1 - (int)s_mk[a], 0);
-                        cb = (uint32_t)min(max(cols, 0) >> kSortShift, kSortBins - 1);
-                    }
-                    key[e] = (uint32_t)(a >> 3) * (uint32_t)nbc + cb;
+                    const int cols = j2 - max(j1 - (int)s_mk[a], 0);
+                    key[e] = (uint32_t)min(max(cols, 0) >> kSortShift, kSortBins - 1);
                     pos[e] = atomicAdd(&s_bin[key[e]], 1u);
                 }
             }
             __syncthreads();
-            block_exclusive_scan(s_bin, nbins, s_wsum);   // bins -> first slot of each bin
+            if (threadIdx.x == 0) {                // exclusive scan over the bins
+                uint32_t acc = 0;
+                for (int b = 0; b < kSortBins; ++b) {
+                    const uint32_t c = s_bin[b];
+                    s_bin[b] = acc;
+                    acc += c;
+                }
+            }
+            __syncthreads();
 #pragma unroll
             for (int e = 0; e < PER; ++e) {
                 const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
