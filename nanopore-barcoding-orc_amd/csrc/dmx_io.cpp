@@ -722,7 +722,7 @@ struct ParGzSource : Source {
         const uint64_t lim = std::min<uint64_t>(c.stop, in.end_bits());
         c.b8.reserve(dmxi::kWin + (size_t)(lim > from ? (lim - from) / 8 * 7 / 2 : 0) + (1u << 16));
         memset(c.b8.p, 0, dmxi::kWin - w.size());
-        memcpy(c.b8.p + dmxi::kWin - w.size(), w.data(), w.size());
+        if (!w.empty()) memcpy(c.b8.p + dmxi::kWin - w.size(), w.data(), w.size());
         c.b8.n = dmxi::kWin;
         c.ev.clear();
         c.start = from;
@@ -747,7 +747,7 @@ struct ParGzSource : Source {
         const size_t o = t.size();
         t.resize(o + keep);
         if (c.bytes) {
-            memcpy(t.data() + o, c.b8.p + dmxi::kWin + (c.n - keep), keep);
+            if (keep) memcpy(t.data() + o, c.b8.p + dmxi::kWin + (c.n - keep), keep);
             return true;
         }
         const uint16_t* s = c.b16.p + dmxi::kWin + (c.n - keep);
@@ -879,7 +879,7 @@ struct ParGzSource : Source {
                 Chunk& c = ch[k];
                 uint8_t* o = out + c.out;
                 if (c.bytes) {
-                    memcpy(o, c.b8.p + dmxi::kWin, c.n);
+                    if (c.n) memcpy(o, c.b8.p + dmxi::kWin, c.n);
                 } else {
                     const uint16_t* s = c.b16.p + dmxi::kWin;
                     const size_t wmiss = dmxi::kWin - c.w0.size();
