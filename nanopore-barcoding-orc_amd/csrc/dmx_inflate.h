@@ -327,6 +327,25 @@ inline int parse_member_header(const In& in, uint64_t& pos) {
     return 1;
 }
 
+// LZ77 copy of `len` elements from `dist` back.  Whole 16-byte words when the distance spans at
+// least one (each word reads only elements already written; the last one may write up to 15
+// bytes past op + len: callers keep kSlack elements of room), a fill for distance 1 (runs of
+// one quality character), elementwise otherwise.
+constexpr uint32_t kSlack = 16;
+template <typename T>
+inline void copy_match(T* op, uint32_t dist, uint32_t len) {
+    constexpr uint32_t W = 16 / sizeof(T);
+    const T* src = op - dist;
+    if (dist >= W) {
+        for (uint32_t i = 0; i < len; i += W) std::memcpy(op + i, src + i, 16);
+    } else if (dist == 1) {
+        const T v = src[0];
+        for (uint32_t i = 0; i < len; ++i) op[i] = v;
+    } else {
+        for (uint32_t i = 0; i < len; ++i) op[i] = src[i];
+    }
+}
+
 // Decode from `pos` until the first block header at or after stop_bit, the end of the stream,
 // or an error.  T = uint8_t: the 32 KiB before out.p[base] hold the real window (out.n starts
 // at base = kWin); T = uint16_t: they hold markers 256 + w.  hist0: the first output index a
@@ -396,7 +415,7 @@ Stop inflate_run(const In& in, uint64_t& pos, bool& at_member, Buf<T>& out, uint
                     out.n = (size_t)(op - out.p);
                     return Stop::kNeedMore;
                 }
-                room(258);
+                room(258 + kSlack);
                 uint64_t v = in.peek(pos);   // >= 57 valid bits
                 uint32_t e = decode_sym<kLitBits>(lit, v);
                 if (!e) {
@@ -460,12 +479,7 @@ Stop inflate_run(const In& in, uint64_t& pos, bool& at_member, Buf<T>& out, uint
                     out.n = (size_t)at;
                     return Stop::kError;
                 }
-                const T* src = op - dist;
-                if (dist >= len) {
-                    std::memcpy(op, src, len * sizeof(T));
-                } else {
-                    for (uint32_t i = 0; i < len; ++i) op[i] = src[i];
-                }
+                copy_match(op, dist, len);
                 op += len;
                 cap_left -= len;
             }
