@@ -447,6 +447,26 @@ def test_parallel_inflate_single_member_levels(fq_text, monkeypatch, chunk_kb, t
         assert r == 0 and out == fq_text, (level, r, len(out))
 
 
+@pytest.mark.parametrize("threads", [1, 4])
+def test_parallel_inflate_match_periods(monkeypatch, threads):
+    """LZ77 copies of every period 1..40 (csrc/dmx_inflate.h copy_match: fill for distance 1,
+    elementwise below one 16-byte word, whole words above; both the byte decoder and the
+    speculative 16-bit one), with lengths up to 258 and matches ending at chunk edges."""
+    monkeypatch.setenv("DMX_INFLATE_CHUNK_KB", "16")
+    rng = np.random.default_rng(5)
+    parts = []
+    for rep in range(6):
+        for period in range(1, 41):
+            unit = rng.integers(65, 91, period, dtype=np.uint8).tobytes()
+            parts.append(unit * int(rng.integers(1, 400 // period + 3)))
+            parts.append(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8).tobytes())
+    text = b"".join(parts) * 3
+    for level in (1, 6, 9):
+        gz = gzip.compress(text, compresslevel=level)
+        r, out = _inflate(gz, threads)
+        assert r == 0 and out == text, (level, r, len(out))
+
+
 @pytest.mark.parametrize("kind", ["fixed", "stored", "huffman", "rle", "sync", "random_bytes",
                                   "header_fields", "text_mixed"])
 def test_parallel_inflate_block_kinds(fq_text, monkeypatch, kind):
