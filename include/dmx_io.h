@@ -7,8 +7,9 @@
  * (scripts/02_cutadapt_loop.sh:70-71,100-101; scripts/04_cleaning_primers.sh:377-388).
  * dnaio/xopen are not vendored in /root/reference; conventions restated in dmx_io.cpp.
  *
- * Reader: a background thread inflates (zlib; multi-member gzip accepted) and a pool of
- * `threads` workers indexes lines, validates records and packs sequences into the libdmx device
+ * Reader: a background thread feeds a pool of `threads` workers that inflate gzip input in
+ * parallel (any gzip stream: members in parallel, and a single member by speculative chunked
+ * decoding, csrc/dmx_inflate.h), index lines, validate records and pack sequences into the libdmx device
  * layout (include/dmx.h, DMX_PACK_PAD), one batch of about `batch_bytes` of text at a time, up
  * to two batches ahead of the consumer.  Writer ("sink"): dmx_sink_write renders the records of
  * a batch into per-output buffers and compresses them as independent gzip members on
