@@ -419,7 +419,7 @@ struct GzSource : Source {
 
 // Any other gzip stream: parallel inflate (ParGzSource below), or zlib's sequential inflate
 // with DMX_SEQ_INFLATE=1.
-std::unique_ptr<Source> make_gz_source(std::unique_ptr<Source> raw, int threads);
+std::unique_ptr<Source> make_gz_source(std::unique_ptr<Source> raw, int threads, bool ahead);
 
 // gzip members that state their own size — our writer's "DX" extra subfield (compressed and
 // uncompressed member size) or BGZF's "BC" (bgzip, htslib) — are inflated in parallel, each
@@ -544,7 +544,7 @@ struct MemberGzSource : Source {
         pre->inner = std::move(raw);
         cbuf.clear();
         cpos = 0;
-        seq = make_gz_source(std::move(pre), threads);
+        seq = make_gz_source(std::move(pre), threads, false);
     }
 
     long read(uint8_t* dst, size_t cap) override {
@@ -989,10 +989,111 @@ struct ParGzSource : Source {
     }
 };
 
-std::unique_ptr<Source> make_gz_source(std::unique_ptr<Source> raw, int threads) {
+// Read-ahead: a thread of its own pulls blocks from the inner source (the parallel inflate's
+// rounds) up to `depth` blocks ahead, so inflating the next text overlaps the reader's newline
+// scan, parse and pack of the current batch (both fan out to the same work pool; before, the
+// reader thread ran them strictly one after the other).  Consumed blocks go back to the thread
+// (no re-faulting of 64 MB buffers).
+struct AheadSource : Source {
+    struct Blk {
+        std::unique_ptr<uint8_t[]> p;   // blk bytes, uninitialised
+        size_t n = 0;
+    };
+    std::unique_ptr<Source> in;
+    size_t blk = 64u << 20;
+    size_t depth = 2;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Blk> full, spare;
+    bool eof = false, failed = false, stop = false;
+    Blk cur;
+    size_t cpos = 0;
+
+    explicit AheadSource(std::unique_ptr<Source> s) : in(std::move(s)) {
+        if (const char* e = getenv("DMX_INFLATE_AHEAD_KB")) {   // tests: many small blocks
+            const long kb = atol(e);
+            if (kb > 0) blk = (size_t)kb << 10;
+        }
+        th = std::thread([this] { run(); });
+    }
+    ~AheadSource() override {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        th.join();   // a read in progress finishes first (bounded: one inflate round)
+    }
+    size_t chunk_hint() const override { return 1u << 30; }
+    void run() {
+        for (;;) {
+            Blk b;
+            {
+                std::unique_lock<std::mutex> l(mu);
+                cv.wait(l, [&] { return stop || full.size() < depth; });
+                if (stop) return;
+                if (!spare.empty()) {
+                    b = std::move(spare.front());
+                    spare.pop_front();
+                }
+            }
+            if (!b.p) b.p.reset(new uint8_t[blk]);
+            const long n = in->read(b.p.get(), blk);
+            std::lock_guard<std::mutex> g(mu);
+            if (n < 0) {
+                err = in->err;
+                failed = true;
+            } else if (n == 0) {
+                eof = true;
+            } else {
+                b.n = (size_t)n;
+                full.push_back(std::move(b));
+            }
+            cv.notify_all();
+            if (n <= 0) return;
+        }
+    }
+    long read(uint8_t* dst, size_t cap) override {
+        size_t got = 0;
+        while (got < cap) {
+            if (cpos == cur.n) {
+                std::unique_lock<std::mutex> l(mu);
+                if (cur.p) spare.push_back(std::move(cur));
+                cur = Blk();
+                cpos = 0;
+                cv.notify_all();
+                cv.wait(l, [&] { return !full.empty() || eof || failed; });
+                if (full.empty()) {
+                    if (failed) return -1;
+                    break;   // end of input
+                }
+                cur = std::move(full.front());
+                full.pop_front();
+                cv.notify_all();
+            }
+            const size_t k = std::min(cap - got, cur.n - cpos);
+            memcpy(dst + got, cur.p.get() + cpos, k);
+            cpos += k;
+            got += k;
+        }
+        return (long)got;
+    }
+};
+
+// The reader's inflating sources run ahead on a thread of their own (DMX_INFLATE_AHEAD=0: A/B,
+// inflate on the reader's thread).
+std::unique_ptr<Source> read_ahead(std::unique_ptr<Source> p, int threads) {
+    const char* a = getenv("DMX_INFLATE_AHEAD");
+    if (threads > 1 && !(a && a[0] == '0')) return std::make_unique<AheadSource>(std::move(p));
+    return p;
+}
+
+std::unique_ptr<Source> make_gz_source(std::unique_ptr<Source> raw, int threads, bool ahead) {
     const char* e = getenv("DMX_SEQ_INFLATE");
     if (e && atoi(e)) return std::make_unique<GzSource>(std::move(raw));
-    return std::make_unique<ParGzSource>(std::move(raw), threads);
+    std::unique_ptr<Source> p = std::make_unique<ParGzSource>(std::move(raw), threads);
+    return ahead ? read_ahead(std::move(p), threads) : std::move(p);
 }
 
 // A memory range as a source (dmx_io_inflate).
@@ -1490,9 +1591,9 @@ int dmx_reader_open(const char* path, size_t batch_bytes, int threads, dmx_reade
         auto m = std::make_unique<MemberGzSource>();
         m->raw = std::move(pre);
         m->threads = clamp_threads(threads);
-        r->src = std::move(m);
+        r->src = read_ahead(std::move(m), clamp_threads(threads));
     } else if (gz) {
-        r->src = make_gz_source(std::move(pre), clamp_threads(threads));
+        r->src = make_gz_source(std::move(pre), clamp_threads(threads), true);
     } else {
         r->src = std::move(pre);
     }
@@ -1531,7 +1632,7 @@ int dmx_io_inflate(const uint8_t* src, size_t n, int threads, uint8_t* out, size
     auto sp = std::make_unique<SpanSource>();
     sp->p = src;
     sp->n = n;
-    auto gz = make_gz_source(std::move(sp), clamp_threads(threads));
+    auto gz = make_gz_source(std::move(sp), clamp_threads(threads), false);
     size_t got = 0;
     for (;;) {
         const long k = gz->read(out + got, cap - got);

@@ -555,6 +555,16 @@ def test_reader_single_member_gzip_records(tmp_path, monkeypatch):
     ref = read_all(plain)
     monkeypatch.setenv("DMX_INFLATE_CHUNK_KB", "16")
     assert read_all(gz) == ref
+    # inflate running ahead on its own thread in 8 KiB blocks, and on the reader's thread
+    monkeypatch.setenv("DMX_INFLATE_AHEAD_KB", "8")
+    assert read_all(gz) == ref
+    monkeypatch.setenv("DMX_INFLATE_AHEAD", "0")
+    assert read_all(gz) == ref
+    monkeypatch.delenv("DMX_INFLATE_AHEAD")
+    with nio.Reader(str(gz), 64 << 10, threads=4) as r:   # closed with inflate still ahead
+        b = next(iter(r))
+        assert b.header(0) == ref[0][0]
+        b.free()
     monkeypatch.setenv("DMX_SEQ_INFLATE", "1")
     assert read_all(gz) == ref
 
