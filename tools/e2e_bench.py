@@ -10,9 +10,12 @@ FASTQ.gz (level 1, parallel members, via libdmx_io), then times
           (speculative chunk-parallel inflate; DMX_E2E_SEQ_A_B=1 adds zlib's sequential path)
   calls : the 13 bin/cutadapt calls of 02_cutadapt_loop.sh:64-103 (per-call drop-in)
   pychopper (--pychopper): bin/pychopper with 01_pychopper.sh:45-57's flags on the .gz input
+  reorient (--reorient): 01 -> 02 on the raw single-member .gz, two ways: bin/pychopper then
+          bin/dmx-demux-loop on its PASS file (the two scripts), and bin/dmx-demux-loop
+          --reorient (one pass); both at the default level 5
 and prints one JSON line with reads/s for each.  Usage:
   python tools/e2e_bench.py --reads 1000000 [--workload c2] [--threads 16] [--skip-calls]
-                            [--skip-fused] [--pychopper]
+                            [--skip-fused] [--pychopper] [--reorient]
 """
 from __future__ import annotations
 
@@ -88,6 +91,7 @@ def main():
     ap.add_argument("--skip-calls", action="store_true")
     ap.add_argument("--skip-fused", action="store_true")
     ap.add_argument("--pychopper", action="store_true")
+    ap.add_argument("--reorient", action="store_true")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--single-level", type=int, default=1,
                     help="zlib level of the single-member .gz (default strategy: LZ77 + "
@@ -144,6 +148,35 @@ def main():
              ("fused_gz_single", gz1), ("fused_gz_single_Z", gz1)]
     if os.environ.get("DMX_E2E_SEQ_A_B") == "1":   # the same file through zlib's sequential path
         fused.append(("fused_gz_single_Z_seq_inflate", gz1))
+    if a.reorient:   # 01 -> 02: the two scripts vs the fused pass, on the raw single member
+        ro = os.path.join(wd, "reorient")
+        os.makedirs(ro, exist_ok=True)
+        chop_cmd = [os.path.join(PKG, "bin", "pychopper"), "-b", chop.PRIMERS_FASTA,
+                    "-c", chop.CONFIG_FILE, "-k", "LSK114", "-Q", "10",
+                    "-w", f"{ro}/rescued.fastq", "-u", f"{ro}/unclass.fastq",
+                    "-l", f"{ro}/short.fastq", "-S", f"{ro}/stats.out", "-p", "-t",
+                    str(a.threads), "-m", "edlib", gz1]
+        t = time.perf_counter()
+        with open(f"{ro}/pychopped_pass.fastq", "wb") as fh:
+            subprocess.run(chop_cmd, check=True, stdout=fh, stderr=subprocess.DEVNULL, env=env)
+        t_chop = time.perf_counter() - t
+        subprocess.run([os.path.join(PKG, "bin", "dmx-demux-loop"), f"{ro}/pychopped_pass.fastq",
+                        "-j", str(a.threads), "--outdir", f"{ro}/demuxed_two_step"], check=True,
+                       env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        t_two = time.perf_counter() - t
+        t = time.perf_counter()
+        p = subprocess.run([os.path.join(PKG, "bin", "dmx-demux-loop"), gz1, "--reorient",
+                            "--pychopper-dir", f"{ro}/fused_pychopped", "-j", str(a.threads),
+                            "--outdir", f"{ro}/demuxed_fused"], check=True,
+                           env=dict(env, DMX_PROFILE_IO="1"), stdout=subprocess.DEVNULL,
+                           stderr=subprocess.PIPE, text=True)
+        t_fused = time.perf_counter() - t
+        res.update({"reorient_two_step_s": round(t_two, 3),
+                    "reorient_two_step_pychopper_s": round(t_chop, 3),
+                    "reorient_fused_s": round(t_fused, 3),
+                    "reorient_fused_reads_per_s": round(a.reads / t_fused, 1),
+                    "reorient_fused_profile": (p.stderr.strip().splitlines()[-1]
+                                               if p.stderr.strip() else "")})
     for tag, path in (() if a.skip_fused else fused):
         t = time.perf_counter()
         fenv = dict(env, DMX_PROFILE_IO="1")
