@@ -1038,11 +1038,18 @@ struct AheadSource : Source {
                     spare.pop_front();
                 }
             }
-            if (!b.p) b.p.reset(new uint8_t[blk]);
-            const long n = in->read(b.p.get(), blk);
+            long n = -1;
+            std::string e;
+            try {   // (an exception must not leave this thread: std::terminate)
+                if (!b.p) b.p.reset(new uint8_t[blk]);
+                n = in->read(b.p.get(), blk);
+                if (n < 0) e = in->err;
+            } catch (const std::bad_alloc&) {
+                e = "out of memory (gzip read-ahead)";
+            }
             std::lock_guard<std::mutex> g(mu);
             if (n < 0) {
-                err = in->err;
+                err = e;
                 failed = true;
             } else if (n == 0) {
                 eof = true;
