@@ -230,7 +230,12 @@ __host__ __device__ inline uint64_t key_t(uint64_t k) { return k & ((1ull << 40)
 __device__ __forceinline__ uint32_t window32(const uint32_t* __restrict__ w, uint64_t bitpos) {
     const uint64_t q = bitpos >> 5;
     const uint32_t sh = (uint32_t)bitpos & 31u;
+#ifdef DMX_WINDOW32_SPLIT   // A/B build: two 4-byte loads
     const uint64_t v = ((uint64_t)w[q + 1] << 32) | (uint64_t)w[q];
+#else
+    uint64_t v;   // words q and q + 1 as ONE 8-byte load (global_load_dwordx2 at a 4-byte
+    __builtin_memcpy(&v, w + q, 8);   // aligned address: one request instead of two)
+#endif
     return (uint32_t)(v >> sh);
 }
 

@@ -1344,7 +1344,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
 // Survivors are compacted into the second window list for the window scan.
 // ---------------------------------------------------------------------------------------------
 #ifndef DMX_SORT_GROUP
-#define DMX_SORT_GROUP 1024
+#define DMX_SORT_GROUP 2048
 #endif
 constexpr int kSortGroup = DMX_SORT_GROUP;   // tasks ordered by length per block step
 constexpr int kSortBins = 64;                // counting-sort bins of 4 columns (last: >= 252)
@@ -2555,7 +2555,8 @@ __device__ __forceinline__ void band_dp2(const uint8_t* rm, const uint32_t* seq,
             w1 = w2;
             n1 = n2;
             base += 16;
-            fetch16s(seq, nmask, tv, base + 32, w2, n2);
+            // the band's last cell reads view position dx - H + ie + W - 2: no fetch past it
+            if (base + 32 <= dx - H + ie + W - 2) fetch16s(seq, nmask, tv, base + 32, w2, n2);
             o = 0;
         }
         const uint32_t codes = o ? __builtin_amdgcn_alignbit(w1, w0, 2 * o) : w0;
@@ -2647,7 +2648,7 @@ __device__ __forceinline__ void band_dp_fast(const uint8_t* rm, const uint32_t* 
             w1 = w2;
             n1 = spread_even(n2);
             base += 16;
-            fetch16s(seq, nmask, tv, base + 32, w2, n2);
+            if (base + 32 <= dx - H + ie + W - 2) fetch16s(seq, nmask, tv, base + 32, w2, n2);
             o = 0;
         }
         const uint32_t codes = o ? __builtin_amdgcn_alignbit(w1, w0, 2 * o) : w0;
