@@ -11,7 +11,8 @@ for line in open(sys.argv[1]):
         cur = m.group(1)
         rows[cur] = {}
         continue
-    m = re.search(r"remark: .*:\s+([A-Za-z ]+(?:\[[^\]]*\])?): (\S+) \[", line)
+    m = re.search(r"\s(VGPRs|VGPRs Spill|SGPRs Spill|TotalSGPRs|AGPRs|ScratchSize \[bytes/lane\]|"
+                  r"LDS Size \[bytes/block\]|Occupancy \[waves/SIMD\]): (\S+) \[", line)
     if m and cur:
         rows[cur][m.group(1).strip()] = m.group(2)
 keys = sys.argv[2:]
