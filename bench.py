@@ -505,7 +505,8 @@ def main():
                     help="number of ranks (one per GPU); default WORLD_SIZE or 1.  Without a "
                          "launcher, N > 1 starts N rank processes itself")
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)   # the first step after one warm-up still ran ~1 ms slow
+    # (after a single warm-up the first timed step still ran ~1 ms slow)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2x24",
                     choices=["c2x24", "c2", "c4", "c1", "c5", "chop"],
                     help="c5 = config 5, linked COI primers (-g F...R) on consensus FASTA; "
