@@ -94,11 +94,19 @@ int ensure_pipeline(Ctx* c) {
             if ((rc = dev_alloc(c, &c->d_origin[r], s))) return rc;
             if ((rc = dev_alloc(c, &c->d_lb[r], s))) return rc;
         }
-        if ((rc = dev_alloc(c, &c->d_items, items))) return rc;
         if ((rc = dev_alloc(c, &c->d_linked, n))) return rc;
         c->slot_cap = s;
-        c->item_cap = items;
         c->cap_reads = n;
+    }
+    // The item list has its own capacity: a linked batch needs reads x pairs items, which can
+    // exceed what an earlier two-round batch allocated (reads) while its winner slots (2 x
+    // reads) still suffice.  Sizing it only with the slots let finalize0_linked write past
+    // d_items (an illegal memory access in a parity sweep that ran a two-round case, then a
+    // linked one of fewer reads, on one context).
+    if (c->item_alloc < items) {
+        int rc;
+        if ((rc = dev_alloc(c, &c->d_items, items))) return rc;
+        c->item_alloc = items;
     }
     c->item_cap = items;
     const size_t want_cl = 4 * std::max(slots0, n) + 65536;

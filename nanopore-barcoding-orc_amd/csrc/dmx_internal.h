@@ -89,7 +89,8 @@ struct Ctx {
     Window* d_win2 = nullptr;
     size_t win_cap = 0;
     ItemView* d_items = nullptr;
-    size_t item_cap = 0;
+    size_t item_cap = 0;                 // round-2 items of the current mode and batch
+    size_t item_alloc = 0;               // entries allocated in d_items (>= item_cap)
     uint32_t* d_shard = nullptr;      // [kShLists][kShards] per-shard list counters (dmx_device.h)
     uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows, [6+2r..] candidates, [10+r] verified windows, [16+4r..] diag
     unsigned long long* d_counts = nullptr;

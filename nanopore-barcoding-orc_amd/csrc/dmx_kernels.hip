@@ -3179,6 +3179,24 @@ static int resolve_grid(const Ctx* c) {
     return 256 * 8;   // grid-stride; one 64-lane block per CU is LDS-limited (ring)
 }
 
+// DMX_DEBUG_SYNC=1 (diagnostics): synchronise after every stage and name the one that failed,
+// so a device fault is attributed to its kernel instead of to the next API call.
+static bool debug_sync() {
+    static const bool on = getenv("DMX_DEBUG_SYNC") != nullptr;
+    return on;
+}
+#define DMX_DBG_SYNC(name)                                                                   \
+    do {                                                                                      \
+        if (debug_sync()) {                                                                   \
+            const hipError_t e_ = hipStreamSynchronize(st);                                   \
+            if (e_ != hipSuccess) {                                                           \
+                fprintf(stderr, "dmx debug: %s (round %d): %s\n", name, round,                \
+                        hipGetErrorString(e_));                                               \
+                return DMX_E_HIP;                                                             \
+            }                                                                                 \
+        }                                                                                     \
+    } while (0)
+
 int launch_round(Ctx* c, int round, hipStream_t st) {
     RoundArgs R;
     R.seq = c->d_seq;
@@ -3243,9 +3261,11 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
         const uint32_t fgrid = (uint32_t)((nviews + kSegViewsPerBlock - 1) / kSegViewsPerBlock);
         if (fgrid > 0) hipLaunchKernelGGL(filter_kernel, dim3(fgrid), dim3(kScanBlock), 0, st, R);
+        DMX_DBG_SYNC("filter_kernel");
         hipEventRecord(c->ev[9 + 2 * round], st);
         if (hp.verify)
             hipLaunchKernelGGL(verify_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
+        DMX_DBG_SYNC("verify_kernel");
         hipEventRecord(c->ev[10 + 2 * round], st);
         if (R.screen) {   // packed quads for panels of <= 32 adapters (DMX_SCREEN_V1: A/B)
             if (hp.n <= 4 * kScreenQuads && !c->screen_v1)
@@ -3253,24 +3273,30 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
             else
                 hipLaunchKernelGGL(iscreen_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         }
+        DMX_DBG_SYNC("iscreen");
         hipEventRecord(c->ev[13 + round], st);
         if (band) hipLaunchKernelGGL(wscan_kernel<true>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(wscan_kernel<false>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
+        DMX_DBG_SYNC("wscan_kernel");
     } else if (grid > 0) {
         hipEventRecord(c->ev[9 + 2 * round], st);
         hipEventRecord(c->ev[10 + 2 * round], st);
         hipEventRecord(c->ev[13 + round], st);
         if (band) hipLaunchKernelGGL(scan_kernel<true>, dim3(grid), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(scan_kernel<false>, dim3(grid), dim3(kScanBlock), 0, st, R);
+        DMX_DBG_SYNC("scan_kernel");
     }
     hipEventRecord(c->ev[round * 3 + 1], st);
     if (band) {
         hipLaunchKernelGGL((band_cand_kernel<0, 3>), dim3(256 * 8), dim3(256), 0, st, R, 0);
+        DMX_DBG_SYNC("band_cand_kernel<0, 3>");
         if (c->band_wide[round])
             hipLaunchKernelGGL((band_cand_kernel<4, 7>), dim3(256 * 4), dim3(256), 0, st, R, 1);
         else   // every cost in list 1 is <= 5: a band of 2 * 5 + 1 diagonals is exact
             hipLaunchKernelGGL((band_cand_kernel<4, 5>), dim3(256 * 4), dim3(256), 0, st, R, 1);
+        DMX_DBG_SYNC("band_cand_kernel<4, 5|7>");
         hipLaunchKernelGGL(select_cand_kernel, dim3(1024), dim3(256), 0, st, R);
+        DMX_DBG_SYNC("select_cand_kernel");
         hipEventRecord(c->ev[round * 3 + 2], st);
         return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
     }
@@ -3289,7 +3315,9 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     else
         hipLaunchKernelGGL(resolve_kernel<kRingLarge>, dim3(resolve_grid(c)), dim3(kResolveBlock),
                            (size_t)kRingLarge * kResolveBlock * 16 + tabs, st, R);
+    DMX_DBG_SYNC("resolve_kernel");
     hipLaunchKernelGGL(select_kernel, dim3(1024), dim3(256), 0, st, R);
+    DMX_DBG_SYNC("select_kernel");
     hipEventRecord(c->ev[round * 3 + 2], st);
     return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
 }
@@ -3348,6 +3376,7 @@ int launch_finalize(Ctx* c, int round, hipStream_t st) {
             if (gi) hipLaunchKernelGGL(finalize1_linked_kernel, dim3(gi), dim3(256), 0, st, F);
             if (gr) hipLaunchKernelGGL(finalize2_linked_kernel, dim3(gr), dim3(256), 0, st, F);
         }
+        DMX_DBG_SYNC("finalize_linked");
         hipEventRecord(c->ev[6 + round], st);
         return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
     }
@@ -3359,6 +3388,7 @@ int launch_finalize(Ctx* c, int round, hipStream_t st) {
         const size_t shm = sizeof(unsigned int) * ((size_t)(F.A0 + 1) * (F.A1 + 1) + 1);
         if (grid) hipLaunchKernelGGL(finalize1_kernel, dim3(grid), dim3(256), shm, st, F);
     }
+    DMX_DBG_SYNC("finalize");
     hipEventRecord(c->ev[6 + round], st);
     return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
 }

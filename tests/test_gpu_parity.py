@@ -205,6 +205,39 @@ def test_config5_linked_matches_oracle(ctx):
     _assert_same(ctx.run(lib.pack(d["blob"], d["offsets"], d["lengths"])), exp)
 
 
+def test_linked_after_two_round_on_one_context():
+    """Item list capacity across modes (parity sweep seed 43: illegal memory access).  A
+    two-round batch of n1 reads sizes the winner slots for 2 n1 and the item list for n1; a later
+    linked batch of n2 < n1 reads with P pairs needs n2 P items while n2 P <= 2 n1 slots still fit,
+    so only the item list has to grow.  Every read here carries every pair, so the linked round 1
+    has n2 P items; the results must equal the oracle's."""
+    rng = np.random.default_rng(43)
+    d = synth.generate("c2", n=2000, seed=9)
+    pairs = [tuple(_random_panel(rng, 2, 20, 26, 0.0)) for _ in range(2)]
+    seqs = []
+    for _ in range(1900):
+        s = ""
+        for f, r in pairs:
+            s += (rand_dna(rng, int(rng.integers(0, 15))) + f + rand_dna(rng, int(rng.integers(30, 120)))
+                  + r)
+        seqs.append(s + rand_dna(rng, int(rng.integers(0, 15))))
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    exp = oracle.run_batch(oracle.Panel([p[0] for p in pairs], oracle.FRONT),
+                           oracle.Panel([p[1] for p in pairs], oracle.BACK),
+                           blob, offs, lens, mode=2, use_rc=False, threads=8)
+    with lib.Context(0) as c:
+        _assert_same(_gpu_two_round(c, d), _oracle_two_round(d))
+        c.set_panel(0, [p[0] for p in pairs], lib.DMX_FRONT)
+        c.set_panel(1, [p[1] for p in pairs], lib.DMX_BACK)
+        c.set_mode(lib.MODE_LINKED)
+        _assert_same(c.run(lib.pack(blob, offs, lens)), exp)
+    assert (exp["bin1"] >= 0).mean() > 0.9
+
+
+def rand_dna(rng, n):
+    return "".join(rng.choice(list("ACGT"), size=n))
+
+
 def test_run_multi_shards_equal_single_context(ctx):
     """dmx_run_multi: length-balanced contiguous shards over several contexts (here three on
     one GPU, each with its own stream and host thread) give the single-context results in
