@@ -202,6 +202,8 @@ def run(argv=None) -> int:
     sink2 = nio.Sink(p2, False, level, threads=args.threads)
     bp2_out = np.zeros(len(n1), np.int64)
     prof = dict(read_wait=0.0, gpu=0.0, plan_write=0.0, drain=0.0)
+    if reo is not None:   # parts of "gpu": pychopper step, view packing
+        prof.update(reo=0.0, pack=0.0)
     n2_out = np.zeros(len(n1), np.int64)
     totals = np.zeros((len(n1) + 1, len(n2) + 1), dtype=np.int64)   # device bin counts
     try:
@@ -220,8 +222,11 @@ def run(argv=None) -> int:
                     packed, lens = batch.packed, batch.lens
                     if reo is not None:   # the PASS records of 01_pychopper.sh, as views
                         views = reo.batch(batch)
+                        tp = time.perf_counter()
+                        prof["reo"] += tp - tw
                         packed = batch.pack_views(views[0], views[1], views[2], views[3],
                                                   threads=args.threads)
+                        prof["pack"] += time.perf_counter() - tp
                         lens = packed.lengths
                         if not len(lens):
                             continue
@@ -271,6 +276,8 @@ def run(argv=None) -> int:
         if reo is not None:
             reo.close()
         prof["drain"] += time.perf_counter() - tw
+    if reo is not None:
+        prof.update({"reo_" + k: v for k, v in reo.prof.items()})
     if os.environ.get("DMX_PROFILE_IO"):
         print("io profile (s): " + ", ".join(f"{k} {v:.3f}" for k, v in prof.items()),
               file=sys.stderr)
@@ -326,22 +333,33 @@ class Reorienter:
         self.stats = chop.ChopStats()
         self.cutoff = args.cutoff
         self.t0 = time.perf_counter()
+        self.prof = dict(qual=0.0, tune=0.0, chop=0.0, rows=0.0)   # parts of the io profile's "reo"
+
+    def _tick(self, key, t):
+        now = time.perf_counter()
+        self.prof[key] += now - t
+        return now
 
     def batch(self, b):
         chop, a = self.chop, self.args
         if self.sink is None:
             self.sink = nio.Sink(self.paths, b.fasta, 1, threads=a.threads)
         n = len(b)
+        t = time.perf_counter()
         qc_ok = np.ones(n, dtype=bool) if b.fasta else b.mean_qual() >= a.min_qual
+        t = self._tick("qual", t)
         if self.cutoff is None:   # tuned on the first -Y QC-passing reads (bin/pychopper's rule)
             self.ctx.load(chop.sample_packed(b.packed, np.nonzero(qc_ok)[0][:a.autotune_n]))
             self.cutoff = self.ch.autotune(np.arange(self.ctx._n_loaded),
                                            a.autotune_samples or chop.AUTOTUNE_SAMPLES)
+            t = self._tick("tune", t)
         self.ctx.load(b.packed)
         self.ch.set_cutoff(self.cutoff)
         nseg, segs = self.ch.run()
+        t = self._tick("chop", t)
         self.sink.write_rows(b, *chop.plan_rows(nseg, segs, b.lens, qc_ok, a.min_len, self.outs))
         self.stats.add(nseg, segs, qc_ok, a.min_len)
+        self._tick("rows", t)
         sread = segs["read"].astype(np.int64)
         sstart = segs["start"].astype(np.int64)
         sstop = segs["stop"].astype(np.int64)
