@@ -2122,6 +2122,130 @@ struct QualTable {
     }
 };
 
+// 32 nt of a packed stream (include/dmx.h layout) from nt position p: their 2-bit codes and
+// their no-match bits.  Reads up to two words past the 32 nt, inside a batch's tail pad.
+inline uint64_t codes32_at(const uint32_t* w, uint64_t p) {
+    const uint64_t i = p / 16;
+    const unsigned __int128 v = (unsigned __int128)w[i] | ((unsigned __int128)w[i + 1] << 32) |
+                                ((unsigned __int128)w[i + 2] << 64);
+    return (uint64_t)(v >> (2 * (unsigned)(p % 16)));
+}
+inline uint32_t mask32_at(const uint32_t* m, uint64_t p) {
+    const uint64_t i = p / 32;
+    return (uint32_t)((((uint64_t)m[i + 1] << 32) | (uint64_t)m[i]) >> (p % 32));
+}
+inline uint64_t rev_fields2(uint64_t x) {   // reverse the order of the 32 2-bit fields
+    x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
+    return __builtin_bswap64(x);
+}
+inline uint32_t rev_bits32(uint32_t x) {
+    x = ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
+    x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
+    x = ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
+    return __builtin_bswap32(x);
+}
+inline uint64_t spread2(uint32_t m) {   // bit k -> bits 2k and 2k + 1
+    uint64_t x = m;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x | (x << 1);
+}
+
+// One view of n nt at nt position p of a batch's packed words, reverse-complemented if rc,
+// packed at g0 (a 32-nt boundary) exactly as dmx::pack_one / pack_one_rc would pack its text:
+// a word copy per 32 nt instead of a table lookup per nt.  The batch words were packed from the
+// same text by pack_one, so a forward copy is that packing; on the reverse strand a code becomes
+// code ^ 3 (A<->T, C<->G) and a no-match nt keeps code 0 and its mask bit.  Whole groups are
+// written, with the fields past n zero.
+inline void pack_view(const uint32_t* seq, const uint32_t* nm, uint64_t p, uint32_t n, bool rc,
+                      uint64_t g0, uint32_t* out_seq, uint32_t* out_nm) {
+    uint32_t* sw = out_seq + g0 / 16;
+    uint32_t* nw = out_nm + g0 / 32;
+    for (uint32_t x = 0; x < n; x += 32) {
+        const uint32_t cnt = n - x < 32u ? n - x : 32u;
+        uint64_t c;
+        uint32_t m;
+        if (!rc) {
+            c = codes32_at(seq, p + x);
+            m = mask32_at(nm, p + x);
+        } else {   // output nt y = complement of view nt n - 1 - (x + y): the block ending there
+            const uint64_t q = p + n - x - 32;   // >= p - 31 >= kPad - 31 > 0
+            m = rev_bits32(mask32_at(nm, q));
+            c = (~rev_fields2(codes32_at(seq, q))) & ~spread2(m);
+        }
+        if (cnt < 32) {
+            c &= (1ull << (2 * cnt)) - 1ull;
+            m &= (1u << cnt) - 1u;
+        }
+        sw[x / 16] = (uint32_t)c;
+        sw[x / 16 + 1] = (uint32_t)(c >> 32);
+        nw[x / 32] = m;
+    }
+}
+
+// Mean qualities of reads [lo, hi): each read's sum runs in read order from 0.0 (bit-exact with
+// a plain loop, oracle/chopper.py mean_qual), but four reads' chains are interleaved, so each
+// add's latency hides behind the other chains' adds.  A chain whose read ends takes the next.
+void mean_qual_range(const Batch* b, const double* tab, size_t lo, size_t hi, double* out) {
+    constexpr int K = 4;
+    const uint8_t* qp[K];
+    uint32_t left[K];
+    double sum[K];
+    size_t rid[K];
+    size_t next = lo;
+    const auto finish = [&](size_t r, double s) {
+        out[r] = -10.0 * std::log10(s / (double)b->lens_v[r]);
+    };
+    const auto refill = [&](int j) {
+        while (next < hi) {
+            const size_t r = next++;
+            if (!b->lens_v[r]) {
+                out[r] = 0.0;
+                continue;
+            }
+            qp[j] = b->text_v.data() + b->qual_v[2 * r];
+            left[j] = b->lens_v[r];
+            sum[j] = 0.0;
+            rid[j] = r;
+            return true;
+        }
+        return false;
+    };
+    int act = 0;
+    while (act < K && refill(act)) ++act;
+    while (act == K) {
+        const uint32_t step = std::min(std::min(left[0], left[1]), std::min(left[2], left[3]));
+        double s0 = sum[0], s1 = sum[1], s2 = sum[2], s3 = sum[3];
+        const uint8_t *a0 = qp[0], *a1 = qp[1], *a2 = qp[2], *a3 = qp[3];
+        for (uint32_t k = 0; k < step; ++k) {
+            s0 += tab[a0[k]];
+            s1 += tab[a1[k]];
+            s2 += tab[a2[k]];
+            s3 += tab[a3[k]];
+        }
+        sum[0] = s0, sum[1] = s1, sum[2] = s2, sum[3] = s3;
+        for (int j = K - 1; j >= 0; --j) {
+            qp[j] += step;
+            left[j] -= step;
+            if (left[j]) continue;
+            finish(rid[j], sum[j]);
+            if (!refill(j)) {   // the range is drained: keep the chains compact
+                --act;
+                qp[j] = qp[act], left[j] = left[act], sum[j] = sum[act], rid[j] = rid[act];
+            }
+        }
+    }
+    for (int j = 0; j < act; ++j) {
+        double s = sum[j];
+        for (uint32_t k = 0; k < left[j]; ++k) s += tab[qp[j][k]];
+        finish(rid[j], s);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -2206,17 +2330,17 @@ int dmx_batch_pack_views(const dmx_batch* bp, size_t n_views, const uint32_t* re
     // the same word count as dmx_pack_words(total, n_views) (include/dmx.h)
     const uint64_t nt = 2 * kPad + total + (uint64_t)dmx::kPackAlign * n_views;
     if (n_words < (size_t)((nt + 31) / 32 * 2 + 4)) return -3;
-    memset(out_seq2b, 0, n_words * sizeof(uint32_t));
-    memset(out_nmask, 0, n_words * sizeof(uint32_t));
-    const uint8_t* st = b->fasta ? b->seqtext_v.data() : b->text_v.data();
+    // views tile [kPad, g) in whole 32-nt groups, each written below: zero the rest only
+    std::fill(out_seq2b, out_seq2b + kPad / 16, 0u);
+    std::fill(out_nmask, out_nmask + kPad / 32, 0u);
+    std::fill(out_seq2b + std::min<size_t>(n_words, g / 16), out_seq2b + n_words, 0u);
+    std::fill(out_nmask + std::min<size_t>(n_words, g / 32), out_nmask + n_words, 0u);
     const int nth = (int)std::min<size_t>(clamp_threads(threads), std::max<size_t>(1, n_views / 1024));
     parallel(nth, [&](int t) {
         const size_t lo = n_views * t / nth, hi = n_views * (t + 1) / nth;
-        for (size_t i = lo; i < hi; ++i) {
-            const uint8_t* src = st + b->seq_v[2 * read[i]] + start[i];
-            if (rc[i]) dmx::pack_one_rc(src, out_lens[i], out_offsets[i], out_seq2b, out_nmask);
-            else dmx::pack_one(src, out_lens[i], out_offsets[i], out_seq2b, out_nmask);
-        }
+        for (size_t i = lo; i < hi; ++i)
+            pack_view(b->seq2b_v.data(), b->nmask_v.data(), b->offs_v[read[i]] + (uint64_t)start[i],
+                      out_lens[i], rc[i] != 0, out_offsets[i], out_seq2b, out_nmask);
     });
     return 0;
 }
@@ -2231,18 +2355,7 @@ int dmx_batch_mean_qual(const dmx_batch* bp, double* out) {
     const int nth = (int)std::min<size_t>(std::min(clamp_threads(0), 16),
                                           std::max<size_t>(1, n / 4096));
     parallel(nth, [&](int t) {
-        const size_t lo = n * t / nth, hi = n * (t + 1) / nth;
-        for (size_t r = lo; r < hi; ++r) {
-            const uint32_t len = b->lens_v[r];
-            if (!len) {
-                out[r] = 0.0;
-                continue;
-            }
-            const uint8_t* q = b->text_v.data() + b->qual_v[2 * r];
-            double sum = 0.0;
-            for (uint32_t k = 0; k < len; ++k) sum += qt.p[q[k]];
-            out[r] = -10.0 * std::log10(sum / (double)len);
-        }
+        mean_qual_range(b, qt.p, n * t / nth, n * (t + 1) / nth, out);
     });
     return 0;
 }

@@ -150,6 +150,23 @@ def test_native_mean_quality_matches_oracle(tmp_path):
     assert got.tolist() == [ochop.mean_qual(q) for q in quals]
 
 
+def test_native_mean_quality_interleaved_chains(tmp_path):
+    """dmx_batch_mean_qual sums four reads at a time in interleaved chains (each in read order):
+    ragged and empty reads across several threads' ranges stay bit-exact with the oracle."""
+    rng = np.random.default_rng(9)
+    n = 9000
+    lens = np.where(rng.random(n) < 0.05, 0, rng.integers(1, 400, n))
+    seqs = ["A" * int(k) for k in lens]
+    quals = ["".join(chr(33 + int(x)) for x in rng.integers(0, 60, size=int(k))) for k in lens]
+    path = str(tmp_path / "q.fastq")
+    write_fastq(path, [f"r{i}" for i in range(n)], seqs, quals)
+    with nio.Reader(path) as r:
+        b = r.next()
+        got = b.mean_qual()
+        b.free()
+    assert got.tolist() == [ochop.mean_qual(q) for q in quals]
+
+
 def test_sink_rows_render_segments(tmp_path):
     path, names, seqs, quals = _fastq(tmp_path, np.random.default_rng(3))
     out = str(tmp_path / "out.fastq")

@@ -574,27 +574,30 @@ def _revcomp(s: bytes) -> bytes:
                                        b"TGCAAKYWSRMBDHVNtgcaakywsrmbdhvn"))[::-1]
 
 
-def test_pack_views_equals_packing_the_oriented_text(tmp_path):
+@pytest.mark.parametrize("n_views,n_rate", [(1500, 0.01), (6000, 0.2)])
+def test_pack_views_equals_packing_the_oriented_text(tmp_path, n_views, n_rate):
     """dmx_batch_pack_views (segments handed to the demultiplexer, the fused 01 -> 02 loop):
-    the packed words, mask, offsets and lengths equal dmx_pack of the oriented view texts."""
+    the packed words, mask, offsets and lengths equal dmx_pack of the oriented view texts.
+    The views are word copies of the batch's own packing (shifted, or reversed and complemented):
+    N-rich reads and several threads' ranges too."""
     recs, text = _records(800, seed=21)
     rng = np.random.default_rng(4)
     lines = text.split("\n")   # some N in the sequence lines (line 2 of each record)
     for k in range(1, len(lines), 4):
-        lines[k] = "".join("N" if rng.random() < 0.01 else c for c in lines[k])
+        lines[k] = "".join("N" if rng.random() < n_rate else c for c in lines[k])
     text = "\n".join(lines)
     (tmp_path / "in.fq").write_text(text)
     with nio.Reader(str(tmp_path / "in.fq"), 64 << 20, threads=4) as r:
         b = r.next()
         n = len(b)
         lens = b.lens.astype(np.int64)
-        read = rng.integers(0, n, 1500)
-        a = (rng.random(1500) * (lens[read] + 1)).astype(np.int64)
-        z = a + (rng.random(1500) * (lens[read] - a + 1)).astype(np.int64)
-        rc = rng.integers(0, 2, 1500).astype(np.uint8)
+        read = rng.integers(0, n, n_views)
+        a = (rng.random(n_views) * (lens[read] + 1)).astype(np.int64)
+        z = a + (rng.random(n_views) * (lens[read] - a + 1)).astype(np.int64)
+        rc = rng.integers(0, 2, n_views).astype(np.uint8)
         got = b.pack_views(read, a, z, rc, threads=4)
         views = []
-        for i in range(1500):
+        for i in range(n_views):
             s = b.sequence(int(read[i]))[a[i]:z[i]]
             views.append(_revcomp(s) if rc[i] else s)
         b.free()
