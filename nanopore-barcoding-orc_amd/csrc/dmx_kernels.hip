@@ -437,6 +437,13 @@ struct CandOut {
 };
 
 // Exclusive prefix sum over the 64 lanes of the wave (every lane calls it), and the total.
+// Sum of v over the wave's 64 lanes (all active), in every lane.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t x = v;
@@ -3075,6 +3082,9 @@ __device__ __forceinline__ uint32_t pick_winner(const FinalArgs& F, uint32_t i, 
 
 // Round 0 epilogue (one thread per read): write m1/bin1, build the round-1 view (the
 // round-0-trimmed sequence: FRONT -> view[rstop:], BACK -> view[:rstart]) and queue it.
+// Block-stride over the reads (kFinalGrid blocks): the bin histogram is flushed once per block,
+// not once per 256 reads (one global atomic per bin and block, on a few dozen addresses).
+constexpr uint32_t kFinalGrid = 2048;
 __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
     __shared__ unsigned int s_hist[2 * (kMaxAdapters + 1) + 1];
     __shared__ uint32_t s_nq, s_qbase;
@@ -3082,54 +3092,64 @@ __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
     for (int x = threadIdx.x; x < nh + 1; x += blockDim.x) s_hist[x] = 0;
     if (threadIdx.x == 0) s_nq = 0;
     __syncthreads();
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    ItemView v;
-    uint32_t qi = ~0u;                 // this read's slot in the block's share of the item list
-    if (r < F.n_reads) {
-        dmx_result out;
-        out.bin1 = -1;
-        out.bin2 = -1;
-        out.rc1 = out.rc2 = 0;
-        out.flags = 0;
-        out._pad = 0;
-        out.m1 = dmx_match{0, 0, 0, 0, 0, 0};
-        out.m2 = out.m1;
-        uint64_t key;
-        int o;
-        const uint32_t ws = pick_winner(F, r, key, o);
-        out.rc1 = (uint8_t)o;
-        if (key != ~0ull) {
-            int a;
-            const uint32_t n = F.lens[r];
-            decode_match(key, F.origin[ws], n, F.p0, out.m1, a, o);
-            out.bin1 = (int16_t)a;
+    uint32_t n_rc = 0;
+    for (uint32_t base = blockIdx.x * 256u; base < F.n_reads; base += gridDim.x * 256u) {
+        const uint32_t r = base + threadIdx.x;
+        ItemView v;
+        uint32_t qi = ~0u;             // this read's slot in the block's share of the item list
+        if (r < F.n_reads) {
+            dmx_result out;
+            out.bin1 = -1;
+            out.bin2 = -1;
+            out.rc1 = out.rc2 = 0;
+            out.flags = 0;
+            out._pad = 0;
+            out.m1 = dmx_match{0, 0, 0, 0, 0, 0};
+            out.m2 = out.m1;
+            uint64_t key;
+            int o;
+            const uint32_t ws = pick_winner(F, r, key, o);
             out.rc1 = (uint8_t)o;
-            if (F.mode == DMX_MODE_TWO_ROUND) {
-                v.read = r;
-                v.strand = (uint8_t)o;
-                v.pad = 0;
-                v.only_adapter = -1;
-                if (F.p0->ad[a].where == kFront) {
-                    v.start = (uint32_t)out.m1.rstop;
-                    v.len = n - (uint32_t)out.m1.rstop;
+            if (key != ~0ull) {
+                int a;
+                const uint32_t n = F.lens[r];
+                decode_match(key, F.origin[ws], n, F.p0, out.m1, a, o);
+                out.bin1 = (int16_t)a;
+                out.rc1 = (uint8_t)o;
+                if (F.mode == DMX_MODE_TWO_ROUND) {
+                    v.read = r;
+                    v.strand = (uint8_t)o;
+                    v.pad = 0;
+                    v.only_adapter = -1;
+                    if (F.p0->ad[a].where == kFront) {
+                        v.start = (uint32_t)out.m1.rstop;
+                        v.len = n - (uint32_t)out.m1.rstop;
+                    } else {
+                        v.start = 0;
+                        v.len = (uint32_t)out.m1.rstart;
+                    }
+                    qi = atomicAdd(&s_nq, 1u);    // LDS; one global atomic per pass below
                 } else {
-                    v.start = 0;
-                    v.len = (uint32_t)out.m1.rstart;
+                    atomicAdd(&s_hist[a + 1], 1u);
                 }
-                qi = atomicAdd(&s_nq, 1u);    // LDS; one global atomic per block below
             } else {
-                atomicAdd(&s_hist[a + 1], 1u);
+                atomicAdd(&s_hist[0], 1u);
             }
-        } else {
-            atomicAdd(&s_hist[0], 1u);
+            n_rc += o ? 1u : 0u;
+            F.res[r] = out;
         }
-        if (o) atomicAdd(&s_hist[nh], 1u);
-        F.res[r] = out;
+        __syncthreads();
+        if (threadIdx.x == 0) {   // (the other threads wait at the barrier below)
+            s_qbase = s_nq ? atomicAdd(F.n_items, s_nq) : 0u;
+            s_nq = 0;
+        }
+        __syncthreads();
+        if (qi != ~0u) F.items[s_qbase + qi] = v;
     }
+    // reads taken reverse-complemented: one LDS atomic per wave
+    n_rc = wave_sum(n_rc);
+    if ((threadIdx.x & 63u) == 0 && n_rc) atomicAdd(&s_hist[nh], n_rc);
     __syncthreads();
-    if (threadIdx.x == 0) s_qbase = s_nq ? atomicAdd(F.n_items, s_nq) : 0u;
-    __syncthreads();
-    if (qi != ~0u) F.items[s_qbase + qi] = v;
     const int stride1 = F.mode == DMX_MODE_TWO_ROUND ? F.A1 + 1 : 1;
     const int ncounts = (F.A0 + 1) * stride1;
     for (int x = threadIdx.x; x < nh + 1; x += blockDim.x) {
@@ -3146,8 +3166,10 @@ __global__ __launch_bounds__(256) void finalize1_kernel(FinalArgs F) {
     const int nbins = (F.A0 + 1) * (F.A1 + 1);
     for (int x = threadIdx.x; x < nbins + 1; x += blockDim.x) s_hist2[x] = 0;
     __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < *F.n_items) {
+    const uint32_t n_items = *F.n_items;
+    uint32_t n_rc = 0;
+    // block-stride (kFinalGrid blocks): one flush of the (bin1, bin2) histogram per block
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n_items; i += gridDim.x * 256u) {
         const ItemView v = F.items[i];
         dmx_result& out = F.res[v.read];
         uint64_t key;
@@ -3161,9 +3183,11 @@ __global__ __launch_bounds__(256) void finalize1_kernel(FinalArgs F) {
             out.bin2 = (int16_t)a;
             b = a;
         }
-        if (o) atomicAdd(&s_hist2[nbins], 1u);
+        n_rc += o ? 1u : 0u;
         atomicAdd(&s_hist2[(out.bin1 + 1) * (F.A1 + 1) + (b + 1)], 1u);
     }
+    n_rc = wave_sum(n_rc);
+    if ((threadIdx.x & 63u) == 0 && n_rc) atomicAdd(&s_hist2[nbins], n_rc);
     __syncthreads();
     for (int x = threadIdx.x; x < nbins + 1; x += blockDim.x) {
         const unsigned int c = s_hist2[x];
@@ -3381,10 +3405,10 @@ int launch_finalize(Ctx* c, int round, hipStream_t st) {
         return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
     }
     if (round == 0) {
-        const uint32_t grid = (uint32_t)((c->n_reads + 255) / 256);
+        const uint32_t grid = (uint32_t)std::min<size_t>((c->n_reads + 255) / 256, kFinalGrid);
         if (grid) hipLaunchKernelGGL(finalize0_kernel, dim3(grid), dim3(256), 0, st, F);
     } else {
-        const uint32_t grid = (uint32_t)((c->item_cap + 255) / 256);
+        const uint32_t grid = (uint32_t)std::min<size_t>((c->item_cap + 255) / 256, kFinalGrid);
         const size_t shm = sizeof(unsigned int) * ((size_t)(F.A0 + 1) * (F.A1 + 1) + 1);
         if (grid) hipLaunchKernelGGL(finalize1_kernel, dim3(grid), dim3(256), shm, st, F);
     }
