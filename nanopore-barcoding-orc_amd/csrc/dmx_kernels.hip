@@ -3038,8 +3038,9 @@ __global__ __launch_bounds__(256) void finalize2_linked_kernel(FinalArgs F) {
     __shared__ unsigned int s_hist[kMaxAdapters + 1];
     for (int x = threadIdx.x; x <= F.A0; x += blockDim.x) s_hist[x] = 0;
     __syncthreads();
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < F.n_reads) {
+    // block-stride (kFinalGrid blocks): one flush of the pair histogram per block
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < F.n_reads;
+         r += gridDim.x * blockDim.x) {
         const uint64_t ck = F.linked_best[r];
         int b = -1;
         if (ck != ~0ull) {
@@ -3398,7 +3399,9 @@ int launch_finalize(Ctx* c, int round, hipStream_t st) {
         } else {
             const uint32_t gi = (uint32_t)((c->item_cap + 255) / 256);
             if (gi) hipLaunchKernelGGL(finalize1_linked_kernel, dim3(gi), dim3(256), 0, st, F);
-            if (gr) hipLaunchKernelGGL(finalize2_linked_kernel, dim3(gr), dim3(256), 0, st, F);
+            if (gr)
+                hipLaunchKernelGGL(finalize2_linked_kernel, dim3(std::min(gr, kFinalGrid)),
+                                   dim3(256), 0, st, F);
         }
         DMX_DBG_SYNC("finalize_linked");
         hipEventRecord(c->ev[6 + round], st);
