@@ -414,3 +414,40 @@ def test_packed_index_screen(ctx, seed, n, lmin, lmax, where, monkeypatch):
     r = 0 if where == "front" else 1
     assert tasks["packed"][r] >= tasks["v1"][r]
     assert tasks["packed"][r] <= 2 * tasks["v1"][r] + 100
+
+
+def _run_mode(ctx, d, linked):
+    f = 0 if linked else lib.DMX_RC
+    ctx.set_panel(0, d["sp5"], lib.DMX_FRONT | f)
+    ctx.set_panel(1, d["sp27"], lib.DMX_BACK | f)
+    ctx.set_mode(lib.MODE_LINKED if linked else lib.MODE_TWO_ROUND)
+    return ctx.run(lib.pack(d["blob"], d["offsets"], d["lengths"])), ctx.counts()
+
+
+def _sub(d, lo, hi):
+    return dict(d, offsets=d["offsets"][lo:hi], lengths=d["lengths"][lo:hi])
+
+
+@pytest.mark.parametrize("config", ["c2", "c5"])
+def test_large_batch_equals_sub_batches(ctx, config):
+    """Above 2048 x 256 reads the finalize kernels take several passes per block (block-stride,
+    one bin-histogram flush per block, the round-2 item list claimed per pass). A 1.2 M-read
+    batch gives the per-read results and per-bin counts of the same reads run as three 400 k
+    sub-batches (one pass each), and a sample of its reads matches the oracle."""
+    n = 1_200_000
+    linked = config == "c5"
+    d = synth.generate(config, n=n, seed=57)
+    got, counts = _run_mode(ctx, d, linked)
+    parts, csum = [], None
+    for lo in range(0, n, 400_000):
+        g, c = _run_mode(ctx, _sub(d, lo, lo + 400_000), linked)
+        parts.append(g)
+        csum = c if csum is None else csum + c
+    _assert_same(got, np.concatenate(parts))
+    assert np.array_equal(counts, csum)
+    idx = np.sort(np.random.default_rng(5).choice(n, 3000, replace=False))
+    exp = oracle.run_batch(oracle.Panel(d["sp5"], oracle.FRONT),
+                           oracle.Panel(d["sp27"], oracle.BACK), d["blob"], d["offsets"][idx],
+                           d["lengths"][idx], mode=2 if linked else 1, use_rc=not linked,
+                           threads=8)
+    _assert_same(got[idx], exp)
