@@ -3085,7 +3085,10 @@ __device__ __forceinline__ uint32_t pick_winner(const FinalArgs& F, uint32_t i, 
 // round-0-trimmed sequence: FRONT -> view[rstop:], BACK -> view[:rstart]) and queue it.
 // Block-stride over the reads (kFinalGrid blocks): the bin histogram is flushed once per block,
 // not once per 256 reads (one global atomic per bin and block, on a few dozen addresses).
-constexpr uint32_t kFinalGrid = 2048;
+#ifndef DMX_FINAL_GRID
+#define DMX_FINAL_GRID 2048
+#endif
+constexpr uint32_t kFinalGrid = DMX_FINAL_GRID;
 __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
     __shared__ unsigned int s_hist[2 * (kMaxAdapters + 1) + 1];
     __shared__ uint32_t s_nq, s_qbase;
