@@ -375,9 +375,15 @@ __device__ __forceinline__ bool viable_lb(int lbk, int lr, int o, int cost) {
 }
 
 // 16 view positions from view position p (may be negative or past the view: guard words).
+// Positions before -64 are read at -64: a view starts >= DMX_PACK_PAD nt into the buffer, so
+// that keeps the forward read inside it and the reverse read within the tail pad.  Callers take
+// such columns as free-start warm-up only, where any codes are safe.  The index screen of a 3'
+// panel at -e 0.3 starts up to m + k columns before a short view (a parity sweep, seed 46, ran
+// off the buffer there).
 __device__ __forceinline__ void fetch16s(const uint32_t* __restrict__ seq,
                                          const uint32_t* __restrict__ nmask, const TaskView& tv,
                                          int p, uint32_t& codes, uint32_t& nbits) {
+    p = max(p, -64);
     if (tv.strand == 0) {
         const uint64_t g = (uint64_t)((int64_t)tv.off + (int64_t)tv.start + p);
         codes = window32(seq, 2 * g);

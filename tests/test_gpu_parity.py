@@ -451,3 +451,29 @@ def test_large_batch_equals_sub_batches(ctx, config):
                            d["lengths"][idx], mode=2 if linked else 1, use_rc=not linked,
                            threads=8)
     _assert_same(got[idx], exp)
+
+
+def test_screen_far_before_short_views(ctx):
+    """The index screen of a 3' panel with a long shared prefix and suffix at -e 0.3 starts its
+    warm-up up to m + k columns before the view, more than the 64-nt head pad for a short first
+    read (a parity sweep, seed 46, faulted there): such positions are read at -64. Short and
+    empty reads first and last, both strands, vs the oracle."""
+    rng = np.random.default_rng(925)
+    pre, suf = rand_dna(rng, 12), rand_dna(rng, 21)
+    panel = [pre + rand_dna(rng, int(rng.integers(6, 28))) + suf for _ in range(15)]
+    seqs = ["", "A", "ACG", rand_dna(rng, 5)]
+    for _ in range(600):
+        s = rand_dna(rng, int(rng.integers(0, 160)))
+        if rng.random() < 0.5:
+            a = panel[int(rng.integers(len(panel)))]
+            cut = int(rng.integers(1, len(a) + 1))
+            s = s + a[:cut]
+        seqs.append(s)
+    seqs += ["", "T", rand_dna(rng, 7)]
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    for use_rc in (True, False):
+        exp = oracle.run_batch(oracle.Panel(panel, oracle.BACK, max_errors=0.3, min_overlap=3),
+                               None, blob, offs, lens, mode=0, use_rc=use_rc, threads=8)
+        ctx.set_panel(0, panel, lib.DMX_BACK | (lib.DMX_RC if use_rc else 0), 0.3, 3)
+        ctx.set_mode(lib.MODE_SINGLE)
+        _assert_same(ctx.run(lib.pack(blob, offs, lens)), exp)
