@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define DMX_ABI_VERSION 3
+#define DMX_ABI_VERSION 4
 
 /* Panel flags (dmx_set_panel.flags). */
 #define DMX_FRONT 0x01  /* -g ADAPTER: 5' adapter, Where.FRONT (prefix of adapter may be skipped at read start) */
@@ -82,6 +82,16 @@ int dmx_set_panel_mixed(dmx_ctx* ctx, int round, const char* const* seqs, const 
                         const int* wheres, int n_adapters, double max_errors, int min_overlap,
                         int rc);
 int dmx_set_mode(dmx_ctx* ctx, int mode);
+/* Host only (no GPU; tests): how far the kernels' gathers reach around a read view for the
+ * panel dmx_set_panel (wheres == NULL) or dmx_set_panel_mixed (wheres, flags & DMX_RC) would
+ * build from these arguments, in nt: out[0] before view position 0 as the kernels' warm-up
+ * formulas ask, out[1] after the clamp at -64 (positions before it are read at -64: warm-up
+ * columns, where any codes are safe), out[2] past the view end, out[3] / out[4] the guard
+ * needed below / above the packed words for the smallest offset and tail dmx_run accepts, out[5]
+ * the guard the device buffers carry.  Returns what dmx_set_panel would return: it refuses a
+ * panel with out[3] or out[4] > out[5] (DMX_E_UNSUPPORTED, out still filled). */
+int dmx_panel_reach(const char* const* seqs, const int* lens, const int* wheres, int n_adapters,
+                    double max_errors, int min_overlap, int flags, int32_t* out, int n_out);
 
 /* Host-side packer (no GPU needed): ASCII reads -> 2-bit codes (A=0,C=1,G=2,T=3, 16 nt per
  * little-endian u32 word) + 1-bit "no-match" mask (any non-ACGT byte, e.g. N).  Reads are laid
@@ -94,9 +104,13 @@ int dmx_pack(const uint8_t* ascii, const uint64_t* offsets, const uint32_t* lens
 
 /* Replaces: the per-read hot loop of one or more cutadapt runs (ReverseComplementer ->
  * AdapterCutter.best_match -> Adapter.match_to -> Aligner.locate, for every read) for the whole
- * input.  Synchronous: uploads, runs both rounds on the GPU, downloads `out`.  Any offsets >= 16
- * that fit n_words are accepted; batches in dmx_pack's layout above 1.5 chunks (DMX_RUN_CHUNK
- * reads, default 2^21) run as overlapped chunks, others in one shot (same results). */
+ * input.  Synchronous: uploads, runs both rounds on the GPU, downloads `out`.  Layout contract
+ * (checked; DMX_E_INVALID otherwise): every read has offsets[i] >= 16 and offsets[i] + lens[i]
+ * + 64 <= 16 * n_words, lens[i] < 2^30.  Reads may overlap or come in any order.  The device
+ * copies carry 1024 nt of zeroed guard on both sides, and every panel is checked to keep the
+ * kernels' gathers around a view inside it for such offsets (dmx_panel_reach).  Batches in
+ * dmx_pack's layout above 1.5 chunks (DMX_RUN_CHUNK reads, default 2^21) run as overlapped
+ * chunks, others in one shot (same results). */
 int dmx_run(dmx_ctx* ctx, const uint32_t* seq2b, const uint32_t* nmask, const uint64_t* offsets,
             const uint32_t* lens, size_t n_words, size_t n_reads, dmx_result* out);
 
@@ -177,7 +191,7 @@ int dmx_counts(dmx_ctx* ctx, uint64_t* out_counts, size_t n_out);
  * piece, adapter) tasks passed by the index screen r0, r1}, and flags
  * (bit0 cluster overflow, bit1 exactness-check violation, bit2 filter-window overflow, bit3
  * candidate-cell overflow, bit4 filter step bucket out of range (a build-knob invariant, see
- * kStepsPerBucket); must be 0). */
+ * kStepsPerBucket), bit5 a bounds violation (DMX_DEBUG_BOUNDS builds); must be 0). */
 int dmx_stats(dmx_ctx* ctx, float* stage_ms, int n_stage, uint64_t* counts, int n_counts,
               int* flags);
 
@@ -193,6 +207,14 @@ int dmx_stats(dmx_ctx* ctx, float* stage_ms, int n_stage, uint64_t* counts, int 
 #define DMX_DBG_CANDS1 4
 #define DMX_DBG_FLAGS 5
 int dmx_debug_fetch(dmx_ctx* ctx, int what, int round, void* out, size_t cap_bytes);
+/* DMX_DEBUG_BOUNDS builds only (dmx/libdmx_bounds.so; DMX_E_UNSUPPORTED otherwise): every gather
+ * of the packed batch and every winner-slot / item / result / count access of every kernel is
+ * checked against its buffer; a violation is skipped, and dmx_exec / dmx_run / dmx_chop_exec fail
+ * with DMX_E_STATE naming the kernel, buffer and index (dmx_last_error).  This self test launches
+ * one gather below the guard, one winner slot past its array and one valid gather; out3 receives
+ * {codes read below the guard (0), slot check result (0), a valid gather}; returns DMX_E_STATE
+ * with the first violation's message when the checks work. */
+int dmx_debug_bounds_selftest(dmx_ctx* ctx, uint32_t* out3);
 
 /* ---- Residual-primer failsafe: exact degenerate-motif location (`seqkit locate -d`) ---------
  * Replaces: `seqkit locate -d --pattern-file PRIMERS ENDS` in the failsafe of

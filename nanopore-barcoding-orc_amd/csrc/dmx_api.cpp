@@ -33,7 +33,7 @@ using namespace dmx;
 namespace {
 
 constexpr int kMinFilterLen = 10; // shortest shared suffix worth a filter pass
-constexpr size_t kGuardWords = 64; // zeroed words before/after the packed device buffers
+// kGuardWords (dmx_device.h): zeroed words before/after the packed device buffers
 
 uint8_t iupac_mask(char ch) {
     switch (ch) {
@@ -214,6 +214,38 @@ int grow_clusters(Ctx* c) {
 
 namespace dmx {
 
+// The kernels' reach around a view, per panel.  A 16-position gather at view
+// position p physically loads two aligned u32 words, i.e. view positions [p - 16, p + 32) on
+// either strand; whole-block loads (ViewBlocks: filter, verify) cover [p - 63, p + 64 s + 127]
+// for s 64-position stretches from p.  Per kernel, the first gather position before the view:
+//   filter, verify, window scan, scan, resolve, chop: >= 0 (their ranges start at column 0);
+//   index screen: x1 - 15 >= -(m_max - pre_len) - kf - 15 (the I_a band's warm-up, both the
+//     last-row test and the 3' last-column test; D' only lowers D there);
+//   edge bands: dx - H >= -(m + 7) (end cell (i, j) with j >= 0, H <= 7 diagonals);
+// and past the view end: ViewBlocks' in-flight block (<= 190 nt), fetch16 prefetches (<= 54).
+// Positions before -kViewReachPre are read at -kViewReachPre (fetch16s).  A read on strand 1
+// maps view positions past its end to nt before its offset, and positions before the view to
+// nt past its end, so both directions must fit either side of the buffer.
+PanelReach panel_reach(const HostPanel& hp, const DevPanel& dp) {
+    int m_max = 0;
+    bool band = true;
+    for (int a = 0; a < hp.n; ++a) {
+        m_max = std::max(m_max, (int)hp.ad[a].m);
+        band &= hp.ad[a].kk <= 7;
+    }
+    PanelReach r;
+    int pre = 63 + 16;   // ViewBlocks' floor to a block, fetch16's floor to a word
+    if (hp.screen) pre = std::max(pre, m_max - dp.pre_len + dp.kf + 15 + 16);
+    if (band) pre = std::max(pre, m_max + 7 + 16);
+    r.pre_raw = pre;
+    r.pre = std::min(pre, std::max(63 + 16, kViewReachPre + 16));
+    r.post = 63 + 64 + 63;   // ViewBlocks: the block after the last stretch's two, in flight
+    // strand 0: before the view -> before the offset; strand 1: before the view -> past the end
+    r.need_pre = std::max(r.pre, r.post) - kMinOffset;
+    r.need_post = std::max(r.pre, r.post) + 32 - kMinTail;   // (+ the 8-byte word pair)
+    return r;
+}
+
 int reset_counts(Ctx* c) {
     CK(hipSetDevice(c->device));
     const size_t nc = counts_size(c);
@@ -325,10 +357,13 @@ int dmx_set_panel_mixed(dmx_ctx* c, int round, const char* const* seqs, const in
                           DMX_FRONT | (rc ? DMX_RC : 0));
 }
 
-static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const int* lens,
-                          const int* wheres, int n, double max_errors, int min_overlap,
-                          int flags) {
-    if (!c || round < 0 || round > 1 || !seqs || !lens) return DMX_E_INVALID;
+// The host and device forms of a panel (parser.py / adapters.py rules above), the filter /
+// verification / screen blocks and the reach check; uses only c->err, c->no_filter, c->no_verify
+// (dmx_panel_reach runs it on a context that was never opened).
+static int build_panel(Ctx* c, const char* const* seqs, const int* lens, const int* wheres, int n,
+                       double max_errors, int min_overlap, int flags, HostPanel& hp,
+                       DevPanel& dp) {
+    if (!seqs || !lens) return DMX_E_INVALID;
     if (n <= 0 || n > kMaxAdapters) {
         c->err = "panel must hold 1..64 adapters";
         return DMX_E_INVALID;
@@ -341,7 +376,7 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
         c->err = "max_errors must be >= 0";
         return DMX_E_INVALID;
     }
-    HostPanel hp;
+    hp = HostPanel();
     hp.n = n;
     hp.n_orient = (flags & DMX_RC) ? 2 : 1;
     for (int a = 0; a < n; ++a) {
@@ -409,7 +444,6 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
                           : ((flags & DMX_FRONT) ? kFront : kBack);
     }
     hp.set = true;
-    DevPanel dp;
     memset(&dp, 0, sizeof(dp));
     dp.n_adapters = hp.n;
     dp.n_orient = hp.n_orient;
@@ -509,6 +543,29 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
             }
         }
     }
+    // Every gather of every kernel must stay inside the device guard words for every offset the
+    // loaders accept (>= kMinOffset nt, >= kMinTail nt before the end): the deepest warm-up
+    // before a view (index screen, edge bands), clamped at -kViewReachPre, and the block loads
+    // past it.  Adapters of <= 64 nt always fit; the check keeps it explicit.
+    hp.reach = panel_reach(hp, dp);
+    if (hp.reach.need_pre > kGuardNt || hp.reach.need_post > kGuardNt) {
+        c->err = "panel: the kernels' reach around a view (" + std::to_string(hp.reach.pre) +
+                 " nt before, " + std::to_string(hp.reach.post) +
+                 " after) exceeds the device guard";
+        return DMX_E_UNSUPPORTED;
+    }
+    for (int a = 0; a < n; ++a) dp.ad[a] = hp.ad[a];
+    return DMX_OK;
+}
+
+static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const int* lens,
+                          const int* wheres, int n, double max_errors, int min_overlap,
+                          int flags) {
+    if (!c || round < 0 || round > 1 || !seqs || !lens) return DMX_E_INVALID;
+    HostPanel hp;
+    DevPanel dp;
+    const int brc = build_panel(c, seqs, lens, wheres, n, max_errors, min_overlap, flags, hp, dp);
+    if (brc) return brc;
     c->panel[round] = hp;
     c->ring_small[round] = hp.ring_small;
     c->band_ok[round] = true;
@@ -518,7 +575,6 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
         kkmax = std::max(kkmax, (int)hp.ad[a].kk);
     }
     c->band_wide[round] = kkmax > 5;   // list 1 (costs 4..kk): 11 diagonals cover kk <= 5
-    for (int a = 0; a < n; ++a) dp.ad[a] = hp.ad[a];
     CK(hipSetDevice(c->device));
     CK(hipMemcpy(c->d_panel[round], &dp, sizeof(dp), hipMemcpyHostToDevice));
     return DMX_OK;
@@ -653,6 +709,37 @@ int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uin
     return load_impl(c, seq2b, m, offsets, lens, n_words, n_reads);
 }
 
+int dmx_panel_reach(const char* const* seqs, const int* lens, const int* wheres, int n,
+                    double max_errors, int min_overlap, int flags, int32_t* out, int n_out) {
+    if (!out || n_out < 6) return DMX_E_INVALID;
+    if (wheres) {   // dmx_set_panel_mixed's form
+        for (int a = 0; a < n; ++a)
+            if (wheres[a] != DMX_FRONT && wheres[a] != DMX_BACK) return DMX_E_INVALID;
+        flags = DMX_FRONT | (flags & DMX_RC);
+    }
+    Ctx tmp;   // never opened: build_panel reads only the A/B switches dmx_open would set
+    const char* nf = std::getenv("DMX_NO_FILTER");
+    tmp.no_filter = nf && nf[0] == '1';
+    const char* nv = std::getenv("DMX_NO_VERIFY");
+    tmp.no_verify = nv && nv[0] == '1';
+    HostPanel hp;
+    DevPanel dp;
+    PanelReach r;
+    const int rc = build_panel(&tmp, seqs, lens, wheres, n, max_errors, min_overlap, flags, hp, dp);
+    if (rc == DMX_OK) r = hp.reach;
+    else if (rc == DMX_E_UNSUPPORTED && hp.set) r = hp.reach;   // refused by the reach check
+    else return rc;
+    const int32_t v[6] = {r.pre_raw, r.pre, r.post, r.need_pre, r.need_post, kGuardNt};
+    for (int i = 0; i < 6; ++i) out[i] = v[i];
+    return rc;
+}
+
+int dmx_debug_bounds_selftest(dmx_ctx* c, uint32_t* out3) {
+    if (!c || !out3) return DMX_E_INVALID;
+    CK(hipSetDevice(c->device));
+    return bounds_selftest(c, out3);
+}
+
 int dmx_exec(dmx_ctx* c) {
     if (!c) return DMX_E_INVALID;
     if (!c->panel[0].set || (c->mode != DMX_MODE_SINGLE && !c->panel[1].set)) {
@@ -686,7 +773,7 @@ int dmx_exec(dmx_ctx* c) {
         if ((rc = launch_finalize(c, 1, st))) return rc;
     }
     c->executed = true;
-    return DMX_OK;
+    return bounds_check(c, "dmx_exec");   // DMX_DEBUG_BOUNDS builds only (else DMX_OK)
 }
 
 int dmx_sync(dmx_ctx* c) {

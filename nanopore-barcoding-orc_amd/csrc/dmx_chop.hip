@@ -83,8 +83,7 @@ static_assert(sizeof(dmx_chop_hit) == 16 && sizeof(dmx_chop_seg) == 16, "record 
 static_assert(sizeof(ChopLabel) % 8 == 0 && offsetof(ChopPanel, lab) % 8 == 0, "panel layout");
 
 struct ChopArgs {
-    const uint32_t* seq;
-    const uint32_t* nmask;
+    Packed pk;                 // the resident packed batch (+ bounds in DMX_DEBUG_BOUNDS builds)
     const uint64_t* offs;
     const uint32_t* lens;
     uint32_t n_reads;
@@ -184,7 +183,7 @@ __device__ __forceinline__ void chop_scan(const ChopArgs& A, const ChopLabel& L,
     uint32_t bstop = 0;
     for (uint32_t p = ws; p < send; p += 16) {
         uint32_t codes, nb;
-        fetch16(A.seq, A.nmask, off, n, 0u, 0u, p, codes, nb);
+        fetch16(A.pk, off, n, 0u, 0u, p, codes, nb);
         const uint32_t cnt = min(16u, send - p);
         uint64_t eqv[16];
 #pragma unroll
@@ -247,7 +246,7 @@ __device__ int chop_start(const ChopArgs& A, const ChopLabel& R, uint32_t read, 
     int start = -1;
     for (uint32_t t0 = 0; t0 < tmax; t0 += 16) {
         uint32_t codes, nb;
-        fetch16(A.seq, A.nmask, off, n, 1u, 0u, n - stop + t0, codes, nb);
+        fetch16(A.pk, off, n, 1u, 0u, n - stop + t0, codes, nb);
         const uint32_t cnt = min(16u, tmax - t0);
         for (uint32_t q = 0; q < cnt; ++q) {
             const uint64_t eq = R.peq[((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)];
@@ -860,11 +859,13 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
         s->blk_cap = nb;
     }
     size_t n_big = 0;
+    CHOP_CK(bounds_reset(c, st));
     for (;;) {
         CHOP_CK(hipMemsetAsync(s->d_ctr, 0, 4 * sizeof(unsigned long long), st));
         ChopArgs A;
-        A.seq = c->d_seq;
-        A.nmask = c->d_nmask;
+        A.pk.seq = c->d_seq;
+        A.pk.nmask = c->d_nmask;
+        A.pk.bd = make_bounds(c, kKerChop);
         A.offs = c->d_offs;
         A.lens = c->d_lens;
         A.n_reads = (uint32_t)n;
@@ -909,6 +910,7 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
             CHOP_CK(hipMemcpyAsync(s->d_ovf_base, base.data(), (no + 1) * 8,
                                    hipMemcpyHostToDevice, st));
             CHOP_CK(hipMemsetAsync(s->d_big_cnt, 0, (no + 1) * 4, st));
+            set_kid(A.pk.bd, kKerChopBig);
             hipLaunchKernelGGL(chop_big_kernel, dim3((uint32_t)no), dim3(kChopBlock), 0, st, A,
                                (const uint64_t*)s->d_ovf_base, s->d_big, s->d_big + s->big_cap,
                                s->d_big_cnt);
@@ -953,6 +955,7 @@ extern "C" int dmx_chop_exec(dmx_ctx* c, uint64_t* n_hits, uint64_t* n_segs) {
     }
     CHOP_CK(hipEventRecord(s->ev[3], st));
     CHOP_CK(hipEventSynchronize(s->ev[3]));
+    if (const int brc = bounds_check(c, "dmx_chop_exec")) return brc;
     hipEventElapsedTime(&s->ms[0], s->ev[0], s->ev[1]);
     hipEventElapsedTime(&s->ms[1], s->ev[2], s->ev[3]);
     s->n_hits = ctr[0];

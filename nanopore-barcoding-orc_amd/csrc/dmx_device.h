@@ -223,13 +223,86 @@ __host__ __device__ inline int key_adapter(uint64_t k) { return (int)((k >> 40) 
 __host__ __device__ inline uint64_t key_t(uint64_t k) { return k & ((1ull << 40) - 1); }
 
 // ---------------------------------------------------------------------------------------------
-// Packed read streams.  seq: 2 bits per nt (16 nt / u32, nt x at bits 2(x%16)); nmask: 1 bit per
-// nt (1 = not ACGT, never matches).  Buffers carry DMX_PACK_PAD (64) nt of padding on both ends
-// so a 32-bit window starting up to 16 nt before a read or ending past it stays in bounds.
+// Bounds of the device buffers.  Release builds: empty, every check is `true`.
+// DMX_DEBUG_BOUNDS builds (dmx/libdmx_bounds.so): every gather of the packed batch and every
+// slot / item / result / count access is checked against its buffer's extent, which the host
+// passes per launch; a violation is not performed (a read returns 0) but sets flag bit 32 and
+// records the first offender (kernel id, buffer id, index) in d_counters[24..27], so the call
+// fails naming the kernel instead of faulting.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t window32(const uint32_t* __restrict__ w, uint64_t bitpos) {
-    const uint64_t q = bitpos >> 5;
+enum BoundsBuf : uint32_t {
+    kBufSeq = 1, kBufMask = 2, kBufSlot = 3, kBufItem = 4, kBufRes = 5, kBufCount = 6,
+    kBufRead = 7, kBufLinked = 8, kBufCand = 9, kBufChop = 10
+};
+enum BoundsKernel : int32_t {
+    kKerFilter = 1, kKerVerify, kKerScreen, kKerScreen4, kKerWscan, kKerScan, kKerBand0,
+    kKerBand1, kKerSelectCand, kKerResolve, kKerSelect, kKerFin0, kKerFin1, kKerFin0L, kKerFin1L,
+    kKerFin2L, kKerChop, kKerChopBig, kKerChopStart, kKerSelfTest
+};
+constexpr int kBoundsRec = 24;     // d_counters[24..27]: kernel id + 1, buffer, index lo / hi
+
+struct Bounds {
+#ifdef DMX_DEBUG_BOUNDS
+    int64_t lo, hi;                // valid u32 word indices of d_seq / d_nmask (guards included)
+    uint64_t slots, items, reads, counts, linked;   // element counts of the other buffers
+    uint32_t* rec;                 // d_counters
+    int32_t kid;                   // the launch's kernel (BoundsKernel)
+#endif
+};
+
+// Is index i of buffer `buf` inside [lo, hi)?  Records the first violation.
+__device__ __forceinline__ bool bchk(const Bounds& b, int64_t i, int64_t lo, int64_t hi,
+                                     uint32_t buf) {
+#ifdef DMX_DEBUG_BOUNDS
+    if (i >= lo && i < hi) return true;
+    atomicOr(b.rec + 3, 32u);
+    if (atomicCAS(b.rec + kBoundsRec, 0u, (uint32_t)b.kid + 1u) == 0u) {
+        b.rec[kBoundsRec + 1] = buf;
+        b.rec[kBoundsRec + 2] = (uint32_t)(uint64_t)i;
+        b.rec[kBoundsRec + 3] = (uint32_t)((uint64_t)i >> 32);
+    }
+    return false;
+#else
+    (void)b, (void)i, (void)lo, (void)hi, (void)buf;
+    return true;
+#endif
+}
+#ifdef DMX_DEBUG_BOUNDS
+#define DMX_BOUND(bd, field, i, buf) bchk((bd), (int64_t)(i), 0, (int64_t)(bd).field, (buf))
+#else
+#define DMX_BOUND(bd, field, i, buf) true
+#endif
+
+// ---------------------------------------------------------------------------------------------
+// Packed read streams.  seq: 2 bits per nt (16 nt / u32, nt x at bits 2(x%16)); nmask: 1 bit per
+// nt (1 = not ACGT, never matches).  dmx_pack puts DMX_PACK_PAD (64) nt of padding at both ends,
+// and the device buffers carry kGuardWords (64) zeroed words on both sides (1024 nt of codes).
+// Every global position is a SIGNED nt index: a gather before the first read floors to a negative
+// word inside the guard (round 4's two faults were unsigned wraps of such positions).  The host
+// checks per panel that the deepest reach of any kernel before / after a view stays inside the
+// guard for every accepted offset (set_panel_impl, dmx_panel_reach).
+// ---------------------------------------------------------------------------------------------
+constexpr int kGuardWords = 64;        // zeroed u32 words before/after d_seq and d_nmask
+constexpr int kGuardNt = 16 * kGuardWords;   // guard of the codes buffer in nt (the mask's is 2x)
+constexpr int kMinOffset = 16;         // smallest read offset dmx_load / dmx_run accept
+constexpr int kMinTail = 64;           // nt every read keeps before the end of the packed words
+constexpr int kViewReachPre = 64;      // fetch16s: positions before -64 are read at -64
+
+struct Packed {
+    const uint32_t* seq;
+    const uint32_t* nmask;
+    Bounds bd;
+};
+
+__device__ __forceinline__ uint32_t window32(const uint32_t* __restrict__ w, int64_t bitpos,
+                                             const Bounds& bd, uint32_t buf) {
+    const int64_t q = bitpos >> 5;   // arithmetic shift: floor for negative positions
     const uint32_t sh = (uint32_t)bitpos & 31u;
+#ifdef DMX_DEBUG_BOUNDS
+    if (!bchk(bd, q, bd.lo, bd.hi - 1, buf)) return 0u;
+#else
+    (void)bd, (void)buf;
+#endif
 #ifdef DMX_WINDOW32_SPLIT   // A/B build: two 4-byte loads
     const uint64_t v = ((uint64_t)w[q + 1] << 32) | (uint64_t)w[q];
 #else
@@ -237,6 +310,13 @@ __device__ __forceinline__ uint32_t window32(const uint32_t* __restrict__ w, uin
     __builtin_memcpy(&v, w + q, 8);   // aligned address: one request instead of two)
 #endif
     return (uint32_t)(v >> sh);
+}
+// 16 codes (32 bits) and 32 no-match bits from global nt position g
+__device__ __forceinline__ uint32_t code32(const Packed& pk, int64_t g) {
+    return window32(pk.seq, 2 * g, pk.bd, kBufSeq);
+}
+__device__ __forceinline__ uint32_t mask32(const Packed& pk, int64_t g) {
+    return window32(pk.nmask, g, pk.bd, kBufMask);
 }
 
 // Reverse the order of the 16 2-bit fields of w.
@@ -248,18 +328,17 @@ __device__ __forceinline__ uint32_t rev_pairs(uint32_t w) {
 // 16 consecutive view positions starting at view position p: 2-bit codes (complemented on the
 // reverse strand) and the no-match bits.  `off`/`n`: the read's first nt and length; view
 // (strand, start).
-__device__ __forceinline__ void fetch16(const uint32_t* __restrict__ seq,
-                                        const uint32_t* __restrict__ nmask, uint64_t off,
-                                        uint32_t n, uint32_t strand, uint32_t start, uint32_t p,
+__device__ __forceinline__ void fetch16(const Packed& pk, uint64_t off, uint32_t n,
+                                        uint32_t strand, uint32_t start, uint32_t p,
                                         uint32_t& codes, uint32_t& nbits) {
     if (strand == 0) {
-        const uint64_t g = off + start + p;
-        codes = window32(seq, 2 * g);
-        nbits = window32(nmask, g) & 0xFFFFu;
-    } else {
-        const uint64_t b = off + (uint64_t)n - 1 - start - p - 15;   // lowest nt of the window
-        codes = ~rev_pairs(window32(seq, 2 * b));                    // complement = 3 - c
-        nbits = __brev(window32(nmask, b)) >> 16;
+        const int64_t g = (int64_t)off + start + p;
+        codes = code32(pk, g);
+        nbits = mask32(pk, g) & 0xFFFFu;
+    } else {   // lowest nt of the window
+        const int64_t b = (int64_t)off + (int64_t)n - 1 - start - (int64_t)p - 15;
+        codes = ~rev_pairs(code32(pk, b));                           // complement = 3 - c
+        nbits = __brev(mask32(pk, b)) >> 16;
     }
 }
 

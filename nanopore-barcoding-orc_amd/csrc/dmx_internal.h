@@ -14,6 +14,15 @@ namespace dmx {
 
 struct ChopState;   // read reorientation (dmx_chop.hip)
 
+// Reach of a panel's gathers around a view, in nt (panel_reach below).
+struct PanelReach {
+    int pre_raw = 0;     // before view position 0, as the kernels' formulas ask
+    int pre = 0;         // ... after the fetch16s clamp at -kViewReachPre
+    int post = 0;        // past the view end
+    int need_pre = 0;    // guard nt needed below the buffer for a read at offset kMinOffset
+    int need_post = 0;   // guard nt needed past n_words for reads keeping kMinTail nt of tail
+};
+
 struct HostPanel {
     bool screen = false;      // index screen usable (filter + verify, index blocks 1..32)
     int n = 0;
@@ -23,6 +32,7 @@ struct HostPanel {
     bool filter = false;
     bool verify = false;
     bool nonpos = false;      // an accepted match may score <= 0 (needs per-orientation winners)
+    PanelReach reach;
     DevAdapter ad[kMaxAdapters];
 };
 
@@ -92,7 +102,7 @@ struct Ctx {
     size_t item_cap = 0;                 // round-2 items of the current mode and batch
     size_t item_alloc = 0;               // entries allocated in d_items (>= item_cap)
     uint32_t* d_shard = nullptr;      // [kShLists][kShards] per-shard list counters (dmx_device.h)
-    uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows, [6+2r..] candidates, [10+r] verified windows, [16+4r..] diag
+    uint32_t* d_counters = nullptr;   // [0..1] clusters, [2] items, [3] flags, [4..5] windows, [6+2r..] candidates, [10+r] verified windows, [16+4r..] diag, [24..27] DMX_DEBUG_BOUNDS record
     unsigned long long* d_counts = nullptr;
     unsigned long long* d_linked = nullptr;
     Window* d_tasks = nullptr;           // index screen survivors (window piece of one adapter)
@@ -123,6 +133,28 @@ int launch_rebase_offsets(uint64_t* offs, uint32_t n, uint64_t g0, hipStream_t s
 // mask[idx[i] - base] = val[i] for the n staged exceptions at d_exc ([idx][val]); stream st
 int launch_mask_scatter(uint32_t* mask, const uint32_t* d_exc, uint32_t n, uint32_t base,
                         hipStream_t st);
+
+// DMX_DEBUG_BOUNDS builds (dmx_device.h Bounds): the extents of c's device buffers for a launch
+// of kernel `kid`; a reset of the violation record (d_counters[24..27]); the check after a run
+// (synchronises, and fails naming the kernel, buffer and index of the first violation).  In
+// release builds make_bounds is empty, set_kid / bounds_reset do nothing and bounds_check
+// returns DMX_OK without synchronising.
+Bounds make_bounds(const Ctx* c, int kid);
+inline void set_kid(Bounds& b, int kid) {
+#ifdef DMX_DEBUG_BOUNDS
+    b.kid = kid;
+#else
+    (void)b, (void)kid;
+#endif
+}
+hipError_t bounds_reset(Ctx* c, hipStream_t st);
+int bounds_check(Ctx* c, const char* where);
+
+// Deepest reach of the kernels' gathers around a view for panel `hp` (nt before position 0,
+// before and after the -kViewReachPre clamp, and past the view end), and the smallest guard
+// that covers them for every offset dmx_load / dmx_run accept.
+PanelReach panel_reach(const HostPanel& hp, const DevPanel& dp);
+int bounds_selftest(Ctx* c, uint32_t* host_out);   // dmx_debug_bounds_selftest
 
 // Where a batch's no-match mask comes from: the dense bitmap (1 bit per nt) of dmx_pack, or its
 // nonzero words as sorted (index, value) exceptions (dmx_mask_exceptions, dmx_run_sparse).

@@ -15,8 +15,7 @@ namespace dmx {
 // shared helpers
 // ---------------------------------------------------------------------------------------------
 struct RoundArgs {
-    const uint32_t* seq;
-    const uint32_t* nmask;
+    Packed pk;                   // the resident packed batch (+ bounds in DMX_DEBUG_BOUNDS builds)
     const uint64_t* offs;
     const uint32_t* lens;
     const DevPanel* panel;
@@ -60,9 +59,20 @@ struct TaskView {
     int o, a;
 };
 
+// An empty view at the first valid offset (DMX_DEBUG_BOUNDS builds: an item or read index out of
+// range; the violation is recorded and the task scans nothing).
+__device__ __forceinline__ bool empty_view(TaskView& tv) {
+    tv.read = 0;
+    tv.n = tv.start = tv.len = tv.strand = 0;
+    tv.off = kMinOffset;
+    tv.o = tv.a = 0;
+    return false;
+}
+
 __device__ __forceinline__ bool task_view(const RoundArgs& R, uint32_t item, int sub, int A,
                                           TaskView& tv) {
     if (R.items) {
+        if (!DMX_BOUND(R.pk.bd, items, item, kBufItem)) return empty_view(tv);
         const ItemView v = R.items[item];
         tv.read = v.read;
         tv.start = v.start;
@@ -87,6 +97,7 @@ __device__ __forceinline__ bool task_view(const RoundArgs& R, uint32_t item, int
             tv.a = sub;
         }
     }
+    if (!DMX_BOUND(R.pk.bd, reads, tv.read, kBufRead)) return empty_view(tv);
     tv.n = R.lens[tv.read];
     tv.off = R.offs[tv.read];
     if (tv.o) {   // reverse complement of the view (strand s, start st, len l) of a read of n nt
@@ -210,15 +221,15 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
 
     uint32_t p0 = js;
     uint32_t ncodes, nnb, ncodes2 = 0, nnb2 = 0;   // the next two chunks, in flight
-    fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb);
+    fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb);
     if (p0 + 16 < jhi)
-        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes2, nnb2);
+        fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes2, nnb2);
     for (; p0 + 16 <= jhi; p0 += 16) {
         const uint32_t codes = ncodes, nb = nnb;
         ncodes = ncodes2;
         nnb = nnb2;
         if (p0 + 32 < jhi)
-            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 32, ncodes2, nnb2);
+            fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 32, ncodes2, nnb2);
 #pragma unroll
         for (int q = 0; q < 16; ++q) DMX_SCAN_STEP(q)
     }
@@ -374,25 +385,25 @@ __device__ __forceinline__ bool viable_lb(int lbk, int lr, int o, int cost) {
     return beats_lb(lbk, lr - 2 * cost, o, cost);
 }
 
-// 16 view positions from view position p (may be negative or past the view: guard words).
-// Positions before -64 are read at -64: a view starts >= DMX_PACK_PAD nt into the buffer, so
-// that keeps the forward read inside it and the reverse read within the tail pad.  Callers take
-// such columns as free-start warm-up only, where any codes are safe.  The index screen of a 3'
-// panel at -e 0.3 starts up to m + k columns before a short view (a parity sweep, seed 46, ran
-// off the buffer there).
-__device__ __forceinline__ void fetch16s(const uint32_t* __restrict__ seq,
-                                         const uint32_t* __restrict__ nmask, const TaskView& tv,
-                                         int p, uint32_t& codes, uint32_t& nbits) {
-    p = max(p, -64);
+// 16 view positions from view position p (may be negative or past the view: pads and guard
+// words).  Positions before -kViewReachPre are read at -kViewReachPre, so a gather never starts
+// more than kViewReachPre + 15 nt before a view, or ends more than kViewReachPre + 32 nt past
+// it on the reverse strand; the host checks per panel that this stays inside the device guard
+// for every offset dmx_load / dmx_run accept (dmx_panel_reach).  Callers take columns before the
+// view as free-start warm-up only, where any codes are safe (the index screen of a 3' panel at
+// -e 0.3 starts up to m + k columns before a short view).  The positions are signed: the seed-46
+// fault of round 4 was an unsigned wrap of such a position below the buffer.
+__device__ __forceinline__ void fetch16s(const Packed& pk, const TaskView& tv, int p,
+                                         uint32_t& codes, uint32_t& nbits) {
+    p = max(p, -kViewReachPre);
     if (tv.strand == 0) {
-        const uint64_t g = (uint64_t)((int64_t)tv.off + (int64_t)tv.start + p);
-        codes = window32(seq, 2 * g);
-        nbits = window32(nmask, g) & 0xFFFFu;
+        const int64_t g = (int64_t)tv.off + (int64_t)tv.start + p;
+        codes = code32(pk, g);
+        nbits = mask32(pk, g) & 0xFFFFu;
     } else {
-        const uint64_t b = (uint64_t)((int64_t)tv.off + (int64_t)tv.n - 1 - (int64_t)tv.start -
-                                      p - 15);
-        codes = ~rev_pairs(window32(seq, 2 * b));
-        nbits = __brev(window32(nmask, b)) >> 16;
+        const int64_t b = (int64_t)tv.off + (int64_t)tv.n - 1 - (int64_t)tv.start - p - 15;
+        codes = ~rev_pairs(code32(pk, b));
+        nbits = __brev(mask32(pk, b)) >> 16;
     }
 }
 
@@ -572,15 +583,15 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
 
     uint32_t p0 = js;
     uint32_t ncodes, nnb, ncodes2 = 0, nnb2 = 0;   // the next two chunks, in flight
-    fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb);
+    fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb);
     if (p0 + 16 < jhi)
-        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes2, nnb2);
+        fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes2, nnb2);
     for (; p0 + 16 <= jhi; p0 += 16) {
         const uint32_t codes = ncodes, nb = nnb;
         ncodes = ncodes2;
         nnb = nnb2;
         if (p0 + 32 < jhi)
-            fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 32, ncodes2, nnb2);
+            fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 32, ncodes2, nnb2);
         if (segset && p0 + 16 >= seg + 64) {   // this chunk could overflow the 64-bit segment
             flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
             segset = false;
@@ -761,7 +772,8 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
         else
             lb = scan_task(R, st, tv, item, sub, s_peq + tv.a, A, R.panel->ad[tv.a],
                            s_acc + 72 * tv.a, s_pacc + 72 * tv.a, 0, true, 1, tv.len, true);
-        if (lb > 0) atomicMax(&R.lb[slot_of(R, item, sub)], lb);
+        const uint32_t slot = slot_of(R, item, sub);
+        if (lb > 0 && DMX_BOUND(R.pk.bd, slots, slot, kBufSlot)) atomicMax(&R.lb[slot], lb);
     }
     if constexpr (BAND) {
         sink.st[0].flush();
@@ -795,8 +807,19 @@ struct ViewBlocks {
     const uint2* np;
     int64_t nxt;                 // the next block to load
     bool rev;
+#ifdef DMX_DEBUG_BOUNDS
+    Bounds bd;
+#endif
 
     __device__ __forceinline__ void load(int k, int64_t b) {
+#ifdef DMX_DEBUG_BOUNDS
+        if (!bchk(bd, 4 * b, bd.lo, bd.hi - 3, kBufSeq) ||
+            !bchk(bd, 2 * b, bd.lo, bd.hi - 1, kBufMask)) {
+            for (int x = 0; x < 4; ++x) cw[4 * k + x] = 0u;
+            nw[2 * k] = nw[2 * k + 1] = 0u;
+            return;
+        }
+#endif
         const uint4 c4 = sp[b];
         cw[4 * k + 0] = c4.x;
         cw[4 * k + 1] = c4.y;
@@ -813,8 +836,11 @@ struct ViewBlocks {
                               : (int64_t)tv.off + tv.start + p;
         const int64_t blk = g >> 6;               // floor: the buffers carry guard words
         const uint32_t sh = (uint32_t)(g & 63);
-        sp = reinterpret_cast<const uint4*>(R.seq);
-        np = reinterpret_cast<const uint2*>(R.nmask);
+        sp = reinterpret_cast<const uint4*>(R.pk.seq);
+        np = reinterpret_cast<const uint2*>(R.pk.nmask);
+#ifdef DMX_DEBUG_BOUNDS
+        bd = R.pk.bd;
+#endif
         load(0, blk);
         load(1, blk + 1);
         nxt = rev ? blk - 1 : blk + 2;
@@ -1661,14 +1687,14 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
                 tv.o = w.o;
                 tv.a = a;
                 uint32_t c0 = 0, n0 = 0, c1 = 0, n1 = 0;   // two chunks in flight
-                if (nch > 0) fetch16s(R.seq, R.nmask, tv, jb, c0, n0);
-                if (nch > 1) fetch16s(R.seq, R.nmask, tv, jb + 16, c1, n1);
+                if (nch > 0) fetch16s(R.pk, tv, jb, c0, n0);
+                if (nch > 1) fetch16s(R.pk, tv, jb + 16, c1, n1);
                 for (int k = 0; k < nch && !pass; ++k) {
                     const int p0 = jb + 16 * k;
                     const uint32_t codes = c0, nb = n0;
                     c0 = c1;
                     n0 = n1;
-                    if (k + 2 < nch) fetch16s(R.seq, R.nmask, tv, p0 + 32, c1, n1);
+                    if (k + 2 < nch) fetch16s(R.pk, tv, p0 + 32, c1, n1);
                     // this chunk's columns p0+1 .. p0+16: the threshold of the regions it touches
                     // and the first column counted (earlier ones are warm-up)
                     const bool inR = rows && p0 + 16 >= xr_lo && p0 + 1 <= xrh;
@@ -1976,14 +2002,14 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                 const char* qb = reinterpret_cast<const char*>(s_q);
                 const uint32_t q8 = 8u * (uint32_t)q;   // the lane's quad within a code row
                 uint32_t c0 = 0, n0 = 0, c1 = 0, n1 = 0;   // two chunks in flight
-                if (nch > 0) fetch16s(R.seq, R.nmask, tv, jb, c0, n0);
-                if (nch > 1) fetch16s(R.seq, R.nmask, tv, jb + 16, c1, n1);
+                if (nch > 0) fetch16s(R.pk, tv, jb, c0, n0);
+                if (nch > 1) fetch16s(R.pk, tv, jb + 16, c1, n1);
                 for (int kc = 0; kc < nch && (need & ~pass_m); ++kc) {
                     const int p0 = jb + 16 * kc;
                     const uint32_t codes = c0, nb = n0;
                     c0 = c1;
                     n0 = n1;
-                    if (kc + 2 < nch) fetch16s(R.seq, R.nmask, tv, p0 + 32, c1, n1);
+                    if (kc + 2 < nch) fetch16s(R.pk, tv, p0 + 32, c1, n1);
                     const bool inR = rows && p0 + 16 >= xr_lo && p0 + 1 <= xrh;
                     const bool inE = lastc && p0 + 16 >= xe_lo;
                     const int qlo = min(inR ? xr_lo : (1 << 30), inE ? xe_lo : (1 << 30)) - p0 - 1;
@@ -2122,7 +2148,8 @@ __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, 
     else
         lb = scan_task(R, st, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
                        s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2, w.lastcol != 0);
-    if (lb > 0) atomicMax(&R.lb[slot_of(R, w.item, sub)], lb);
+    const uint32_t slot = slot_of(R, w.item, sub);
+    if (lb > 0 && DMX_BOUND(R.pk.bd, slots, slot, kBufSlot)) atomicMax(&R.lb[slot], lb);
 }
 
 // Occupancy floor for the window scan (register budget 512 / waves): at 129 VGPRs the compiler
@@ -2298,8 +2325,7 @@ struct PeqRegs {
 
 template <int RING>
 struct Walker {
-    const uint32_t* seq;
-    const uint32_t* nmask;
+    Packed pk;
     uint32_t* flags;
     TaskView tv;
     PeqRegs peq;
@@ -2336,7 +2362,7 @@ struct Walker {
             const int p = j - 1;              // view position of column j's character
             if (p < cbase) {
                 cbase = max(p - 15, 0);
-                fetch16(seq, nmask, tv.off, tv.n, tv.strand, tv.start, (uint32_t)cbase, codes, nb);
+                fetch16(pk, tv.off, tv.n, tv.strand, tv.start, (uint32_t)cbase, codes, nb);
             }
             const int sh = p - cbase;
             const uint32_t code = ((codes >> (2 * sh)) & 3u) | (((nb >> sh) & 1u) << 2);
@@ -2399,6 +2425,7 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
          ci += gridDim.x * kResolveBlock) {
         const Cluster c = R.cl[ci];
         const uint32_t slot = slot_of(R, c.item, c.sub);
+        if (!DMX_BOUND(R.pk.bd, slots, slot, kBufSlot)) continue;
         const int lbk = R.lb[slot];
         const int lbs = lb_score(lbk);                // slot's best score is >= lbs
         Outcome out;
@@ -2429,7 +2456,7 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
         rp[0] = pv;                       // slot(js) = 0
         rm[0] = mv;
 
-        const Walker<RING> W{R.seq, R.nmask, R.flags, tv, peq, rp, rm, js, real, front};
+        const Walker<RING> W{R.pk, R.flags, tv, peq, rp, rm, js, real, front};
         bool found = false;
         int bs = 0, bc = 0, bo = 0;
         uint64_t bt = 0;
@@ -2480,11 +2507,11 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
             since = 0;
         };
         uint32_t ncodes, nnb;             // next chunk, prefetched one chunk ahead
-        fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, (uint32_t)js, ncodes, nnb);
+        fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, (uint32_t)js, ncodes, nnb);
         for (uint32_t p0 = (uint32_t)js; p0 < c.j2; p0 += 16) {
             const uint32_t codes = ncodes, nb = nnb;
             if (p0 + 16 < c.j2)
-                fetch16(R.seq, R.nmask, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes, nnb);
+                fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes, nnb);
             const uint32_t cnt = min(16u, c.j2 - p0);
             for (uint32_t q = 0; q < cnt; ++q) {
                 const uint32_t code = ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
@@ -2538,8 +2565,8 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
 //   diagonal if the characters match or cost(diag) <= min(up, left); else up (insertion) if
 //   cost(up) <= cost(left); else left.  EDGE: the band reaches column 0 or beyond the view end.
 template <int W, bool EDGE>
-__device__ __forceinline__ void band_dp2(const uint8_t* rm, const uint32_t* seq,
-                                         const uint32_t* nmask, const TaskView& tv, bool front,
+__device__ __forceinline__ void band_dp2(const uint8_t* rm, const Packed& pk,
+                                         const TaskView& tv, bool front,
                                          int ie, int je, int& cost, int& origin, int& score) {
     constexpr int H = W / 2;
     constexpr int INF = 1 << 20;
@@ -2556,9 +2583,9 @@ __device__ __forceinline__ void band_dp2(const uint8_t* rm, const uint32_t* seq,
     // three 16-code words (w0 current, w1 next, w2 prefetched) advancing 16 rows at a time
     int base = dx - H;
     uint32_t w0, n0, w1, n1, w2, n2;
-    fetch16s(seq, nmask, tv, base, w0, n0);
-    fetch16s(seq, nmask, tv, base + 16, w1, n1);
-    fetch16s(seq, nmask, tv, base + 32, w2, n2);
+    fetch16s(pk, tv, base, w0, n0);
+    fetch16s(pk, tv, base + 16, w1, n1);
+    fetch16s(pk, tv, base + 32, w2, n2);
     int o = 0;
     uint32_t rnext = rm[0];           // rm[i * kMaxAdapters]: row i's match mask (row-major table)
     for (int i = 1; i <= ie; ++i) {
@@ -2569,7 +2596,7 @@ __device__ __forceinline__ void band_dp2(const uint8_t* rm, const uint32_t* seq,
             n1 = n2;
             base += 16;
             // the band's last cell reads view position dx - H + ie + W - 2: no fetch past it
-            if (base + 32 <= dx - H + ie + W - 2) fetch16s(seq, nmask, tv, base + 32, w2, n2);
+            if (base + 32 <= dx - H + ie + W - 2) fetch16s(pk, tv, base + 32, w2, n2);
             o = 0;
         }
         const uint32_t codes = o ? __builtin_amdgcn_alignbit(w1, w0, 2 * o) : w0;
@@ -2634,8 +2661,8 @@ __device__ __forceinline__ uint32_t spread_even(uint32_t x) {
 // smaller cost.  Mismatches for a whole row: the row's code replicated to every 2-bit field,
 // XORed with the 16 read codes; a field is nonzero where they differ (read N: never a match).
 template <int W>
-__device__ __forceinline__ void band_dp_fast(const uint8_t* rm, const uint32_t* seq,
-                                             const uint32_t* nmask, const TaskView& tv, int ie,
+__device__ __forceinline__ void band_dp_fast(const uint8_t* rm, const Packed& pk,
+                                             const TaskView& tv, int ie,
                                              int je, int& cost, int& origin, int& score) {
     static_assert(W <= 15, "origin index: 4 bits");
     constexpr int H = W / 2;
@@ -2647,9 +2674,9 @@ __device__ __forceinline__ void band_dp_fast(const uint8_t* rm, const uint32_t* 
     for (int k = 0; k < W; ++k) S[k] = (uint32_t)k << 3;   // row 0: free start, cost 0
     int base = dx - H;
     uint32_t w0, n0, w1, n1, w2, n2;
-    fetch16s(seq, nmask, tv, base, w0, n0);
-    fetch16s(seq, nmask, tv, base + 16, w1, n1);
-    fetch16s(seq, nmask, tv, base + 32, w2, n2);
+    fetch16s(pk, tv, base, w0, n0);
+    fetch16s(pk, tv, base + 16, w1, n1);
+    fetch16s(pk, tv, base + 32, w2, n2);
     n0 = spread_even(n0);
     n1 = spread_even(n1);
     int o = 0;
@@ -2661,7 +2688,7 @@ __device__ __forceinline__ void band_dp_fast(const uint8_t* rm, const uint32_t* 
             w1 = w2;
             n1 = spread_even(n2);
             base += 16;
-            if (base + 32 <= dx - H + ie + W - 2) fetch16s(seq, nmask, tv, base + 32, w2, n2);
+            if (base + 32 <= dx - H + ie + W - 2) fetch16s(pk, tv, base + 32, w2, n2);
             o = 0;
         }
         const uint32_t codes = o ? __builtin_amdgcn_alignbit(w1, w0, 2 * o) : w0;
@@ -2691,23 +2718,23 @@ __device__ __forceinline__ void band_dp_fast(const uint8_t* rm, const uint32_t* 
 // 2c + 1 diagonals for its largest cost c (wave-uniform branch; H >= c keeps the band exact).
 template <int C, int CMAX, bool EDGE>
 __device__ __forceinline__ void band_dp_cost(int wc, bool fast, const uint8_t* rm,
-                                             const uint32_t* seq, const uint32_t* nmask,
+                                             const Packed& pk,
                                              const TaskView& tv, bool front, int ie, int je,
                                              int& cost, int& origin, int& score) {
     if constexpr (C < CMAX) {
         if (wc > C) {
-            band_dp_cost<C + 1, CMAX, EDGE>(wc, fast, rm, seq, nmask, tv, front, ie, je, cost,
+            band_dp_cost<C + 1, CMAX, EDGE>(wc, fast, rm, pk, tv, front, ie, je, cost,
                                              origin, score);
             return;
         }
     }
     if constexpr (!EDGE) {
         if (fast) {   // block-uniform
-            band_dp_fast<2 * C + 1>(rm, seq, nmask, tv, ie, je, cost, origin, score);
+            band_dp_fast<2 * C + 1>(rm, pk, tv, ie, je, cost, origin, score);
             return;
         }
     }
-    band_dp2<2 * C + 1, EDGE>(rm, seq, nmask, tv, front, ie, je, cost, origin, score);
+    band_dp2<2 * C + 1, EDGE>(rm, pk, tv, front, ie, je, cost, origin, score);
 }
 
 // Band kernel over one candidate list (costs CMIN..CMAX; cost-0 cells need no DP).  Every block
@@ -2801,6 +2828,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                 const uint32_t cj = s_sorted[threadIdx.x];
                 const Cand c = cl[cj];
                 const uint32_t slot = slot_of(R, c.item, c.sub);
+                const bool slot_in = DMX_BOUND(R.pk.bd, slots, slot, kBufSlot);
                 const int cst = c.cost, iend = c.iend;
                 const int j = (int)c.j;
                 const DevAdapter& ad = P->ad[c.a];
@@ -2823,15 +2851,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #endif
                 if (e == 0)
                     band_dp_cost<CMIN == 0 ? 1 : CMIN, CMAX, false>(
-                        wc, fast, s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend, j, c2,
+                        wc, fast, s_rm + c.a, R.pk, tv, ad.where == kFront, iend, j, c2,
                         origin, score);
                 else
                     band_dp_cost<CMIN == 0 ? 1 : CMIN, CMAX, true>(
-                        wc, fast, s_rm + c.a, R.seq, R.nmask, tv, ad.where == kFront, iend, j, c2,
+                        wc, fast, s_rm + c.a, R.pk, tv, ad.where == kFront, iend, j, c2,
                         origin, score);
                 if (c2 != cst) atomicOr(R.flags, 2u);    // band / scan disagreement: bug
                 const int lr = iend + (origin < 0 ? origin : 0);
-                if (lr >= 0 && cst <= (int)ad.acc[lr]) {
+                if (slot_in && lr >= 0 && cst <= (int)ad.acc[lr]) {
                     Outcome out;
                     out.key = make_key(score, c.o, cst, c.a, t);
                     out.origin = origin;
@@ -2850,6 +2878,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             const uint32_t ci = sm.phys(ti);
             const Cand c = cl[ci];
             const uint32_t slot = slot_of(R, c.item, c.sub);
+            const bool slot_in = DMX_BOUND(R.pk.bd, slots, slot, kBufSlot);
             const int cost = c.cost, iend = c.iend;
             const int j = (int)c.j;
             const uint64_t t = iend == P->ad[c.a].m ? (uint64_t)j : (uint64_t)c.len + 1 + iend;
@@ -2859,7 +2888,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             out.pad = 0;
             const int lrmax = min(iend, j + cost);
             const int ub = lrmax - 2 * cost;
-            if (viable_lb(R.lb[slot], lrmax, c.o, cost) &&
+            if (slot_in && viable_lb(R.lb[slot], lrmax, c.o, cost) &&
                 make_key(ub, c.o, cost, c.a, t) <= R.winner[slot]) {
                 if (cost == 0) {              // exact: the pointer chain is the pure diagonal
                     const int origin = j - iend;
@@ -2907,6 +2936,7 @@ __global__ void select_cand_kernel(RoundArgs R) {
             const Outcome o = R.cand_out[list][ci];
             if (o.key == ~0ull) continue;
             const uint32_t slot = (uint32_t)o.pad;   // band_cand_kernel stores the cell's slot
+            if (!DMX_BOUND(R.pk.bd, slots, slot, kBufSlot)) continue;
             if (R.winner[slot] == o.key) R.origin[slot] = o.origin;
         }
     }
@@ -2921,6 +2951,7 @@ __global__ void select_kernel(RoundArgs R) {
         if (o.key == ~0ull) continue;
         const Cluster c = R.cl[ci];
         const uint32_t slot = slot_of(R, c.item, c.sub);
+        if (!DMX_BOUND(R.pk.bd, slots, slot, kBufSlot)) continue;
         if (R.winner[slot] == o.key) R.origin[slot] = o.origin;
     }
 }
@@ -2973,6 +3004,7 @@ struct FinalArgs {
     const unsigned long long* winner0;   // per (read, pair) front winners
     const int32_t* origin0;
     unsigned long long* linked_best;     // per read: best pair key
+    Bounds bd;                           // DMX_DEBUG_BOUNDS: extents of the buffers above
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -2988,7 +3020,9 @@ __global__ __launch_bounds__(256) void finalize0_linked_kernel(FinalArgs F) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t nmine = 0, qi = 0;
     uint32_t n = 0;
-    if (r < F.n_reads) {
+    if (r < F.n_reads && DMX_BOUND(F.bd, reads, r, kBufRes) &&
+        DMX_BOUND(F.bd, linked, r, kBufLinked) &&
+        DMX_BOUND(F.bd, slots, (size_t)r * F.A0 + F.A0 - 1, kBufSlot)) {
         dmx_result out;
         out.bin1 = out.bin2 = -1;
         out.rc1 = out.rc2 = 0;
@@ -3020,7 +3054,8 @@ __global__ __launch_bounds__(256) void finalize0_linked_kernel(FinalArgs F) {
             v.only_adapter = (int16_t)a;
             v.start = (uint32_t)m.rstop;
             v.len = n - (uint32_t)m.rstop;
-            F.items[idx++] = v;
+            if (DMX_BOUND(F.bd, items, idx, kBufItem)) F.items[idx] = v;
+            ++idx;
         }
     }
 }
@@ -3028,10 +3063,12 @@ __global__ __launch_bounds__(256) void finalize0_linked_kernel(FinalArgs F) {
 __global__ __launch_bounds__(256) void finalize1_linked_kernel(FinalArgs F) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= *F.n_items) return;
+    if (!DMX_BOUND(F.bd, items, i, kBufItem) || !DMX_BOUND(F.bd, slots, i, kBufSlot)) return;
     const ItemView v = F.items[i];
     const uint64_t kb = F.winner[i];
     if (kb == ~0ull) return;
     const int a = v.only_adapter;
+    if (!DMX_BOUND(F.bd, linked, v.read, kBufLinked)) return;
     const uint64_t kf = F.winner0[(size_t)v.read * F.A0 + a];
     const int sum = key_score(kf) + key_score(kb);
     const int err = key_cost(kf) + key_cost(kb);
@@ -3047,11 +3084,14 @@ __global__ __launch_bounds__(256) void finalize2_linked_kernel(FinalArgs F) {
     // block-stride (kFinalGrid blocks): one flush of the pair histogram per block
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < F.n_reads;
          r += gridDim.x * blockDim.x) {
-        const uint64_t ck = F.linked_best[r];
+        const uint64_t ck = DMX_BOUND(F.bd, linked, r, kBufLinked) ? F.linked_best[r] : ~0ull;
         int b = -1;
         if (ck != ~0ull) {
             const uint32_t i = (uint32_t)(ck & ((1ull << 38) - 1));
             const int a = (int)((ck >> 38) & 255);
+            if (!DMX_BOUND(F.bd, items, i, kBufItem) || !DMX_BOUND(F.bd, slots, i, kBufSlot) ||
+                !DMX_BOUND(F.bd, reads, r, kBufRes))
+                continue;
             const ItemView v = F.items[i];
             dmx_result& out = F.res[r];
             int aa, o;
@@ -3065,7 +3105,8 @@ __global__ __launch_bounds__(256) void finalize2_linked_kernel(FinalArgs F) {
     }
     __syncthreads();
     for (int x = threadIdx.x; x <= F.A0; x += blockDim.x)
-        if (s_hist[x]) atomicAdd(&F.counts[x * (F.A0 + 1) + x], (unsigned long long)s_hist[x]);
+        if (s_hist[x] && DMX_BOUND(F.bd, counts, x * (F.A0 + 1) + x, kBufCount))
+            atomicAdd(&F.counts[x * (F.A0 + 1) + x], (unsigned long long)s_hist[x]);
 }
 
 // The winning key of slot base `i` and its orientation.  With one slot per orientation,
@@ -3075,6 +3116,11 @@ __global__ __launch_bounds__(256) void finalize2_linked_kernel(FinalArgs F) {
 // and unmatched).  Returns the index of the chosen slot.
 __device__ __forceinline__ uint32_t pick_winner(const FinalArgs& F, uint32_t i, uint64_t& key,
                                                 int& o) {
+    if (!DMX_BOUND(F.bd, slots, F.oslot ? 2 * (uint64_t)i + 1 : i, kBufSlot)) {
+        key = ~0ull;
+        o = 0;
+        return 0;
+    }
     if (!F.oslot) {
         key = F.winner[i];
         o = key != ~0ull ? key_orient(key) : 0;
@@ -3107,7 +3153,7 @@ __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
         const uint32_t r = base + threadIdx.x;
         ItemView v;
         uint32_t qi = ~0u;             // this read's slot in the block's share of the item list
-        if (r < F.n_reads) {
+        if (r < F.n_reads && DMX_BOUND(F.bd, reads, r, kBufRes)) {
             dmx_result out;
             out.bin1 = -1;
             out.bin2 = -1;
@@ -3154,7 +3200,7 @@ __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
             s_nq = 0;
         }
         __syncthreads();
-        if (qi != ~0u) F.items[s_qbase + qi] = v;
+        if (qi != ~0u && DMX_BOUND(F.bd, items, s_qbase + qi, kBufItem)) F.items[s_qbase + qi] = v;
     }
     // reads taken reverse-complemented: one LDS atomic per wave
     n_rc = wave_sum(n_rc);
@@ -3165,8 +3211,9 @@ __global__ __launch_bounds__(256) void finalize0_kernel(FinalArgs F) {
     for (int x = threadIdx.x; x < nh + 1; x += blockDim.x) {
         const unsigned int v = s_hist[x];
         if (!v) continue;
-        if (x == nh) atomicAdd(&F.counts[ncounts], (unsigned long long)v);
-        else atomicAdd(&F.counts[x * stride1], (unsigned long long)v);
+        const int ix = x == nh ? ncounts : x * stride1;
+        if (DMX_BOUND(F.bd, counts, ix, kBufCount))
+            atomicAdd(&F.counts[ix], (unsigned long long)v);
     }
 }
 
@@ -3180,7 +3227,9 @@ __global__ __launch_bounds__(256) void finalize1_kernel(FinalArgs F) {
     uint32_t n_rc = 0;
     // block-stride (kFinalGrid blocks): one flush of the (bin1, bin2) histogram per block
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n_items; i += gridDim.x * 256u) {
+        if (!DMX_BOUND(F.bd, items, i, kBufItem)) break;
         const ItemView v = F.items[i];
+        if (!DMX_BOUND(F.bd, reads, v.read, kBufRes)) continue;
         dmx_result& out = F.res[v.read];
         uint64_t key;
         int o;
@@ -3201,7 +3250,9 @@ __global__ __launch_bounds__(256) void finalize1_kernel(FinalArgs F) {
     __syncthreads();
     for (int x = threadIdx.x; x < nbins + 1; x += blockDim.x) {
         const unsigned int c = s_hist2[x];
-        if (c) atomicAdd(&F.counts[x == nbins ? nbins + 1 : x], (unsigned long long)c);
+        const int ix = x == nbins ? nbins + 1 : x;
+        if (c && DMX_BOUND(F.bd, counts, ix, kBufCount))
+            atomicAdd(&F.counts[ix], (unsigned long long)c);
     }
 }
 
@@ -3231,10 +3282,114 @@ static bool debug_sync() {
         }                                                                                     \
     } while (0)
 
+Bounds make_bounds(const Ctx* c, int kid) {
+    Bounds b;
+#ifdef DMX_DEBUG_BOUNDS
+    b.lo = -(int64_t)kGuardWords;
+    b.hi = (int64_t)c->cap_words + kGuardWords;   // both buffers: cap_words + 2 guards words
+    b.slots = c->slot_cap;
+    b.items = c->item_alloc;
+    b.reads = c->n_reads;
+    b.counts = c->n_counts;
+    b.linked = c->cap_reads;
+    b.rec = c->d_counters;
+    b.kid = kid;
+#else
+    (void)c, (void)kid;
+#endif
+    return b;
+}
+
+hipError_t bounds_reset(Ctx* c, hipStream_t st) {
+#ifdef DMX_DEBUG_BOUNDS
+    return hipMemsetAsync(c->d_counters + kBoundsRec, 0, 4 * sizeof(uint32_t), st);
+#else
+    (void)c, (void)st;
+    return hipSuccess;
+#endif
+}
+
+int bounds_check(Ctx* c, const char* where) {
+#ifdef DMX_DEBUG_BOUNDS
+    static const char* const kKer[] = {
+        "?", "filter_kernel", "verify_kernel", "iscreen_kernel", "iscreen4_kernel",
+        "wscan_kernel", "scan_kernel", "band_cand_kernel<0,3>", "band_cand_kernel<4,5|7>",
+        "select_cand_kernel", "resolve_kernel", "select_kernel", "finalize0_kernel",
+        "finalize1_kernel", "finalize0_linked_kernel", "finalize1_linked_kernel",
+        "finalize2_linked_kernel", "chop_kernel", "chop_big_kernel", "chop_start",
+        "bounds_selftest_kernel"};
+    static const char* const kBuf[] = {"?", "seq", "nmask", "winner slots", "items", "results",
+                                       "counts", "reads", "linked keys", "candidates", "chop"};
+    uint32_t rec[4];
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpy(rec, c->d_counters + kBoundsRec, sizeof(rec), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        c->err = std::string(where) + ": " + hipGetErrorString(e);
+        return DMX_E_HIP;
+    }
+    if (!rec[0]) return DMX_OK;
+    const int k = (int)rec[0] - 1;
+    const int64_t idx = (int64_t)(((uint64_t)rec[3] << 32) | rec[2]);
+    char msg[256];
+    snprintf(msg, sizeof msg, "%s: bounds violation in %s: %s index %lld outside its buffer",
+             where, k > 0 && k < (int)(sizeof kKer / sizeof *kKer) ? kKer[k] : "?",
+             rec[1] < sizeof kBuf / sizeof *kBuf ? kBuf[rec[1]] : "?", (long long)idx);
+    c->err = msg;
+    return DMX_E_STATE;
+#else
+    (void)c, (void)where;
+    return DMX_OK;
+#endif
+}
+
+// DMX_DEBUG_BOUNDS builds: one gather below the guard, one slot past the winner array and one
+// in range, through the checked accessors (dmx_debug_bounds_selftest).
+__global__ void bounds_selftest_kernel(Packed pk, uint64_t slot_probe, uint32_t* out) {
+#ifdef DMX_DEBUG_BOUNDS
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    out[0] = code32(pk, (int64_t)(-16 * kGuardWords - 64));       // below the guard: refused
+    out[1] = DMX_BOUND(pk.bd, slots, slot_probe, kBufSlot) ? 1u : 0u;
+    out[2] = code32(pk, kMinOffset);                               // in range
+#else
+    (void)pk, (void)slot_probe, (void)out;
+#endif
+}
+
+int bounds_selftest(Ctx* c, uint32_t* host_out) {
+#ifdef DMX_DEBUG_BOUNDS
+    if (!c->d_seq || !c->d_winner[0]) {
+        c->err = "dmx_debug_bounds_selftest: load and run a batch first";
+        return DMX_E_STATE;
+    }
+    uint32_t* d_out = nullptr;
+    if (hipMalloc((void**)&d_out, 3 * sizeof(uint32_t)) != hipSuccess) return DMX_E_HIP;
+    Packed pk;
+    pk.seq = c->d_seq;
+    pk.nmask = c->d_nmask;
+    pk.bd = make_bounds(c, kKerSelfTest);
+    hipMemsetAsync(c->d_counters + 3, 0, sizeof(uint32_t), c->stream);
+    bounds_reset(c, c->stream);
+    hipLaunchKernelGGL(bounds_selftest_kernel, dim3(1), dim3(64), 0, c->stream, pk,
+                       (uint64_t)c->slot_cap, d_out);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpy(host_out, d_out, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    hipFree(d_out);
+    if (e != hipSuccess) return DMX_E_HIP;
+    return bounds_check(c, "dmx_debug_bounds_selftest");
+#else
+    (void)host_out;
+    c->err = "dmx_debug_bounds_selftest: not a DMX_DEBUG_BOUNDS build";
+    return DMX_E_UNSUPPORTED;
+#endif
+}
+
 int launch_round(Ctx* c, int round, hipStream_t st) {
     RoundArgs R;
-    R.seq = c->d_seq;
-    R.nmask = c->d_nmask;
+    R.pk.seq = c->d_seq;
+    R.pk.nmask = c->d_nmask;
+    R.pk.bd = make_bounds(c, 0);
     R.offs = c->d_offs;
     R.lens = c->d_lens;
     R.panel = c->d_panel[round];
@@ -3294,21 +3449,27 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     if (hp.filter && !linked) {   // linked primers: short, no shared suffix block; plain scan
         const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
         const uint32_t fgrid = (uint32_t)((nviews + kSegViewsPerBlock - 1) / kSegViewsPerBlock);
+        set_kid(R.pk.bd, kKerFilter);
         if (fgrid > 0) hipLaunchKernelGGL(filter_kernel, dim3(fgrid), dim3(kScanBlock), 0, st, R);
         DMX_DBG_SYNC("filter_kernel");
         hipEventRecord(c->ev[9 + 2 * round], st);
+        set_kid(R.pk.bd, kKerVerify);
         if (hp.verify)
             hipLaunchKernelGGL(verify_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
         DMX_DBG_SYNC("verify_kernel");
         hipEventRecord(c->ev[10 + 2 * round], st);
         if (R.screen) {   // packed quads for panels of <= 32 adapters (DMX_SCREEN_V1: A/B)
-            if (hp.n <= 4 * kScreenQuads && !c->screen_v1)
+            if (hp.n <= 4 * kScreenQuads && !c->screen_v1) {
+                set_kid(R.pk.bd, kKerScreen4);
                 hipLaunchKernelGGL(iscreen4_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
-            else
+            } else {
+                set_kid(R.pk.bd, kKerScreen);
                 hipLaunchKernelGGL(iscreen_kernel, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
+            }
         }
         DMX_DBG_SYNC("iscreen");
         hipEventRecord(c->ev[13 + round], st);
+        set_kid(R.pk.bd, kKerWscan);
         if (band) hipLaunchKernelGGL(wscan_kernel<true>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(wscan_kernel<false>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         DMX_DBG_SYNC("wscan_kernel");
@@ -3316,19 +3477,23 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         hipEventRecord(c->ev[9 + 2 * round], st);
         hipEventRecord(c->ev[10 + 2 * round], st);
         hipEventRecord(c->ev[13 + round], st);
+        set_kid(R.pk.bd, kKerScan);
         if (band) hipLaunchKernelGGL(scan_kernel<true>, dim3(grid), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(scan_kernel<false>, dim3(grid), dim3(kScanBlock), 0, st, R);
         DMX_DBG_SYNC("scan_kernel");
     }
     hipEventRecord(c->ev[round * 3 + 1], st);
     if (band) {
+        set_kid(R.pk.bd, kKerBand0);
         hipLaunchKernelGGL((band_cand_kernel<0, 3>), dim3(256 * 8), dim3(256), 0, st, R, 0);
         DMX_DBG_SYNC("band_cand_kernel<0, 3>");
+        set_kid(R.pk.bd, kKerBand1);
         if (c->band_wide[round])
             hipLaunchKernelGGL((band_cand_kernel<4, 7>), dim3(256 * 4), dim3(256), 0, st, R, 1);
         else   // every cost in list 1 is <= 5: a band of 2 * 5 + 1 diagonals is exact
             hipLaunchKernelGGL((band_cand_kernel<4, 5>), dim3(256 * 4), dim3(256), 0, st, R, 1);
         DMX_DBG_SYNC("band_cand_kernel<4, 5|7>");
+        set_kid(R.pk.bd, kKerSelectCand);
         hipLaunchKernelGGL(select_cand_kernel, dim3(1024), dim3(256), 0, st, R);
         DMX_DBG_SYNC("select_cand_kernel");
         hipEventRecord(c->ev[round * 3 + 2], st);
@@ -3343,6 +3508,7 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
+    set_kid(R.pk.bd, kKerResolve);
     if (c->ring_small[round])
         hipLaunchKernelGGL(resolve_kernel<kRingSmall>, dim3(resolve_grid(c)), dim3(kResolveBlock),
                            (size_t)kRingSmall * kResolveBlock * 16 + tabs, st, R);
@@ -3350,6 +3516,7 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         hipLaunchKernelGGL(resolve_kernel<kRingLarge>, dim3(resolve_grid(c)), dim3(kResolveBlock),
                            (size_t)kRingLarge * kResolveBlock * 16 + tabs, st, R);
     DMX_DBG_SYNC("resolve_kernel");
+    set_kid(R.pk.bd, kKerSelect);
     hipLaunchKernelGGL(select_kernel, dim3(1024), dim3(256), 0, st, R);
     DMX_DBG_SYNC("select_kernel");
     hipEventRecord(c->ev[round * 3 + 2], st);
@@ -3401,13 +3568,17 @@ int launch_finalize(Ctx* c, int round, hipStream_t st) {
     F.winner0 = c->d_winner[0];
     F.origin0 = c->d_origin[0];
     F.linked_best = c->d_linked;
+    F.bd = make_bounds(c, kKerFin0);
     if (c->mode == DMX_MODE_LINKED) {
         const uint32_t gr = (uint32_t)((c->n_reads + 255) / 256);
         if (round == 0) {
+            set_kid(F.bd, kKerFin0L);
             if (gr) hipLaunchKernelGGL(finalize0_linked_kernel, dim3(gr), dim3(256), 0, st, F);
         } else {
             const uint32_t gi = (uint32_t)((c->item_cap + 255) / 256);
+            set_kid(F.bd, kKerFin1L);
             if (gi) hipLaunchKernelGGL(finalize1_linked_kernel, dim3(gi), dim3(256), 0, st, F);
+            set_kid(F.bd, kKerFin2L);
             if (gr)
                 hipLaunchKernelGGL(finalize2_linked_kernel, dim3(std::min(gr, kFinalGrid)),
                                    dim3(256), 0, st, F);
@@ -3422,6 +3593,7 @@ int launch_finalize(Ctx* c, int round, hipStream_t st) {
     } else {
         const uint32_t grid = (uint32_t)std::min<size_t>((c->item_cap + 255) / 256, kFinalGrid);
         const size_t shm = sizeof(unsigned int) * ((size_t)(F.A0 + 1) * (F.A1 + 1) + 1);
+        set_kid(F.bd, kKerFin1);
         if (grid) hipLaunchKernelGGL(finalize1_kernel, dim3(grid), dim3(256), shm, st, F);
     }
     DMX_DBG_SYNC("finalize");

@@ -12,7 +12,7 @@ the same either way; tests cover both).
 
 Isolation: one server per (user, checkout, SLURM job, GPU visibility, library build). The socket
 name hashes SLURM_JOB_ID, the GPU-visibility variables (HIP/ROCR/CUDA_VISIBLE_DEVICES,
-GPU_DEVICE_ORDINAL) and the library selectors (DMX_LIBDMX, DMX_LIBDIR), so a job never talks to another job's server (which would use the other
+GPU_DEVICE_ORDINAL) and the library selectors (DMX_LIBDMX, DMX_LIBDIR, DMX_DEBUG_BOUNDS), so a job never talks to another job's server (which would use the other
 job's GPUs and die with it, `04_cleaning_primers.sh:4,7` is a 96-task array), and the server,
 spawned by its first client, sees exactly the devices its callers see. A request is served
 with only its own DMX_* variables; contexts are cached per (devices, dmx_open-time switches).
@@ -44,7 +44,7 @@ VISIBILITY_ENV = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_D
 # variables that decide which libdmx / libdmx_io build a process loads (read once at import by
 # dmx/lib.py and dmx/nio.py, so a server cannot switch them per request): a call that sets them
 # (A/B or sanitizer builds) gets a server of its own
-LIBRARY_ENV = ("DMX_LIBDMX", "DMX_LIBDIR")
+LIBRARY_ENV = ("DMX_LIBDMX", "DMX_LIBDIR", "DMX_DEBUG_BOUNDS")
 
 
 def socket_path(env=None) -> str:

@@ -15,8 +15,11 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 # DMX_LIBDMX: an alternative in-tree build of the same library (A/B kernel variants)
 # DMX_LIBDIR: a directory with another build of every library (host sanitizer builds)
-LIB_PATH = os.environ.get("DMX_LIBDMX") or os.path.join(os.environ.get("DMX_LIBDIR") or HERE,
-                                                      "libdmx.so")
+# DMX_DEBUG_BOUNDS=1: the bounds-checking build (every gather and slot access checked; a
+#   violation fails the call naming the kernel), dmx/libdmx_bounds.so
+BOUNDS = os.environ.get("DMX_DEBUG_BOUNDS", "") not in ("", "0")
+LIB_PATH = os.environ.get("DMX_LIBDMX") or os.path.join(
+    os.environ.get("DMX_LIBDIR") or HERE, "libdmx_bounds.so" if BOUNDS else "libdmx.so")
 
 DMX_FRONT, DMX_BACK, DMX_RC = 0x01, 0x02, 0x10
 MODE_SINGLE, MODE_TWO_ROUND, MODE_LINKED = 0, 1, 2
@@ -36,7 +39,9 @@ EXPORTS = ["dmx_abi_version", "dmx_open", "dmx_close", "dmx_last_error", "dmx_se
            "dmx_run_multi", "dmx_locate", "dmx_chop_set", "dmx_chop_exec", "dmx_chop_fetch",
            "dmx_chop_stats", "dmx_comm_unique_id", "dmx_comm_init_rank", "dmx_comm_init_all",
            "dmx_comm_size", "dmx_allreduce_counts", "dmx_debug_fetch", "dmx_run_sparse",
-           "dmx_mask_exceptions", "dmx_host_register", "dmx_host_unregister"]
+           "dmx_mask_exceptions", "dmx_host_register", "dmx_host_unregister", "dmx_panel_reach",
+           "dmx_debug_bounds_selftest"]
+ABI_VERSION = 4
 COMM_ID_BYTES = 128
 
 LOC_IGNORE_CASE, LOC_ONLY_POSITIVE = 0x1, 0x2
@@ -126,7 +131,10 @@ def load() -> ctypes.CDLL:
     L.dmx_mask_exceptions.restype = c_size
     L.dmx_host_register.argtypes = [P, c_size]
     L.dmx_host_unregister.argtypes = [P]
-    if L.dmx_abi_version() != 3:
+    L.dmx_panel_reach.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int), P,
+                                  c_int, ctypes.c_double, c_int, c_int, P, c_int]
+    L.dmx_debug_bounds_selftest.argtypes = [P, P]
+    if L.dmx_abi_version() != ABI_VERSION:
         raise DmxError("libdmx ABI mismatch")
     _lib = L
     return L
@@ -230,6 +238,13 @@ class Context:
                                                 float(max_errors), int(min_overlap), int(rc)),
                     "dmx_set_panel_mixed")
         self.panel_sizes[rnd] = len(seqs)
+
+    def bounds_selftest(self):
+        """DMX_DEBUG_BOUNDS builds: (return code, message, the kernel's 3 outputs)."""
+        out = np.zeros(3, dtype=np.uint32)
+        rc = self._L.dmx_debug_bounds_selftest(self._h, out.ctypes.data)
+        msg = self._L.dmx_last_error(self._h)
+        return rc, (msg.decode() if msg else ""), out
 
     def set_mode(self, mode: int):
         self._check(self._L.dmx_set_mode(self._h, mode), "dmx_set_mode")
@@ -400,6 +415,21 @@ class Context:
                 "traces": cl[6:8].tolist(), "windows_raw": cl[8:10].tolist(),
                 "tasks": cl[10:12].tolist(),
                 "flags": fl.value}
+
+
+def panel_reach(seqs, flags: int, max_errors: float = 0.1, min_overlap: int = 3,
+                wheres=None):
+    """Host only: (status, reach) of the panel dmx_set_panel would build — how far the kernels'
+    gathers reach around a read view, in nt (include/dmx.h dmx_panel_reach)."""
+    L = load()
+    arr = (ctypes.c_char_p * len(seqs))(*[s.encode("ascii") for s in seqs])
+    lens = (ctypes.c_int * len(seqs))(*[len(s) for s in seqs])
+    wh = (ctypes.c_int * len(seqs))(*wheres) if wheres is not None else None
+    out = np.zeros(6, dtype=np.int32)
+    rc = L.dmx_panel_reach(arr, lens, wh, len(seqs), float(max_errors), int(min_overlap),
+                           int(flags), out.ctypes.data, 6)
+    return rc, dict(zip(["pre_raw", "pre", "post", "need_pre", "need_post", "guard"],
+                        out.tolist()))
 
 
 def host_register(arrays) -> list:

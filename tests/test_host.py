@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
     exported = set(re.findall(r" T (dmx_\w+)", out))
     assert declared <= exported
     L = lib.load()
-    assert L.dmx_abi_version() == 3
+    assert L.dmx_abi_version() == 4
 
 
 def _unpack(p: lib.Packed, i: int) -> str:
