@@ -453,14 +453,16 @@ struct CandOut {
     uint32_t seg = 0;
 };
 
-// Exclusive prefix sum over the 64 lanes of the wave (every lane calls it), and the total.
-// Sum of v over the wave's 64 lanes (all active), in every lane.
+// Sum of v over the wave's 64 lanes, in every lane.  Precondition: wave64 with ALL 64 lanes
+// active, i.e. called after reconvergence (both callers, finalize0/1, reach it after block-stride
+// loops whose exits every lane takes; an inactive lane would contribute garbage to the xor tree).
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
 }
 
+// Exclusive prefix sum over the 64 lanes of the wave (every lane calls it), and the total.
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t x = v;

@@ -141,9 +141,11 @@ def run(argv=None, keep_contexts: bool = False) -> int:
     if not args.output:
         _unsupported("-o is required")
     if "{name1}" in args.output or "{name2}" in args.output:
-        _unsupported("{name1}/{name2} (combinatorial demultiplexing of paired-end reads) is not "
-                     "implemented; single-end demultiplexing takes {name} (the fused two-round "
-                     "layout is bin/dmx-demux-loop)")
+        _unsupported("{name1}/{name2} (cutadapt's combinatorial demultiplexing of paired-end "
+                     "reads) needs paired input; single-end demultiplexing takes {name}.  The "
+                     "two-round SP5 x SP27 layout {name1}_{name2} is `dmx-demux-loop IN "
+                     "--template '{name1}_{name2}.fastq.gz'` (default: the script's "
+                     "'{name2}_{name1}_{ds}.fastq.gz')")
     aset = panel.AdapterSet()
     for where, spec in args.adapters:
         aset.add_spec(spec, where)

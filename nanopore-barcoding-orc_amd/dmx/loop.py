@@ -12,6 +12,11 @@ view of every read, no host round trip) and writes the files the script leaves b
   demuxed/SP27/{SP27_j}_{SP5_i}_{dataset}.fastq.gz  round-2 output, j <= 8 (:100, :114-118)
   demuxed/SP27/{SP5_i}_{dataset}.json               round-2 report per SP5 bin (:102)
 
+The round-2 names are the two-name layout `{name2}_{name1}_{ds}.fastq.gz` (name1 = the SP5 bin,
+name2 = the SP27 bin; the script's `-o SP27/{name}_<id>_<ds>` with <id> = the SP5 bin).
+`--template` sets another layout under demuxed/SP27/ (e.g. '{name1}_{name2}.fastq.gz' or
+'{name1}/{name2}.fastq'); a name without .gz is written uncompressed.
+
 with the same record content and order as the 13 cutadapt calls (tests/test_cli_gpu.py checks
 it against the per-call CLI and the oracle).  `--reorient` takes the RAW reads instead: per
 batch it finds the primer segments on the GPU (bin/pychopper's semantics, dmx/chop.py), writes
@@ -37,6 +42,27 @@ from . import report
 from .report import Stats
 
 INVALID_SP27 = ("SP27_009", "SP27_010", "SP27_011", "SP27_012")   # 02_cutadapt_loop.sh:114-118
+# 02_cutadapt_loop.sh:100: `-o demuxed/SP27/{name}_${identifier}_${dataset}.fastq.gz` per SP5 bin
+DEFAULT_TEMPLATE = "{name2}_{name1}_{ds}.fastq.gz"
+
+
+def round2_path(outdir: str, template: str, name1: str, name2: str, ds: str) -> str:
+    """A round-2 output path: `template` with {name1} (SP5 bin), {name2} (SP27 bin) and {ds}
+    (dataset) substituted, under <outdir>/SP27/."""
+    rel = template.replace("{name1}", name1).replace("{name2}", name2).replace("{ds}", ds)
+    return os.path.join(outdir, "SP27", rel)
+
+
+def check_template(template: str) -> str | None:
+    """Why a --template cannot name every (SP5, SP27) bin apart, or None."""
+    if "{name1}" not in template or "{name2}" not in template:
+        return "--template needs both {name1} and {name2} (one file per (SP5, SP27) bin)"
+    rest = template.replace("{name1}", "").replace("{name2}", "").replace("{ds}", "")
+    if "{" in rest or "}" in rest:
+        return "--template knows only {name1}, {name2} and {ds}"
+    if os.path.isabs(template) or ".." in template.split("/"):
+        return "--template is a path under <outdir>/SP27/"
+    return None
 
 
 def dataset_name(infile: str) -> str:
@@ -61,6 +87,10 @@ def build_parser():
     p.add_argument("--outdir", default=None, help="default: $(dirname $(dirname IN))/demuxed")
     p.add_argument("--no-cleanup", action="store_true",
                    help="keep the unknown and SP27_009..012 outputs (:107-119 delete them)")
+    p.add_argument("--template", default=DEFAULT_TEMPLATE,
+                   help="round-2 output names under <outdir>/SP27/: {name1} = SP5 bin, {name2} "
+                        "= SP27 bin ('unknown' for the --no-cleanup round-2 unknown files), "
+                        "{ds} = dataset (default: the script's " + DEFAULT_TEMPLATE + ")"),
     # cutadapt's defaults (the script's calls pass neither): level 5; -Z = level 1
     p.add_argument("--compression-level", type=int,
                    default=int(os.environ.get("DMX_COMPRESSION_LEVEL", "5") or 5))
@@ -138,6 +168,10 @@ def run(argv=None) -> int:
     else:
         ds = dataset_name(infile)
         demux_in = infile
+    why = check_template(args.template)
+    if why:
+        print(f"dmx-demux-loop: error: {why}", file=sys.stderr)
+        return 2
     outdir = args.outdir or os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(demux_in))), "demuxed")
     print("=========================================")
@@ -179,10 +213,15 @@ def run(argv=None) -> int:
     for i, ident in enumerate(n1):
         if args.no_cleanup:
             out2[i, 0] = len(p2)
-            p2.append(f"{outdir}/SP27/unknown_{ident}_{ds}.fastq.gz")
+            p2.append(round2_path(outdir, args.template, ident, "unknown", ds))
         for j in keep2:
             out2[i, j + 1] = len(p2)
-            p2.append(f"{outdir}/SP27/{n2[j]}_{ident}_{ds}.fastq.gz")
+            p2.append(round2_path(outdir, args.template, ident, n2[j], ds))
+    if len(set(p2)) != len(p2):
+        print("dmx-demux-loop: error: --template gives two bins the same file", file=sys.stderr)
+        return 2
+    for d in sorted({os.path.dirname(x) for x in p2}):
+        os.makedirs(d, exist_ok=True)
 
     st1 = Stats(ads1)
     st1.rc_mode = True

@@ -10,7 +10,8 @@ import pytest
 
 import oracle
 from dmx import panel, synth
-from helpers import (CLI, LOOP, amplicon_reads, oracle_linked, oracle_round, random_quals, read_fastq,
+from helpers import (CLI, LOOP, amplicon_reads, instantiate, oracle_linked, oracle_round,
+                     random_quals, read_fastq,
                      write_fastq)
 
 pytestmark = pytest.mark.gpu
@@ -193,3 +194,97 @@ def test_unverified_rule_cases_match_the_oracle(tmp_path):
             for k, (an, _) in enumerate(c["adapters"]):
                 assert read_fastq(str(out / f"{name}_{an}.fastq")) == per.get(k, []), (name, an)
             assert read_fastq(str(out / f"{name}_unknown.fastq")) == per.get(-1, []), name
+
+
+def test_04_unlinked_round2_dropin(tmp_path):
+    """scripts/04_cleaning_primers.sh:464-507 (--run-round2): one call on round 1's untrimmed
+    consensuses with every round-1 pair as UNLINKED primers, `-g FWD -a REV` per pair in pair
+    order (the reference's COI and rRNA primer files, literal IUPAC primers), default -e, no
+    --rc, no --untrimmed-output and no {name}: every record, trimmed or not, goes to -o in
+    input order (FASTA in, FASTA out).  Records equal the oracle's (one mixed FRONT / BACK
+    panel: best_match over the adapters in command-line order; -g keeps seq[rstop:], -a keeps
+    seq[:rstart])."""
+    data = os.path.dirname(panel.SP5_FASTA)
+    pairs = (panel.primer_pairs(os.path.join(data, "COI_primers.fa")) +
+             panel.primer_pairs(os.path.join(data, "RNA_primers.fa")))
+    assert len(pairs) == 4
+    rng = np.random.default_rng(507)
+    # round 1's untrimmed records: one primer of a pair, damaged copies, or none
+    seqs = []
+    for _ in range(3000):
+        _, f, r = pairs[int(rng.integers(len(pairs)))]
+        body = "".join(rng.choice(list("ACGT"), size=int(rng.integers(60, 900))))
+        u = rng.random()
+        if u < 0.4:
+            s = instantiate(rng, f) + body
+        elif u < 0.75:
+            s = body + instantiate(rng, r)
+        elif u < 0.85:
+            s = instantiate(rng, f)[int(rng.integers(1, 8)):] + body   # partial at the start
+        else:
+            s = body
+        flank = "".join(rng.choice(list("ACGT"), size=int(rng.integers(0, 30))))
+        seqs.append(flank + s)
+    names = [f"cluster{i};size={int(rng.integers(2, 90))}" for i in range(len(seqs))]
+    infile = tmp_path / "untrimmed_round1.fasta"
+    infile.write_text("".join(f">{n}\n{s}\n" for n, s in zip(names, seqs)))
+    out = tmp_path / "round2_primerless.fasta"
+    cmd = [CLI, "-j", "4"]
+    adapters, wheres = [], []
+    for _, f, r in pairs:
+        cmd += ["-g", f, "-a", r]
+        adapters += [f, r]
+        wheres += [oracle.FRONT, oracle.BACK]
+    cmd += ["-o", str(out), str(infile)]
+    subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL)
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    res = oracle.run_batch(oracle.Panel(adapters, wheres), None, blob, offs, lens, mode=0,
+                           use_rc=False, threads=8)
+    exp = []
+    for n, s, r in zip(names, seqs, res):
+        b = int(r["bin1"])
+        if b < 0:
+            exp.append((n, s, None))
+        elif wheres[b] == oracle.FRONT:
+            exp.append((n, s[int(r["m1_rstop"]):], None))
+        else:
+            exp.append((n, s[:int(r["m1_rstart"])], None))
+    n_front = sum(1 for r in res if r["bin1"] >= 0 and wheres[int(r["bin1"])] == oracle.FRONT)
+    n_back = sum(1 for r in res if r["bin1"] >= 0 and wheres[int(r["bin1"])] == oracle.BACK)
+    assert n_front > 500 and n_back > 500 and sum(res["bin1"] < 0) > 100
+    assert _read_fasta(str(out)) == exp
+
+
+def test_loop_two_name_template(tmp_path):
+    """dmx-demux-loop --template: the two-name layout of north_star ({name1}_{name2}), also with
+    a directory per SP5 bin and plain text, writes the same records per (SP5, SP27) bin as the
+    script's default names (02_cutadapt_loop.sh:100)."""
+    d = synth.generate("c2", n=2500, seed=77)
+    seqs = synth.to_strings(d)
+    rng = np.random.default_rng(77)
+    names = [f"r{i}" for i in range(len(seqs))]
+    infile = tmp_path / "pychopped" / "pychopped_ds7.fastq"
+    infile.parent.mkdir()
+    write_fastq(str(infile), names, seqs, random_quals(rng, map(len, seqs)))
+    n5, _ = panel.load_panel(panel.SP5_FASTA)
+    n27, _ = panel.load_panel(panel.SP27RC_FASTA)
+    runs = {}
+    for tag, tmpl in (("default", None), ("n1n2", "{name1}_{name2}.fastq.gz"),
+                      ("dirs", "{name1}/{name2}_{ds}.fastq")):
+        od = tmp_path / tag
+        cmd = [LOOP, str(infile), "-j", "4", "--outdir", str(od)]
+        if tmpl:
+            cmd += ["--template", tmpl]
+        subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL)
+        runs[tag] = od
+    kept = [b for b in n27 if b not in ("SP27_009", "SP27_010", "SP27_011", "SP27_012")]
+    total = 0
+    for a in n5:
+        for b in kept:
+            ref = read_fastq(f"{runs['default']}/SP27/{b}_{a}_ds7.fastq.gz")
+            assert read_fastq(f"{runs['n1n2']}/SP27/{a}_{b}.fastq.gz") == ref, (a, b)
+            assert read_fastq(f"{runs['dirs']}/SP27/{a}/{b}_ds7.fastq") == ref, (a, b)
+            total += len(ref)
+    assert total > 0.5 * len(seqs)
+    # same file set otherwise: no default-named round-2 file in the templated runs
+    assert not glob.glob(f"{runs['n1n2']}/SP27/SP27_*_SP5_*")
