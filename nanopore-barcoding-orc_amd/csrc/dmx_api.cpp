@@ -504,6 +504,13 @@ static int build_panel(Ctx* c, const char* const* seqs, const int* lens, const i
         }
         dp.kf = kf;
         dp.max_mk = mk;
+        // clean flags: the exact stages read a window's view from j1 - (m + k
+        // + 1) (window scan) and j1 - (m + 7) (band DP); off when that exceeds 128 positions
+        int reach = 0;
+        for (int a = 0; a < n; ++a)
+            reach = std::max(reach, (int)hp.ad[a].m + std::max((int)hp.ad[a].k + 1, 7));
+        reach = (reach + 15) / 16 * 16;
+        dp.clean_reach = reach <= 128 && !std::getenv("DMX_NO_CLEAN") ? reach : 0;
 
         // shared prefix for the verification pass
         int pre = lens[0];

@@ -64,7 +64,11 @@ struct DevPanel {
     // suffix of the block ends at the same column and costs no more, so its cost is a lower
     // bound of b(j) and the filter stays a necessary condition (verify / screen keep filter_len)
     int32_t scan_len;
-    int32_t pad_scan;
+    // reach of the exact stages before a window, in view positions (window scan start m + k + 1,
+    // band start m + 7), rounded up to 16; 0 = no clean flags (every window loads the mask).  The
+    // filter marks a window `clean` when the no-match mask is zero over [j1 - clean_reach, j2]
+    // 
+    int32_t clean_reach;
     uint32_t filter_peq[8];
     int8_t pf[72];       // max over adapters of pacc[L]
     // Shared-prefix verification (0 = disabled): the first `pre_len` (<= 32) characters are common
@@ -95,11 +99,14 @@ struct Window {
     uint8_t lastcol;     // 3' panel: window ends at the final column (last-column cells)
     uint8_t strand;      // oriented view of the item (copied so the window scan needs no
     uint8_t bmin;        // dependent loads): strand, start, len, read length n, first nt off;
-    uint32_t j1, j2;     // bmin = min suffix-block cost over the hits (255 = no hit)
+    uint32_t j1, j2;     // bmin = min suffix-block cost over the hits (255 = no hit).
+                         // strand bit 1 (kWinClean): the view's no-match mask is zero over
+                         // [j1 - clean_reach, j2], so the exact stages need not load it
     uint32_t n, start, len, info;
     uint64_t off;
 };
 static_assert(sizeof(Window) == 40, "Window layout");
+constexpr uint8_t kWinClean = 2;   // Window.strand bit 1
 
 constexpr int kStageCap = 256;    // LDS staging of emitted records per block
 // Appendable lists are split into kShards shards, each with its own counter (a slot of
@@ -195,7 +202,7 @@ struct Cand {
     uint8_t cost;
     uint32_t j;          // end column
     uint32_t n, start, len;
-    uint8_t strand, o, a, pad;
+    uint8_t strand, o, a, clean;   // clean: the band reads codes only (Window kWinClean)
     uint64_t off;
 };
 static_assert(sizeof(Cand) == 40, "Cand layout");
@@ -328,17 +335,18 @@ __device__ __forceinline__ uint32_t rev_pairs(uint32_t w) {
 // 16 consecutive view positions starting at view position p: 2-bit codes (complemented on the
 // reverse strand) and the no-match bits.  `off`/`n`: the read's first nt and length; view
 // (strand, start).
+// load_mask = false (a `clean` view range): the codes only, no-match bits 0.
 __device__ __forceinline__ void fetch16(const Packed& pk, uint64_t off, uint32_t n,
                                         uint32_t strand, uint32_t start, uint32_t p,
-                                        uint32_t& codes, uint32_t& nbits) {
+                                        uint32_t& codes, uint32_t& nbits, bool load_mask = true) {
     if (strand == 0) {
         const int64_t g = (int64_t)off + start + p;
         codes = code32(pk, g);
-        nbits = mask32(pk, g) & 0xFFFFu;
+        nbits = load_mask ? mask32(pk, g) & 0xFFFFu : 0u;
     } else {   // lowest nt of the window
         const int64_t b = (int64_t)off + (int64_t)n - 1 - start - (int64_t)p - 15;
         codes = ~rev_pairs(code32(pk, b));                           // complement = 3 - c
-        nbits = __brev(mask32(pk, b)) >> 16;
+        nbits = load_mask ? __brev(mask32(pk, b)) >> 16 : 0u;
     }
 }
 

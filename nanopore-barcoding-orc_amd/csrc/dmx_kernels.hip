@@ -53,10 +53,22 @@ struct RoundArgs {
     uint32_t task_scap;
 };
 
+// DESIGN.md §3.10.  The filter, the prefix verification and the index screen are necessary
+// conditions that only compare lower bounds of edit costs with thresholds.  Reading a read's
+// non-ACGT bases as the 2-bit code packed for them (A) instead of "matches nothing" can only turn
+// a mismatch into a match, so every cost they compute can only go down: they stay necessary
+// conditions, and the exact stages (window scan, band DP) still see the no-match mask.  So by
+// default those three never use the mask (DMX_MASK_SKIP=0: the round-4 behaviour, for A/B).
+#ifndef DMX_MASK_SKIP
+#define DMX_MASK_SKIP 1
+#endif
+constexpr bool kNecessaryMask = !DMX_MASK_SKIP;
+
 struct TaskView {
     uint32_t read, n, strand, start, len;
     uint64_t off;
     int o, a;
+    bool clean = false;   // the exact stages may skip the no-match mask (Window kWinClean)
 };
 
 // An empty view at the first valid offset (DMX_DEBUG_BOUNDS builds: an item or read index out of
@@ -374,7 +386,7 @@ __device__ __forceinline__ Cand make_cand(const TaskView& tv, uint32_t item, int
     c.strand = (uint8_t)tv.strand;
     c.o = (uint8_t)tv.o;
     c.a = (uint8_t)tv.a;
-    c.pad = 0;
+    c.clean = tv.clean ? 1 : 0;
     c.off = tv.off;
     return c;
 }
@@ -393,18 +405,26 @@ __device__ __forceinline__ bool viable_lb(int lbk, int lr, int o, int cost) {
 // view as free-start warm-up only, where any codes are safe (the index screen of a 3' panel at
 // -e 0.3 starts up to m + k columns before a short view).  The positions are signed: the seed-46
 // fault of round 4 was an unsigned wrap of such a position below the buffer.
+// MASK = false: the codes only, no-match bits 0 (one 8-byte gather instead of two).
+template <bool MASK = true>
 __device__ __forceinline__ void fetch16s(const Packed& pk, const TaskView& tv, int p,
                                          uint32_t& codes, uint32_t& nbits) {
     p = max(p, -kViewReachPre);
     if (tv.strand == 0) {
         const int64_t g = (int64_t)tv.off + (int64_t)tv.start + p;
         codes = code32(pk, g);
-        nbits = mask32(pk, g) & 0xFFFFu;
+        nbits = (MASK && !tv.clean) ? mask32(pk, g) & 0xFFFFu : 0u;
     } else {
         const int64_t b = (int64_t)tv.off + (int64_t)tv.n - 1 - (int64_t)tv.start - p - 15;
         codes = ~rev_pairs(code32(pk, b));
-        nbits = __brev(mask32(pk, b)) >> 16;
+        nbits = (MASK && !tv.clean) ? __brev(mask32(pk, b)) >> 16 : 0u;
     }
+}
+
+// The no-match bits of view positions [p, p + 32) (the filter's clean-flag history).
+__device__ __forceinline__ uint32_t mask32s(const Packed& pk, const TaskView& tv, int p) {
+    if (tv.strand == 0) return mask32(pk, (int64_t)tv.off + (int64_t)tv.start + p);
+    return __brev(mask32(pk, (int64_t)tv.off + (int64_t)tv.n - 1 - (int64_t)tv.start - p - 31));
 }
 
 template <class Sink>
@@ -585,15 +605,16 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
 
     uint32_t p0 = js;
     uint32_t ncodes, nnb, ncodes2 = 0, nnb2 = 0;   // the next two chunks, in flight
-    fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb);
+    const bool lm = !tv.clean;                      // clean windows: codes only
+    fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb, lm);
     if (p0 + 16 < jhi)
-        fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes2, nnb2);
+        fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes2, nnb2, lm);
     for (; p0 + 16 <= jhi; p0 += 16) {
         const uint32_t codes = ncodes, nb = nnb;
         ncodes = ncodes2;
         nnb = nnb2;
         if (p0 + 32 < jhi)
-            fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 32, ncodes2, nnb2);
+            fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 32, ncodes2, nnb2, lm);
         if (segset && p0 + 16 >= seg + 64) {   // this chunk could overflow the 64-bit segment
             flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
             segset = false;
@@ -800,7 +821,10 @@ __device__ __forceinline__ uint32_t bsel(uint32_t mask, uint32_t a, uint32_t b) 
 // stretches start 64 positions apart, so its bit alignment inside the blocks never changes and the
 // extraction is the filter's (seg_extract): word selects + funnel shifts, no indexed registers.
 // Strand 1 walks the global blocks downwards and reverses + complements each 16-position chunk.
+// MASK = false: the no-match mask is not loaded and every chunk's no-match bits are 0 (a read N
+// reads as its packed code, A): for the necessary-condition stages.
 // ---------------------------------------------------------------------------------------------
+template <bool MASK = true>
 struct ViewBlocks {
     uint32_t cw[12], nw[6];      // [0..7]/[0..3]: blocks B, B + 1 (ascending); [8..11]/[4..5]:
                                  // the block in flight (B + 2 on strand 0, B - 1 on strand 1)
@@ -816,7 +840,7 @@ struct ViewBlocks {
     __device__ __forceinline__ void load(int k, int64_t b) {
 #ifdef DMX_DEBUG_BOUNDS
         if (!bchk(bd, 4 * b, bd.lo, bd.hi - 3, kBufSeq) ||
-            !bchk(bd, 2 * b, bd.lo, bd.hi - 1, kBufMask)) {
+            (MASK && !bchk(bd, 2 * b, bd.lo, bd.hi - 1, kBufMask))) {
             for (int x = 0; x < 4; ++x) cw[4 * k + x] = 0u;
             nw[2 * k] = nw[2 * k + 1] = 0u;
             return;
@@ -827,9 +851,13 @@ struct ViewBlocks {
         cw[4 * k + 1] = c4.y;
         cw[4 * k + 2] = c4.z;
         cw[4 * k + 3] = c4.w;
-        const uint2 n2 = np[b];
-        nw[2 * k + 0] = n2.x;
-        nw[2 * k + 1] = n2.y;
+        if constexpr (MASK) {
+            const uint2 n2 = np[b];
+            nw[2 * k + 0] = n2.x;
+            nw[2 * k + 1] = n2.y;
+        } else {
+            nw[2 * k + 0] = nw[2 * k + 1] = 0u;
+        }
     }
     // view positions [p, p + 64 * n_stretch) of the view (strand, start, n, off) of tv
     __device__ __forceinline__ void init(const RoundArgs& R, const TaskView& tv, int p) {
@@ -870,14 +898,14 @@ struct ViewBlocks {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 vc[c] = asc[c];
-                vn[c] = (an[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+                vn[c] = MASK ? (an[c >> 1] >> (16 * (c & 1))) & 0xFFFFu : 0u;
             }
         } else {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const int d = 3 - c;
                 vc[c] = ~rev_pairs(asc[d]);                        // complement = 3 - code
-                vn[c] = __brev((an[d >> 1] >> (16 * (d & 1))) & 0xFFFFu) >> 16;
+                vn[c] = MASK ? __brev((an[d >> 1] >> (16 * (d & 1))) & 0xFFFFu) >> 16 : 0u;
             }
         }
         // slide: strand 0 (lo, hi, in flight) -> (hi, in flight, next);
@@ -939,12 +967,13 @@ static_assert(kLastBuckets * kStepsPerBucket * 64 >= kSegSpan,
               "every last segment's step count must fall into one of the four step buckets");
 
 __device__ __forceinline__ Window make_window(uint32_t item, int o, const TaskView& tv,
-                                              uint32_t j1, uint32_t j2, int lastcol, int bmin) {
+                                              uint32_t j1, uint32_t j2, int lastcol, int bmin,
+                                              bool clean = false) {
     Window w;
     w.item = item;
     w.o = (uint8_t)o;
     w.lastcol = (uint8_t)lastcol;
-    w.strand = (uint8_t)tv.strand;
+    w.strand = (uint8_t)(tv.strand | (clean ? kWinClean : 0u));
     w.bmin = (uint8_t)min(bmin, 255);
     w.j1 = j1;
     w.j2 = j2;
@@ -962,7 +991,26 @@ struct SegState {
     bool have;
     uint32_t w1, w2;
     int wb;
+    uint64_t dh;    // clean flags: bit c = a no-match bit in view positions [hb + 16c, +16)
+    int hb;
 };
+
+// The filter's clean-flag history spans clean_reach (<= 128) positions before the segment and
+// the segment itself in 16-position chunks: 64 bits hold it for spans up to 768.
+constexpr bool kCleanHist = (kSegSpan + 128) / 16 + 4 <= 64;
+
+// Is the no-match mask zero over the view positions an exact stage reads for window [w1, w2]
+// (columns): [w1 - rb, w2 - 1], clipped at the view start?  (Positions outside the view are
+// never used by them.)  rb = clean_reach, 0 = off.
+__device__ __forceinline__ bool window_clean(const SegState& S, uint32_t w1, uint32_t w2, int rb) {
+    if (!kCleanHist || rb == 0) return false;
+    const int lo = max(0, (int)w1 - rb), hi = (int)w2 - 1;
+    if (hi < lo) return true;                     // nothing of the view is read
+    const int cl = (lo - S.hb) >> 4, ch = (hi - S.hb) >> 4;
+    if (cl < 0 || ch > 63) return false;          // outside the history: unknown
+    const uint64_t m = (ch - cl >= 63 ? ~0ull : ((2ull << (ch - cl)) - 1ull)) << cl;
+    return (S.dh & m) == 0;
+}
 
 // Myers step of the filter block, stored in the TOP filter_len bits of the word (the rows
 // below are all-match padding that stays at cost 0, so they act as row 0): the last row is bit
@@ -1000,12 +1048,13 @@ template <bool CAREFUL>
 __device__ __forceinline__ void filter_chunk(uint32_t codes, uint32_t nb, uint32_t p0, int cnt,
                                              SegState& S, const uint32_t* s_fpeq,
                                              const int8_t* s_thr, int kf_far, uint32_t gap,
-                                             uint32_t hit_from,
+                                             uint32_t hit_from, int rb,
                                              const WaveStage<Window, kWaveWinCap>& st,
                                              uint32_t item, int o,
                                              const TaskView& tv) {
     uint32_t eq[16];
-    if (__builtin_amdgcn_ballot_w64(nb != 0u) == 0) {   // ACGT only (wave-uniform): byte offsets
+    // N read as A unless kNecessaryMask: the spread path for every chunk
+    if (!kNecessaryMask || __builtin_amdgcn_ballot_w64(nb != 0u) == 0) {   // byte offsets
         const uint32_t lo = spread_codes(codes, 0x0c010c00u);
         const uint32_t hi = spread_codes(codes, 0x0c030c02u);
         const char* base = reinterpret_cast<const char*>(s_fpeq);
@@ -1050,7 +1099,9 @@ __device__ __forceinline__ void filter_chunk(uint32_t codes, uint32_t nb, uint32
             S.w2 = j;
             S.wb = min(S.wb, cb);
         } else {
-            if (S.have) st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb));
+            if (S.have)
+                st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb,
+                                    window_clean(S, S.w1, S.w2, rb)));
             S.have = true;
             S.w1 = S.w2 = j;
             S.wb = cb;
@@ -1064,14 +1115,32 @@ __device__ __forceinline__ void filter_segment(const RoundArgs& R, const TaskVie
                                                uint32_t P0, uint32_t P1, SegState& S,
                                                const uint32_t* s_fpeq, const int8_t* s_thr,
                                                int kf_far, uint32_t gap, uint32_t hit_from,
-                                               const WaveStage<Window, kWaveWinCap>& st,
+                                               int rb, const WaveStage<Window, kWaveWinCap>& st,
                                                uint32_t item, int o) {
-    ViewBlocks B;
+    ViewBlocks<true> B;
     B.init(R, tv, (int)P0);
+    // clean-flag history: 16-position chunks from hb = P0 - rb; the rb
+    // positions before the segment are read as mask words (none before the view start: the
+    // exact stages never read there), the segment's own from its blocks below
+    S.hb = (int)P0 - rb;
+    S.dh = 0;
+    if (kCleanHist && rb) {
+        for (int q = 0; q < rb; q += 32) {
+            const int p = S.hb + q;
+            if (p + 32 <= 0) continue;
+            const uint32_t m = mask32s(R.pk, tv, p);   // (a chunk past P0: the segment's own)
+            S.dh |= (uint64_t)(((m & 0xFFFFu) ? 1u : 0u) | ((m >> 16) ? 2u : 0u)) << (q >> 4);
+        }
+    }
     const uint32_t nsteps = (P1 - P0 + 63u) / 64u;
     for (uint32_t s = 0, p0 = P0; p0 < P1; ++s, p0 += 64) {
         uint32_t vc[4], vn[4];
         B.extract(vc, vn, s + 2u < nsteps);
+        if (kCleanHist && rb) {
+            const uint32_t nz = (vn[0] ? 1u : 0u) | (vn[1] ? 2u : 0u) | (vn[2] ? 4u : 0u) |
+                                (vn[3] ? 8u : 0u);
+            S.dh |= (uint64_t)nz << ((rb >> 4) + 4 * (int)s);
+        }
         // per-column thresholds only near the view start (segment 0, grouped first in the
         // block's task order, so the branch is wave-uniform but for one wave); later segments
         // have threshold kf_far everywhere and mask their warm-up columns
@@ -1081,10 +1150,10 @@ __device__ __forceinline__ void filter_segment(const RoundArgs& R, const TaskVie
             const int cnt = (int)P1 - (int)pc;
             if (careful)
                 filter_chunk<true>(vc[0], vn[0], pc, cnt, S, s_fpeq, s_thr, kf_far, gap,
-                                   hit_from, st, item, o, tv);
+                                   hit_from, rb, st, item, o, tv);
             else
                 filter_chunk<false>(vc[0], vn[0], pc, cnt, S, s_fpeq, s_thr, kf_far, gap,
-                                    hit_from, st, item, o, tv);
+                                    hit_from, rb, st, item, o, tv);
             vc[0] = vc[1];
             vc[1] = vc[2];
             vc[2] = vc[3];
@@ -1289,6 +1358,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     const bool front = P->where == kFront;
     const int kf_far = min(kf, (int)s_pf[71]);
     const uint32_t gap = (uint32_t)P->max_mk;
+    const int rb = kCleanHist ? P->clean_reach : 0;   // clean flags for the exact stages
     // the block's rows sit in the top L bits (filter_peq, host side): rows start at cost i
     const uint32_t pv_rows = L >= 32 ? ~0u : ~0u << (32 - L);
 
@@ -1353,19 +1423,26 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             S.have = false;
             S.w1 = S.w2 = 0;
             S.wb = 255;
-            filter_segment(R, tv, P0, P1, S, s_fpeq, s_thr, kf_far, gap, seg0, st, item, o);
+            filter_segment(R, tv, P0, P1, S, s_fpeq, s_thr, kf_far, gap, seg0, rb, st, item,
+                           o);
             const uint32_t len = tv.len;
             if (!front && P1 == len) {
                 // 3' panels: the last column (adapter prefix off the read end) is always checked
                 if (S.have && len - S.w2 <= gap) {
-                    st.push(make_window(item, o, tv, S.w1, len, 1, S.wb));
+                    st.push(make_window(item, o, tv, S.w1, len, 1, S.wb,
+                                        window_clean(S, S.w1, len, rb)));
                 } else {
-                    if (S.have) st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb));
-                    st.push(make_window(item, o, tv, len, len, 1, 255));
+                    if (S.have)
+                        st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb,
+                                            window_clean(S, S.w1, S.w2, rb)));
+                    st.push(make_window(item, o, tv, len, len, 1, 255,
+                                        window_clean(S, len, len, rb)));
                 }
                 S.have = false;
             }
-            if (S.have) st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb));
+            if (S.have)
+                st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb,
+                                    window_clean(S, S.w1, S.w2, rb)));
         }
         __builtin_amdgcn_wave_barrier();
         if (st.count() > kWaveWinCap / 2) st.flush();
@@ -1480,7 +1557,7 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
                 TaskView tv;
                 tv.read = 0;
                 tv.n = w.n;
-                tv.strand = w.strand;
+                tv.strand = w.strand & 1u;
                 tv.start = w.start;
                 tv.len = w.len;
                 tv.off = w.off;
@@ -1504,7 +1581,7 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
                 // the columns js + 1 .. hi as 64-position stretches of whole aligned blocks
                 // (one lane per window: the block loads are scattered, so few and wide)
                 const int nst = (hi - js + 63) >> 6;
-                ViewBlocks vb;
+                ViewBlocks<kNecessaryMask> vb;   // N read as A: a lower bound of D_pre
                 if (nst > 0) vb.init(R, tv, js);
                 for (int st_i = 0; st_i < nst; ++st_i) {
                     uint32_t vc[4], vn[4];
@@ -1682,21 +1759,21 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
                 TaskView tv;
                 tv.read = 0;
                 tv.n = w.n;
-                tv.strand = w.strand;
+                tv.strand = w.strand & 1u;
                 tv.start = w.start;
                 tv.len = w.len;
                 tv.off = w.off;
                 tv.o = w.o;
                 tv.a = a;
                 uint32_t c0 = 0, n0 = 0, c1 = 0, n1 = 0;   // two chunks in flight
-                if (nch > 0) fetch16s(R.pk, tv, jb, c0, n0);
-                if (nch > 1) fetch16s(R.pk, tv, jb + 16, c1, n1);
+                if (nch > 0) fetch16s<kNecessaryMask>(R.pk, tv, jb, c0, n0);
+                if (nch > 1) fetch16s<kNecessaryMask>(R.pk, tv, jb + 16, c1, n1);
                 for (int k = 0; k < nch && !pass; ++k) {
                     const int p0 = jb + 16 * k;
                     const uint32_t codes = c0, nb = n0;
                     c0 = c1;
                     n0 = n1;
-                    if (k + 2 < nch) fetch16s(R.pk, tv, p0 + 32, c1, n1);
+                    if (k + 2 < nch) fetch16s<kNecessaryMask>(R.pk, tv, p0 + 32, c1, n1);
                     // this chunk's columns p0+1 .. p0+16: the threshold of the regions it touches
                     // and the first column counted (earlier ones are warm-up)
                     const bool inR = rows && p0 + 16 >= xr_lo && p0 + 1 <= xrh;
@@ -1995,7 +2072,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                 TaskView tv;
                 tv.read = 0;
                 tv.n = w.n;
-                tv.strand = w.strand;
+                tv.strand = w.strand & 1u;
                 tv.start = w.start;
                 tv.len = w.len;
                 tv.off = w.off;
@@ -2004,14 +2081,14 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                 const char* qb = reinterpret_cast<const char*>(s_q);
                 const uint32_t q8 = 8u * (uint32_t)q;   // the lane's quad within a code row
                 uint32_t c0 = 0, n0 = 0, c1 = 0, n1 = 0;   // two chunks in flight
-                if (nch > 0) fetch16s(R.pk, tv, jb, c0, n0);
-                if (nch > 1) fetch16s(R.pk, tv, jb + 16, c1, n1);
+                if (nch > 0) fetch16s<kNecessaryMask>(R.pk, tv, jb, c0, n0);
+                if (nch > 1) fetch16s<kNecessaryMask>(R.pk, tv, jb + 16, c1, n1);
                 for (int kc = 0; kc < nch && (need & ~pass_m); ++kc) {
                     const int p0 = jb + 16 * kc;
                     const uint32_t codes = c0, nb = n0;
                     c0 = c1;
                     n0 = n1;
-                    if (kc + 2 < nch) fetch16s(R.pk, tv, p0 + 32, c1, n1);
+                    if (kc + 2 < nch) fetch16s<kNecessaryMask>(R.pk, tv, p0 + 32, c1, n1);
                     const bool inR = rows && p0 + 16 >= xr_lo && p0 + 1 <= xrh;
                     const bool inE = lastc && p0 + 16 >= xe_lo;
                     const int qlo = min(inR ? xr_lo : (1 << 30), inE ? xe_lo : (1 << 30)) - p0 - 1;
@@ -2132,7 +2209,8 @@ __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, 
     sub = w.o * A + a;
     tv.read = 0;
     tv.n = w.n;
-    tv.strand = w.strand;
+    tv.strand = w.strand & 1u;
+    tv.clean = (w.strand & kWinClean) != 0;
     tv.start = w.start;
     tv.len = w.len;
     tv.off = w.off;
@@ -2839,6 +2917,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                 tv.read = 0;
                 tv.n = c.n;
                 tv.strand = c.strand;
+                tv.clean = c.clean != 0;
                 tv.start = c.start;
                 tv.len = c.len;
                 tv.off = c.off;

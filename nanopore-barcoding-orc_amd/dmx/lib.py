@@ -63,7 +63,7 @@ WINDOW_DTYPE = np.dtype([("item", "<u4"), ("o", "u1"), ("lastcol", "u1"), ("stra
                          ("start", "<u4"), ("len", "<u4"), ("info", "<u4"), ("off", "<u8")])
 CAND_DTYPE = np.dtype([("item", "<u4"), ("sub", "<u2"), ("iend", "u1"), ("cost", "u1"),
                        ("j", "<u4"), ("n", "<u4"), ("start", "<u4"), ("len", "<u4"),
-                       ("strand", "u1"), ("o", "u1"), ("a", "u1"), ("pad", "u1"), ("pad2", "<u4"),
+                       ("strand", "u1"), ("o", "u1"), ("a", "u1"), ("clean", "u1"), ("pad2", "<u4"),
                        ("off", "<u8")])
 assert WINDOW_DTYPE.itemsize == 40 and CAND_DTYPE.itemsize == 40
 DBG_WINDOWS, DBG_VERIFIED, DBG_TASKS, DBG_CANDS0, DBG_CANDS1, DBG_FLAGS = range(6)

@@ -477,3 +477,49 @@ def test_screen_far_before_short_views(ctx):
         ctx.set_panel(0, panel, lib.DMX_BACK | (lib.DMX_RC if use_rc else 0), 0.3, 3)
         ctx.set_mode(lib.MODE_SINGLE)
         _assert_same(ctx.run(lib.pack(blob, offs, lens)), exp)
+
+
+@pytest.mark.parametrize("n_rate,where", [(0.004, "spread"), (0.03, "spread"),
+                                          (0.05, "adapters")])
+def test_n_dense_reads_and_clean_flags(ctx, n_rate, where, monkeypatch):
+    """the filter, the prefix verification and the index screen read a read's N
+    as A (still necessary conditions), and the filter marks a window `clean` when the no-match
+    mask is zero over every view position the window scan and the band DP read for it, which
+    then skip the mask.  Reads with N sprinkled everywhere, or right at and before the adapters
+    (inside the clean reach, where a wrong flag would turn an N into a match), two rounds on the
+    24 x 24 panels with --rc: every result byte equals the oracle's, and equals the run with the
+    clean flags off (DMX_NO_CLEAN) and with every stage reading the mask (no window is clean)."""
+    d = synth.generate("c2x24", n=6000, seed=int(n_rate * 1000) + (7 if where == "adapters" else 0))
+    seqs = synth.to_strings(d)
+    rng = np.random.default_rng(int(n_rate * 1e4))
+    out = []
+    for s in seqs:
+        b = bytearray(s.encode())
+        if where == "spread":
+            m = rng.random(len(b)) < n_rate
+        else:   # the ends: adapters and the positions just before / after them
+            m = np.zeros(len(b), bool)
+            k = min(len(b), 160)
+            m[:k] = rng.random(k) < 0.03
+            m[len(b) - k:] |= rng.random(k) < 0.03
+        for i in np.nonzero(m)[0]:
+            b[i] = ord("N")
+        out.append(b.decode())
+    blob, offs, lens = oracle.pack_ascii(out)
+    exp = oracle.run_batch(oracle.Panel(d["sp5"], oracle.FRONT),
+                           oracle.Panel(d["sp27"], oracle.BACK), blob, offs, lens, mode=1,
+                           threads=8)
+    ctx.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC)
+    ctx.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC)
+    ctx.set_mode(lib.MODE_TWO_ROUND)
+    p = lib.pack(blob, offs, lens)
+    got = ctx.run(p)
+    _assert_same(got, exp)
+    wins = ctx.debug_fetch(lib.DBG_VERIFIED, 1)
+    assert len(wins) > 0 and (wins["strand"] & 2).any()   # some windows run clean
+    monkeypatch.setenv("DMX_NO_CLEAN", "1")
+    ctx.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC)
+    ctx.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC)
+    got2 = ctx.run(p)
+    assert (ctx.debug_fetch(lib.DBG_VERIFIED, 1)["strand"] & 2).sum() == 0
+    assert got2.tobytes() == got.tobytes()
