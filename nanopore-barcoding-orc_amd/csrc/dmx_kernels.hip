@@ -252,13 +252,16 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
     }
 #undef DMX_SCAN_STEP
 
-    // 3' adapters: cutadapt also scans the last column (cells (i, n), i < m: adapter prefix
-    // aligned at the read end).  Flag it if any such cell would be accepted.
+    // 3' adapters: cutadapt also scans the last column (cells (i, n), i <= m: adapter prefix
+    // aligned at the read end).  Flag it if any such cell would be accepted.  Cell (m, n) is a
+    // last-row cell the column loop reports, except in an empty view (no column): there only the
+    // last-column scan sees it (cost m, score -2m: accepted at rates >= 1, e.g. -e 3 and m = 3).
     const uint32_t len = tv.len;
     if (lastcol && !front) {   // an empty view too: cells (i, 0) cost i (rate >= 1 accepts)
         int dd = 0;
         int ubl = -128;
-        for (int i = 1; i < m; ++i) {
+        const int ilast = len == 0 ? m : m - 1;
+        for (int i = 1; i <= ilast; ++i) {
             dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
             if (dd <= (int)acc[i]) {              // accepted for sure (aligned length is i)
                 ubl = max(ubl, i - 2 * dd);
@@ -471,6 +474,7 @@ struct CandOut {
     uint64_t rows0 = 0, rows1 = 0;      // rows by list (cost <= 3 / > 3)
     uint64_t pv = 0, mv = 0;            // column `len`: the rows' costs
     uint32_t seg = 0;
+    int mlist = -1;                     // cell (m, 0) of an empty 3' view: its list, -1 = none
 };
 
 // Sum of v over the wave's 64 lanes, in every lane.  Precondition: wave64 with ALL 64 lanes
@@ -500,8 +504,10 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) 
 // Called by all lanes of the wave at a wave-uniform point; lanes without a task hold nothing.
 __device__ __forceinline__ void emit_cands(const RoundArgs& R, const CandOut& co,
                                            const TaskView& tv, uint32_t item, int sub, int m) {
-    const uint32_t n1 = (uint32_t)(__popcll(co.cells & co.c2) + __popcll(co.rows1));
-    const uint32_t n0 = (uint32_t)(__popcll(co.cells & ~co.c2) + __popcll(co.rows0));
+    const uint32_t n1 = (uint32_t)(__popcll(co.cells & co.c2) + __popcll(co.rows1) +
+                                   (co.mlist == 1 ? 1 : 0));
+    const uint32_t n0 = (uint32_t)(__popcll(co.cells & ~co.c2) + __popcll(co.rows0) +
+                                   (co.mlist == 0 ? 1 : 0));
     uint32_t tot;
     const uint32_t pre = wave_excl_scan(n0 | (n1 << 16), tot);   // <= 64 x 128 per list
     if (tot == 0) return;                                        // wave-uniform
@@ -533,6 +539,8 @@ __device__ __forceinline__ void emit_cands(const RoundArgs& R, const CandOut& co
         const int cost = col_cost(co.pv, co.mv, i);
         put(cost > 3, make_cand(tv, item, sub, i, cost, tv.len));
     }
+    if (co.mlist >= 0)   // (m, 0): a last-row cell, key position t = j = 0 (band kernel)
+        put(co.mlist, make_cand(tv, item, sub, m, col_cost(co.pv, co.mv, m), tv.len));
 }
 
 template <int HB, class Sink>
@@ -652,15 +660,19 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
 #undef DMX_CAND_REC
 #undef DMX_CAND_VISIT
 #undef DMX_CAND_EQ
-    // 3' adapters: last-column cells (adapter prefix aligned at the read end)
+    // 3' adapters: last-column cells (adapter prefix aligned at the read end); cell (m, 0) of
+    // an empty view (no column loop reports it as a last-row cell) in `mrow`
     uint64_t rows = 0;
+    bool mrow = false;
     const uint32_t len = tv.len;
     if (lastcol && !front) {   // an empty view too: cells (i, 0) cost i (rate >= 1 accepts)
         int dd = 0;
-        for (int i = 1; i < m; ++i) {
+        const int ilast = len == 0 ? m : m - 1;
+        for (int i = 1; i <= ilast; ++i) {
             dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
             if (dd <= (int)acc[i]) {              // accepted for sure (aligned length is i)
-                rows |= 1ull << i;
+                if (i < m) rows |= 1ull << i;
+                else mrow = true;
                 lbk = max(lbk, lb_key(i - 3 * dd, tv.o, dd));
             }
         }
@@ -691,6 +703,11 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
             if (cost <= 3) out->rows0 |= 1ull << i;
             else out->rows1 |= 1ull << i;
         }
+        out->mlist = -1;
+        if (mrow) {
+            const int cost = col_cost(pv, mv, m);
+            if (viable_lb(lbk, m, tv.o, cost)) out->mlist = cost <= 3 ? 0 : 1;
+        }
         return lbk;
     }
     if (cm) flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
@@ -702,6 +719,14 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
         const Cand cd = make_cand(tv, item, sub, i, cost, len);
         if (cost <= 3) sink.st[0].push(cd);
         else sink.st[1].push(cd);
+    }
+    if (mrow) {
+        const int cost = col_cost(pv, mv, m);
+        if (viable_lb(lbk, m, tv.o, cost)) {
+            const Cand cd = make_cand(tv, item, sub, m, cost, len);
+            if (cost <= 3) sink.st[0].push(cd);
+            else sink.st[1].push(cd);
+        }
     }
     return lbk;
 }
@@ -2610,12 +2635,14 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
             }
         }
         drain();
-        if (c.lastcol && !front) {
+        if (c.lastcol && !front) {   // (m, 0) of an empty view: a last-row cell at t = 0
             int dd = 0;
-            for (int i = 1; i < m; ++i) {
+            const int ilast = tv.len == 0 ? m : m - 1;
+            for (int i = 1; i <= ilast; ++i) {
                 dd += (int)((pv >> (i - 1)) & 1ull) - (int)((mv >> (i - 1)) & 1ull);
                 if (dd <= (int)acc[i])
-                    consider(i, (int)tv.len, sl, dd, (uint64_t)tv.len + 1 + i);
+                    consider(i, (int)tv.len, sl, dd,
+                             i == m ? (uint64_t)tv.len : (uint64_t)tv.len + 1 + i);
             }
         }
         if (found) {

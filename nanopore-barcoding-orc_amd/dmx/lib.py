@@ -131,10 +131,12 @@ def load() -> ctypes.CDLL:
     L.dmx_mask_exceptions.restype = c_size
     L.dmx_host_register.argtypes = [P, c_size]
     L.dmx_host_unregister.argtypes = [P]
-    L.dmx_panel_reach.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int), P,
-                                  c_int, ctypes.c_double, c_int, c_int, P, c_int]
-    L.dmx_debug_bounds_selftest.argtypes = [P, P]
-    if L.dmx_abi_version() != ABI_VERSION:
+    if hasattr(L, "dmx_panel_reach"):
+        L.dmx_panel_reach.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int), P,
+                                      c_int, ctypes.c_double, c_int, c_int, P, c_int]
+        L.dmx_debug_bounds_selftest.argtypes = [P, P]
+    # DMX_ALLOW_ABI=1: load an older in-tree build for a regression A/B (tools/replay_sweep.py)
+    if L.dmx_abi_version() != ABI_VERSION and os.environ.get("DMX_ALLOW_ABI") != "1":
         raise DmxError("libdmx ABI mismatch")
     _lib = L
     return L

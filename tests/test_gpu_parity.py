@@ -523,3 +523,51 @@ def test_n_dense_reads_and_clean_flags(ctx, n_rate, where, monkeypatch):
     got2 = ctx.run(p)
     assert (ctx.debug_fetch(lib.DBG_VERIFIED, 1)["strand"] & 2).sum() == 0
     assert got2.tobytes() == got.tobytes()
+
+
+@pytest.mark.parametrize("variant", ["scan_band", "scan_ring", "filter_ring", "two_round"])
+def test_empty_reads_accept_whole_adapter_deletion(ctx, variant, monkeypatch):
+    """cutadapt's last-column scan runs i = first_i .. m: in an EMPTY read the cell (m, 0) of a
+    3' adapter (every adapter character deleted: cost m, score -2m) is seen only there, and is
+    accepted when the error allowance reaches m (an absolute -e >= m).  A parity sweep (seed 48,
+    round 5) found the GPU skipping it (row loops ran i < m).  Empty reads among short ones,
+    BACK panels with --rc, on the full scan with band or ring resolve, the windowed path, and
+    the second round of a two-round run (empty round-1 tails)."""
+    rng = np.random.default_rng(48)
+    if variant == "filter_ring":
+        suf = rand_dna(rng, 12)
+        panel = [rand_dna(rng, int(rng.integers(0, 4))) + suf for _ in range(6)]
+        e = 12.0
+    else:
+        panel = ["GACG", "AGCTG", "CCAA", "ACT", "GAC", "TTT", "CGTCC"]
+        e = 3.0
+    if variant == "scan_ring" or variant == "filter_ring":
+        monkeypatch.setenv("DMX_RESOLVE", "ring")
+    seqs = []
+    for _ in range(400):
+        u = rng.random()
+        seqs.append("" if u < 0.3 else rand_dna(rng, int(rng.integers(1, 12))))
+    seqs += ["", ""]
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    with lib.Context(0) as c:
+        if variant == "two_round":
+            front = [rand_dna(rng, 9) for _ in range(3)]
+            reads = [front[int(rng.integers(3))] + s if rng.random() < 0.7 else s for s in seqs]
+            blob, offs, lens = oracle.pack_ascii(reads)
+            exp = oracle.run_batch(oracle.Panel(front, oracle.FRONT),
+                                   oracle.Panel(panel, oracle.BACK, max_errors=e), blob, offs,
+                                   lens, mode=1, threads=8)
+            c.set_panel(0, front, lib.DMX_FRONT | lib.DMX_RC)
+            c.set_panel(1, panel, lib.DMX_BACK | lib.DMX_RC, e, 3)
+            c.set_mode(lib.MODE_TWO_ROUND)
+            got = c.run(lib.pack(blob, offs, lens))
+            assert (exp["bin2"] >= 0).any()
+        else:
+            exp = oracle.run_batch(oracle.Panel(panel, oracle.BACK, max_errors=e), None, blob,
+                                   offs, lens, mode=0, use_rc=True, threads=8)
+            c.set_panel(0, panel, lib.DMX_BACK | lib.DMX_RC, e, 3)
+            c.set_mode(lib.MODE_SINGLE)
+            got = c.run(lib.pack(blob, offs, lens))
+            empty = lens == 0
+            assert (exp["bin1"][empty] >= 0).all()   # the whole-deletion cell is accepted
+    _assert_same(got, exp)
