@@ -362,8 +362,8 @@ struct ShardMap {
     }
 };
 
-#ifndef DMX_WAVE_CAND_CAP
-#define DMX_WAVE_CAND_CAP 32   // rare: cells of earlier 64-column segments
+#ifndef DMX_WAVE_CAND_CAP   // rare: cells of earlier 64-column segments (16 from round 5:
+#define DMX_WAVE_CAND_CAP 16   // the window scan's per-lane vector rows need the LDS)
 #endif
 #ifndef DMX_WAVE_CAND_FLUSH
 #define DMX_WAVE_CAND_FLUSH (DMX_WAVE_CAND_CAP / 2)
@@ -543,7 +543,10 @@ __device__ __forceinline__ void emit_cands(const RoundArgs& R, const CandOut& co
         put(co.mlist, make_cand(tv, item, sub, m, col_cost(co.pv, co.mv, m), tv.len));
 }
 
-template <int HB, class Sink>
+// PSTRIDE: u64 between a match vector table's code rows; ZROW: the table has one code row per
+// read code 0..3 plus an all-zero row 4 for non-ACGT (the window scan's per-lane rows) instead
+// of the panel table's rows 4..7.
+template <int HB, class Sink, int PSTRIDE = kPeqStride, bool ZROW = false>
 __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink& sink,
                                                  const TaskView& tv, uint32_t item, int sub,
                                                  const uint64_t* peq, int A, const DevAdapter& ad,
@@ -607,8 +610,9 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
         hit(p0 + (uint32_t)q + 1u, dq.get(q) + e0);                                    \
     }
 #define DMX_CAND_EQ                                                                       \
-    const auto eqv = [&](int q) __attribute__((always_inline)) {                                                         \
-        return peq[(((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2)) * kPeqStride];   \
+    const auto eqv = [&](int q) __attribute__((always_inline)) {                          \
+        const uint32_t cq = (codes >> (2 * q)) & 3u, nq = (nb >> q) & 1u;                 \
+        return peq[(ZROW ? (nq ? 4u : cq) : (cq | (nq << 2))) * PSTRIDE];                 \
     };
 
     uint32_t p0 = js;
@@ -733,7 +737,7 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
 
 // The last adapter row's bit sits in the low or the high word of the 64-bit vectors; both
 // variants are compiled so the step needs no per-column select.
-template <class Sink>
+template <class Sink, int PSTRIDE = kPeqStride, bool ZROW = false>
 __device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const Sink& sink,
                                               const TaskView& tv, uint32_t item, int sub,
                                               const uint64_t* peq, int A, const DevAdapter& ad,
@@ -742,10 +746,10 @@ __device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const Sink& si
                                               uint32_t jhi, bool lastcol,
                                               CandOut* out = nullptr) {
     if (ad.m > 32)
-        return scan_task_cand_hb<1, Sink>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real,
-                                          jlo, jhi, lastcol, out);
-    return scan_task_cand_hb<0, Sink>(R, sink, tv, item, sub, peq, A, ad, acc, pacc, js, real, jlo,
-                                      jhi, lastcol, out);
+        return scan_task_cand_hb<1, Sink, PSTRIDE, ZROW>(R, sink, tv, item, sub, peq, A, ad, acc,
+                                                         pacc, js, real, jlo, jhi, lastcol, out);
+    return scan_task_cand_hb<0, Sink, PSTRIDE, ZROW>(R, sink, tv, item, sub, peq, A, ad, acc,
+                                                     pacc, js, real, jlo, jhi, lastcol, out);
 }
 
 #define DMX_CAND_STAGE                                                                    \
@@ -2225,12 +2229,22 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
 // (piece, adapter) — in a block-uniform grid stride over the device-side count, so that the
 // block can flush its staged records between strides.
 // One (window or piece, adapter) task of the window scan.
+// Window-scan match vectors: the 64 lanes of a wave scan random (task,
+// adapter, code) triples, and a gather of 64-bit vectors from the panel's [code][adapter] table
+// conflicted ~2 extra LDS cycles per read.  A lane's adapter is fixed for its task, so it copies
+// the adapter's four vectors into rows of its own (s_lrow[code][thread], plus a zero row 4 for
+// non-ACGT codes): the 32 lanes of a ds_read_b64 group then always read 32 distinct bank pairs.
+#ifndef DMX_WSCAN_LANE_ROWS
+#define DMX_WSCAN_LANE_ROWS 1
+#endif
+constexpr int kLaneRows = 5;
+
 template <bool BAND, class ClStage, class Sink>
 __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, int a, int A,
                                            const uint64_t* s_peq, const int8_t* s_acc,
                                            const int8_t* s_pacc, const ClStage& st,
                                            const Sink& sink, CandOut& co, TaskView& tv,
-                                           int& sub) {
+                                           int& sub, uint64_t* lrow) {
     sub = w.o * A + a;
     tv.read = 0;
     tv.n = w.n;
@@ -2246,11 +2260,18 @@ __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, 
     const bool real = js <= 0;
     if (real) js = 0;
     int lb;
-    if constexpr (BAND)
+    if constexpr (BAND && DMX_WSCAN_LANE_ROWS) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) lrow[c * kScanBlock] = s_peq[c * kPeqStride + a];
+        lb = scan_task_cand<Sink, kScanBlock, true>(R, sink, tv, w.item, sub, lrow, A, ad,
+                                                    s_acc + 72 * a, s_pacc + 72 * a,
+                                                    (uint32_t)js, real, w.j1, w.j2,
+                                                    w.lastcol != 0, &co);
+    } else if constexpr (BAND) {
         lb = scan_task_cand(R, sink, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
                             s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2,
                             w.lastcol != 0, &co);
-    else
+    } else
         lb = scan_task(R, st, tv, w.item, sub, s_peq + a, A, ad, s_acc + 72 * a,
                        s_pacc + 72 * a, (uint32_t)js, real, w.j1, w.j2, w.lastcol != 0);
     const uint32_t slot = slot_of(R, w.item, sub);
@@ -2271,6 +2292,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     __shared__ uint32_t s_clcnt, s_clbase;
     __shared__ Cand s_wcand[BAND ? kScanBlock / 64 : 1][2][kWaveCandCap];
     __shared__ uint32_t s_wcn[kScanBlock / 64][2];
+    constexpr bool kRows = BAND && DMX_WSCAN_LANE_ROWS;
+    __shared__ uint64_t s_lrow[kRows ? kLaneRows * kScanBlock : 1];   // [code][thread]
+    if constexpr (kRows) s_lrow[4 * kScanBlock + threadIdx.x] = 0ull;   // non-ACGT: no match
+    uint64_t* const lrow = s_lrow + (kRows ? threadIdx.x : 0u);
 #ifdef DMX_WSCAN_LDS_PAD   // A/B: occupancy cap through LDS
     __shared__ uint32_t s_pad[DMX_WSCAN_LDS_PAD / 4];
     if (threadIdx.x == 0) s_pad[R.n_items & 7] = 0;
@@ -2305,7 +2330,8 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
       // c2x24: wave max / mean 1.90 -> 1.09; window scan 4.8 -> 4.1 ms).  3' panels' tasks
       // are already even (1.08), and there the sort only costs (2.4 -> 2.6 ms): not sorted.
       const bool sorted = R.panel->where == kFront;
-      __shared__ uint32_t s_ord[kSortGroup];
+      __shared__ uint16_t s_ord[kSortGroup];   // (indices < kSortGroup: 16 bits halve the LDS)
+      static_assert(kSortGroup <= 65536, "sort-group indices are 16-bit");
       __shared__ uint32_t s_bin[kSortBins];
       __shared__ uint8_t s_mk[kMaxAdapters];
       for (int a = threadIdx.x; a < A; a += blockDim.x)
@@ -2345,7 +2371,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
 #pragma unroll
             for (int e = 0; e < PER; ++e) {
                 const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
-                if (li < gn) s_ord[s_bin[key[e]] + pos[e]] = li;
+                if (li < gn) s_ord[s_bin[key[e]] + pos[e]] = (uint16_t)li;
             }
             __syncthreads();
             }
@@ -2359,7 +2385,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                     const Window w = tl[sm.phys(gb + (sorted ? s_ord[li] : li))];
                     item = w.item;
                     wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, st, sink, co,
-                                     tv, sub);
+                                     tv, sub, lrow);
                 }
                 if constexpr (BAND) {
                     emit_cands(R, co, tv, item, sub, R.panel->ad[tv.a].m);
@@ -2393,7 +2419,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             const Window w = wl[sm.phys((uint32_t)(t / A))];
             const int a = (int)(t % A);
             item = w.item;
-            wscan_task<BAND>(R, w, a, A, s_peq, s_acc, s_pacc, st, sink, co, tv, sub);
+            wscan_task<BAND>(R, w, a, A, s_peq, s_acc, s_pacc, st, sink, co, tv, sub, lrow);
         }
         if constexpr (BAND) {                        // wave-uniform: no block barrier
             emit_cands(R, co, tv, item, sub, R.panel->ad[tv.a].m);

@@ -34,6 +34,25 @@ options:
             whose segments have the greatest summed length (usable bases) over the first -Y
             QC-passing reads (ties -> the smaller cutoff)
 
+[UNVERIFIED] choices (RULES below; the build implements the first reading of each, the drop-in
+and the kernels follow it): every choice pychopper 2.7.10's source would settle has a switch with
+one alternative reading, and tools/pychopper_cases.py holds one small case per switch whose
+outputs differ between the two readings (tests/test_chop.py checks that they do).
+tools/parity_vs_pychopper.sh runs those cases through a real pychopper 2.7.x wherever one is
+installed and diffs the outputs against the drop-in's: a DIFF names the switch to flip.
+  tune_grid    autotune grid: linspace(0.1, 0.6, -L) | "0.0-0.5": linspace(0.0, 0.5, -L)
+  tune_sample  autotune reads: the first -Y QC-passing reads | "stride": -Y reads spread evenly
+               over all QC-passing reads (every ceil(n / Y)-th), as a sample of the whole input
+  tune_score   autotune criterion: most usable bases (summed segment length) | "reads": most
+               reads with exactly one segment (the round-1/2 stand-in)
+  seg_score    best path over a read's candidate segments: greatest summed length | "count":
+               most segments, then greatest summed length
+  naming       segment records: "{start}:{stop}|{id} strand=+|-{comment}" | "nostrand":
+               "{start}:{stop}|{id}{comment}" (the strand only implied by the orientation)
+The `-k LSK114` kit is not a switch: with -b, -c, -m, -Q and -p given (01_pychopper.sh:45-57)
+the restatement reads it as unused, and the reference holds no LSK114 primer or parameter file
+that an alternative reading could draw on, so no case can separate it (parity unpinned).
+
 Only tests/ (and bench.py's cpu_baseline leg, through `batch_hit_counts`) use this module, as
 the checker of libdmx's `dmx_chop_*` (HIP) path and of the `bin/pychopper` drop-in.
 """
@@ -48,10 +67,19 @@ import oracle as _orc
 
 AUTOTUNE_SAMPLES = 30
 
+# [UNVERIFIED] readings (module docstring); tests flip one at a time and restore it
+DEFAULT_RULES = {"tune_grid": "0.1-0.6", "tune_sample": "first", "tune_score": "bases",
+                 "seg_score": "length", "naming": "strand"}
+ALT_RULES = {"tune_grid": "0.0-0.5", "tune_sample": "stride", "tune_score": "reads",
+             "seg_score": "count", "naming": "nostrand"}
+RULES = dict(DEFAULT_RULES)
+
 
 def autotune_cutoffs(samples: int = AUTOTUNE_SAMPLES):
-    """The -q grid tried without -q: `samples` values evenly spaced over [0.1, 0.6]."""
-    return [float(x) for x in np.linspace(0.1, 0.6, num=samples)]
+    """The -q grid tried without -q: `samples` values evenly spaced over [0.1, 0.6]
+    (RULES["tune_grid"] "0.0-0.5": over [0.0, 0.5])."""
+    lo, hi = (0.1, 0.6) if RULES["tune_grid"] == "0.1-0.6" else (0.0, 0.5)
+    return [float(x) for x in np.linspace(lo, hi, num=samples)]
 
 _COMP = str.maketrans("ACGTUMRWSYKVHDBNacgtumrwsykvhdbn", "TGCAAKYWSRMBDHVNtgcaakywsrmbdhvn")
 _IUPAC = {"A": "A", "C": "C", "G": "G", "T": "T", "U": "T", "R": "AG", "Y": "CT", "S": "CG",
@@ -183,13 +211,20 @@ def segments(hits, rules, keep: bool):
             a = h1[0] if keep else h1[1]
             b = h2[1] if keep else h2[0]
             cand[i] = (a, max(a, b), rs[1], rs[0])
-    best = [0] * (c + 2)    # best[i]: greatest summed length using hits i.. only
+    # best[i]: the best (segment count, summed length) using hits i.. only, compared by
+    # summed length (RULES["seg_score"] "length") or by count, then length ("count")
+    by_count = RULES["seg_score"] == "count"
+    best = [(0, 0)] * (c + 2)
     take = [False] * c
+
+    def key(v):
+        return v if by_count else (v[1], v[0])
+
     for i in range(c - 2, -1, -1):
         best[i] = best[i + 1]
         if cand[i] is not None:
-            t = cand[i][1] - cand[i][0] + best[i + 2]
-            if t >= best[i + 1]:
+            t = (best[i + 2][0] + 1, cand[i][1] - cand[i][0] + best[i + 2][1])
+            if key(t) >= key(best[i + 1]):
                 best[i], take[i] = t, True
     segs, i = [], 0
     while i + 1 < c:
@@ -221,6 +256,8 @@ def seg_name(head: str, a: int, b: int, strand: int) -> str:
         if ch in " \t":
             cut = i
             break
+    if RULES["naming"] == "nostrand":
+        return f"{a}:{b}|{head[:cut]}{head[cut:]}"
     return f"{a}:{b}|{head[:cut]} strand={'-' if strand else '+'}{head[cut:]}"
 
 
@@ -256,10 +293,17 @@ def autotune(records, primers, config: str, keep: bool = True, min_qual: float =
     over the first `sample` QC-passing reads; ties -> the smaller cutoff."""
     labs = labels(primers)
     rules = parse_config(config, [p[0] for p in primers])
-    pool = [s for _, s, q in records if fasta or mean_qual(q) >= min_qual][:sample]
+    pool = [s for _, s, q in records if fasta or mean_qual(q) >= min_qual]
+    if RULES["tune_sample"] == "stride" and len(pool) > sample:
+        step = -(-len(pool) // sample)
+        pool = pool[::step]
+    pool = pool[:sample]
     best, best_n = None, -1
     for q in autotune_cutoffs(samples):
-        c = sum(usable_length(segments(read_hits(labs, s, q), rules, keep)) for s in pool)
+        if RULES["tune_score"] == "reads":
+            c = sum(1 for s in pool if len(segments(read_hits(labs, s, q), rules, keep)) == 1)
+        else:
+            c = sum(usable_length(segments(read_hits(labs, s, q), rules, keep)) for s in pool)
         if c > best_n:
             best, best_n = q, c
     return best

@@ -486,3 +486,55 @@ def test_fused_reorient_loop_equals_pychopper_then_loop(tmp_path, q):
                 j.pop("input")
             assert ja == jb, o
     assert n_rec > 0.5 * len(seqs)
+
+
+def _pychopper_cases():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "pychopper_cases", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
+            __file__))), "tools", "pychopper_cases.py"))
+    pc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pc)
+    return pc
+
+
+def test_unverified_pychopper_cases_tell_the_readings_apart():
+    """Every [UNVERIFIED] pychopper switch (oracle/chopper.py RULES: autotune grid, autotune
+    sample, autotune criterion, best-path score, record naming) has a case in
+    tools/pychopper_cases.py whose outputs differ between the build's reading and the
+    alternative one, so tools/parity_vs_pychopper.sh can settle each against a real
+    pychopper 2.7.x; flipping one switch leaves the other cases' distinctions to their own."""
+    pc = _pychopper_cases()
+    assert set(v[0] for v in pc.CASES.values()) == set(ochop.DEFAULT_RULES)
+    for name in pc.CASES:
+        c = pc.build(name)
+        a = pc.oracle_outputs(c)
+        b = pc.oracle_outputs(c, {c["switch"]: ochop.ALT_RULES[c["switch"]]})
+        assert a != b, name
+        assert ochop.RULES == ochop.DEFAULT_RULES     # restored
+        assert len(a["pass"]) + len(a["rescued"]) > 0, name
+
+
+@pytest.mark.gpu
+def test_unverified_pychopper_cases_match_the_default_readings(tmp_path):
+    """The drop-in (bin/pychopper) on every [UNVERIFIED] case: outputs and tuned cutoff equal
+    the oracle's default readings (what tools/parity_vs_pychopper.sh compares with a real
+    pychopper 2.7.x)."""
+    pc = _pychopper_cases()
+    cases = tmp_path / "cases"
+    pc.write(str(cases))
+    for row in open(cases / "cases.tsv").read().splitlines():
+        name, inp, opts = row.split("\t")
+        o = tmp_path / name
+        with open(f"{o}_pass.fastq", "wb") as fh:
+            subprocess.run([BIN] + opts.split() + ["-w", f"{o}_rescued.fastq", "-u",
+                                                   f"{o}_unclass.fastq", "-l", f"{o}_short.fastq",
+                                                   "-S", f"{o}_stats.out", "-t", "4", inp],
+                           stdout=fh, check=True, cwd=str(cases))
+        exp = pc.oracle_outputs(pc.build(name))
+        st = dict(((a, b), v) for a, b, v in (line.split("\t") for line in
+                                              open(f"{o}_stats.out").read().splitlines()[1:]))
+        assert float(st[("Parameters", "cutoff")]) == exp["cutoff"], name
+        fq = lambda recs: [("@" + h, s, q) for h, s, q in recs]  # noqa: E731
+        for k in ("pass", "rescued", "unclass", "short"):
+            assert read_fastq(f"{o}_{k}.fastq") == fq(exp[k]), (name, k)
