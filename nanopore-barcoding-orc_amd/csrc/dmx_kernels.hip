@@ -1026,7 +1026,10 @@ struct SegState {
 
 // The filter's clean-flag history spans clean_reach (<= 128) positions before the segment and
 // the segment itself in 16-position chunks: 64 bits hold it for spans up to 768.
-constexpr bool kCleanHist = (kSegSpan + 128) / 16 + 4 <= 64;
+#ifndef DMX_CLEAN_OFF   // A/B: 1 = no clean flags (every window loads the mask, round 4)
+#define DMX_CLEAN_OFF 0
+#endif
+constexpr bool kCleanHist = !DMX_CLEAN_OFF && (kSegSpan + 128) / 16 + 4 <= 64;
 
 // Is the no-match mask zero over the view positions an exact stage reads for window [w1, w2]
 // (columns): [w1 - rb, w2 - 1], clipped at the view start?  (Positions outside the view are
@@ -2231,11 +2234,14 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
 // One (window or piece, adapter) task of the window scan.
 // Window-scan match vectors: the 64 lanes of a wave scan random (task,
 // adapter, code) triples, and a gather of 64-bit vectors from the panel's [code][adapter] table
-// conflicted ~2 extra LDS cycles per read.  A lane's adapter is fixed for its task, so it copies
-// the adapter's four vectors into rows of its own (s_lrow[code][thread], plus a zero row 4 for
-// non-ACGT codes): the 32 lanes of a ds_read_b64 group then always read 32 distinct bank pairs.
+// conflicts ~2 extra LDS cycles per read.  DMX_WSCAN_LANE_ROWS=1 (A/B): a lane copies its task's
+// adapter vectors into rows of its own (s_lrow[code][thread], plus a zero row 4 for non-ACGT
+// codes), so the 32 lanes of a ds_read_b64 group read 32 distinct bank pairs.  Measured (round
+// 5, profiles/r5_ab_wscan_lane_rows.txt): conflict cycles per LDS instruction 1.94 / 2.01 ->
+// 0.62 / 0.83, window scan time unchanged (3.64 / 2.18 vs 3.62 / 2.16 ms): LDS waits are 0.1 %
+// of its wave cycles, it waits on its global gathers.  Off by default (10 KB more LDS).
 #ifndef DMX_WSCAN_LANE_ROWS
-#define DMX_WSCAN_LANE_ROWS 1
+#define DMX_WSCAN_LANE_ROWS 0
 #endif
 constexpr int kLaneRows = 5;
 
