@@ -1053,6 +1053,9 @@ __device__ __forceinline__ void myers_step_top(uint32_t eq, uint32_t& pv, uint32
     const uint32_t xh = (((eq & pv) + pv) ^ pv) | eq;
     const uint32_t ph = mv | ~(xh | pv);
     const uint32_t mh = pv & xh;
+    // (round 5 A/B: the +1 / -1 as shifts + v_add3 instead of the carries removes the VCC
+    // hazard s_nops, 33 -> 3 per 16 columns, but lengthens the dependent chain: filter 11.6 ->
+    // 13.9 ms, profiles/r5_ab_filter_cost_shift.txt)
     uint32_t cp, cm;
     const uint32_t ph2 = __builtin_addc(ph, ph, 0u, &cp);
     const uint32_t mh2 = __builtin_addc(mh, mh, 0u, &cm);
