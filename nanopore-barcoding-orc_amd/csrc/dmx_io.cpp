@@ -1752,21 +1752,31 @@ inline void put32(uint8_t* p, uint32_t v) {
 // Level 1 (`-Z`) is Huffman-only deflate: on FASTQ (2-bit-entropy bases, skewed qualities)
 // zlib's level-1 LZ77 finds little and costs most of the time — zlib's Huffman-only strategy
 // measured 2.6x faster and 4 % smaller here, and the table-driven encoder of dmx_deflate.h is
-// several times faster again (same kind of stream).  Other levels use libdeflate.  Appends to
-// `out`.
+// several times faster again (same kind of stream).  Appends to `out`.
+// Levels 2..9 use the record-aware encoder of dmx_deflate.h (fq_deflate: LZ77 in header lines
+// only, sequence lines and the rest in blocks with codes of their own): on FASTQ its members
+// are smaller than zlib's and libdeflate's at any level, at several times libdeflate -5's speed
+// (profiles/r5_gzip_levels.json), so every level above 1 gets it.  DMX_GZIP_LIBDEFLATE=1 selects
+// libdeflate at the requested level instead.  Level 0: stored blocks (libdeflate).
+const bool kLibdeflateLevels = [] {
+    const char* e = getenv("DMX_GZIP_LIBDEFLATE");
+    return e && *e && strcmp(e, "0") != 0;
+}();
+
 bool gzip_member(const uint8_t* src, size_t n, int level, Bytes& out) {
-    if (level == 1) {
+    if (level == 1 || (level >= 2 && !kLibdeflateLevels)) {
         const size_t base = out.size();
         const size_t hdr = 24;
         out.resize(base + hdr + dmxz::huff_bound(n) + 16);
         uint8_t* h = out.data() + base;
-        const uint8_t fixed[12] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 4, 3, 12, 0};
+        const uint8_t fixed[12] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, (uint8_t)(level == 1 ? 4 : 0), 3, 12, 0};
         memcpy(h, fixed, 12);
         h[12] = 'D';
         h[13] = 'X';
         h[14] = 8;
         h[15] = 0;
-        const size_t clen = dmxz::huff_deflate(src, n, h + hdr);
+        const size_t clen = level == 1 ? dmxz::huff_deflate(src, n, h + hdr)
+                                       : dmxz::fq_deflate(src, n, h + hdr);
         const size_t total = hdr + clen + 8;
         put32(h + 16, (uint32_t)total);
         put32(h + 20, (uint32_t)n);

@@ -247,7 +247,8 @@ def run(argv=None, keep_contexts: bool = False) -> int:
     _phase("close", marks)
     if marks is not None:
         print("dmx cli phases: " + " ".join(f"{k}={v:.3f}" for k, v in marks) +
-              f" exec_to_import={_EXEC_TO_IMPORT:.2f}", file=sys.stderr)
+              f" exec_to_import={_EXEC_TO_IMPORT:.2f} peak_rss_mb={nio.peak_rss_mb():.0f}",
+              file=sys.stderr)
     return 0
 
 

@@ -318,8 +318,8 @@ def run(argv=None) -> int:
     if reo is not None:
         prof.update({"reo_" + k: v for k, v in reo.prof.items()})
     if os.environ.get("DMX_PROFILE_IO"):
-        print("io profile (s): " + ", ".join(f"{k} {v:.3f}" for k, v in prof.items()),
-              file=sys.stderr)
+        print("io profile (s): " + ", ".join(f"{k} {v:.3f}" for k, v in prof.items()) +
+              f"; peak_rss_mb {nio.peak_rss_mb():.0f}", file=sys.stderr)
     # the devices' (SP5, SP27) bin counts (RCCL-summed over GPUs) vs the per-read results
     st1.check_totals(totals[1:, :].sum(axis=1))
     for i, s in enumerate(st2):

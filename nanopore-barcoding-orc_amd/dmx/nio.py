@@ -242,6 +242,19 @@ def _read_int(path: str):
         return None
 
 
+def peak_rss_mb() -> float:
+    """This process's peak resident set (VmHWM, MB): what a SLURM job's --mem limit meets.
+    0.0 where /proc is not readable."""
+    try:
+        with open("/proc/self/status") as fh:
+            for line in fh:
+                if line.startswith("VmHWM:"):
+                    return int(line.split()[1]) / 1024
+    except (OSError, ValueError, IndexError):
+        pass
+    return 0.0
+
+
 def available_memory_bytes():
     """Memory this process can still take: the smaller of MemAvailable (/proc/meminfo) and the
     cgroup's limit minus its usage (v2 memory.max / memory.current, or v1 limit / usage; a

@@ -275,6 +275,63 @@ def test_huffman_gzip_members_inflate_with_zlib():
     assert len(nio.gzip_member(fq, 1)) < 0.45 * len(fq)
 
 
+def test_record_aware_gzip_members_inflate_with_zlib():
+    """Levels >= 2 (csrc/dmx_deflate.h fq_deflate: LZ77 matches in header lines, sequence lines
+    in blocks of their own) are standard gzip on every shape of text the writers can be handed
+    or a member can be cut from: records cut mid-line at both ends, quality lines starting with
+    '@' or '>' (not headers: they follow a lone "+"), "+name" separator lines, empty sequence
+    lines, FASTA, headers longer than a match (258) repeated further apart than 4 KiB and
+    than the 32 KiB window, non-FASTQ bytes, and short inputs."""
+    import gzip
+    import zlib
+    rng = np.random.default_rng(11)
+
+    def dna(n):
+        return bytes(rng.choice(list(b"ACGT"), n).astype(np.uint8))
+
+    def qual(n, first=None):
+        q = bytes((rng.integers(2, 41, n) + 33).astype(np.uint8))
+        return (first + q[1:]) if first and n else q
+
+    long_head = b"@" + b"x" * 300 + b" runid=" + b"ab12" * 20
+    recs = []
+    for i in range(3000):
+        n = int(rng.integers(0, 400)) if i % 7 else 0
+        head = long_head + b" %d" % i if i % 5 == 0 else b"@read%d ch=%d runid=%s" % (
+            i, i % 512, b"0f" * 20)
+        sep = b"+" if i % 11 else b"+" + head[1:]
+        recs.append(head + b"\n" + dna(n) + b"\n" + sep + b"\n" +
+                    qual(n, first=b"@>"[i % 2:i % 2 + 1] if i % 3 == 0 else None) + b"\n")
+    fq = b"".join(recs)
+    far = b"".join(b"@" + b"h" * 40 + b"%d\n" % i + dna(20000) + b"\n+\n" + qual(20000) + b"\n"
+                   for i in range(4))          # the previous header 40 kB back: no window match
+    fa = b"".join(b">seq%d descr=abc%d\n%s\n" % (i, i % 9, dna(int(rng.integers(1, 300))))
+                  for i in range(2000))
+    cases = [b"A", b"@\n", b"@r\nAC\n+\nII\n", fq, fq[12345:612345], fa, fa[777:], far,
+             rng.integers(0, 256, size=300_000, dtype=np.uint8).tobytes(),
+             b"@same header line\n" * 40_000, fq * 2]
+    for data in cases:
+        for level in (5, 9):
+            m = nio.gzip_member(data, level)
+            assert zlib.decompress(m, 31) == data
+        assert gzip.decompress(nio.gzip_member(data, 2)) == data
+    assert nio.gzip_member(b"", 5) and gzip.decompress(nio.gzip_member(b"", 5)) == b""
+
+
+def test_record_aware_level5_is_smaller_than_zlib_level5():
+    """cutadapt's default --compression-level 5 (dmx/cli.py): on nanopore-style FASTQ
+    (tests/fastq_like.py) the writers' 1 MiB members come out smaller than zlib -5's and
+    libdeflate -5's (profiles/r5_gzip_levels.json: 2.32 vs 2.10 and 2.15 on 48 MB)."""
+    import zlib
+
+    from fastq_like import nanopore_fastq
+    data = nanopore_fastq(3 << 20, seed=3)
+    M = 1 << 20
+    ours = sum(len(nio.gzip_member(data[k:k + M], 5)) for k in range(0, len(data), M))
+    z5 = sum(len(zlib.compress(data[k:k + M], 5)) for k in range(0, len(data), M))
+    assert ours < 0.95 * z5
+
+
 def test_retained_outputs_read_back_without_the_file(tmp_path):
     """dmx_sink_retain (the resident server's round-2 cache, 02_cutadapt_loop.sh:91-103): a
     reader of an unchanged retained .gz output gets the same records from memory; a changed
