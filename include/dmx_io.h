@@ -51,9 +51,17 @@ typedef struct dmx_reader dmx_reader;
 typedef struct dmx_sink dmx_sink;
 
 int dmx_io_abi_version(void);
+/* Process-wide memory budget of the readers' and writers' buffers, in bytes (0 = none, the
+ * default): with a budget, the parallel inflate cuts smaller chunks (its working set about
+ * budget / 16), the read-ahead blocks shrink, and the pools of recycled batch buffers hold at
+ * most budget / 32 each.  Readers opened later use it.  The batch size is the caller's
+ * (dmx/nio.py batch_bytes_for_budget).  Returns the previous budget. */
+uint64_t dmx_io_set_memory_budget(uint64_t bytes);
 /* One gzip member of src[0, n) in the writers' format (RFC 1952 with a "DX" size subfield;
- * level 1 = Huffman-only DEFLATE, other levels libdeflate at that level): written to out (cap bytes, at least
- * 2 n + 4096), its length to *out_len.  0 on success, negative if cap is too small. */
+ * level 1 = Huffman-only DEFLATE, levels 2..9 the record-aware encoder (header-line LZ77,
+ * sequence lines in blocks of their own; DMX_GZIP_LIBDEFLATE=1: libdeflate at that level), 0 =
+ * stored): written to out (cap bytes, at least 2 n + 4096), its length to *out_len.  0 on
+ * success, negative if cap is too small. */
 int dmx_io_gzip(const uint8_t* src, size_t n, int level, uint8_t* out, size_t cap,
                 size_t* out_len);
 

@@ -12,13 +12,20 @@
 //     dmx_run_multi): ncclCommInitAll over the contexts' devices, grouped calls;
 //   * dmx_comm_unique_id + dmx_comm_init_rank — one process per GPU (bench.py under torchrun):
 //     rank 0 draws the id, the launcher's control plane hands it to the other ranks.
+//
+// librccl.so is opened on the first communicator, not linked: its fat binary (573 MB in this
+// ROCm) made ~570 MB of every single-GPU process's resident set, CLI calls and the resident
+// server included, against the reference jobs' --mem=4G / 2G (profiles/r5_rss_probe*.json).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <atomic>
 #include <cstring>
+#include <mutex>
 #include <set>
 #include <string>
+#include <type_traits>
 
 #include "dmx_internal.h"
 
@@ -26,12 +33,63 @@ using namespace dmx;
 
 static_assert(sizeof(ncclUniqueId) == DMX_COMM_ID_BYTES, "RCCL unique id size");
 
+namespace {
+
+// The RCCL entry points dmx uses, resolved from librccl.so.1 at first use.
+struct Rccl {
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+    std::string err;   // why loading failed ("" = loaded)
+};
+
+const Rccl* rccl(std::string* why = nullptr) {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* name = getenv("DMX_RCCL_LIB");
+        void* h = dlopen(name && *name ? name : "librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char* e = dlerror();
+            r.err = std::string("cannot load RCCL: ") + (e ? e : "dlopen failed");
+            return;
+        }
+        bool ok = true;
+        auto sym = [&](auto& fn, const char* s) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, s));
+            ok = ok && fn != nullptr;
+        };
+        sym(r.GetUniqueId, "ncclGetUniqueId");
+        sym(r.CommInitRank, "ncclCommInitRank");
+        sym(r.CommInitAll, "ncclCommInitAll");
+        sym(r.CommDestroy, "ncclCommDestroy");
+        sym(r.AllReduce, "ncclAllReduce");
+        sym(r.GroupStart, "ncclGroupStart");
+        sym(r.GroupEnd, "ncclGroupEnd");
+        sym(r.GetErrorString, "ncclGetErrorString");
+        if (!ok) r.err = "cannot load RCCL: a symbol is missing from the library";
+    });
+    if (!r.err.empty()) {
+        if (why) *why = r.err;
+        return nullptr;
+    }
+    return &r;
+}
+
+}  // namespace
+
 namespace dmx {
 
 void comm_release(Ctx* c) {
     if (c->comm) {
         hipSetDevice(c->device);
-        ncclCommDestroy(c->comm);
+        if (const Rccl* R = rccl()) R->CommDestroy(c->comm);
         c->comm = nullptr;
     }
     c->comm_ranks = 0;
@@ -48,8 +106,16 @@ namespace {
 std::atomic<uint64_t> g_group{0};   // distinguishes communicator sets made by dmx_comm_init_all
 
 int nccl_fail(Ctx* c, const char* what, ncclResult_t r) {
-    c->err = std::string(what) + ": " + ncclGetErrorString(r);
+    c->err = std::string(what) + ": " + rccl()->GetErrorString(r);
     return DMX_E_HIP;
+}
+
+// RCCL for ctx c's call, or nullptr with c->err set.
+const Rccl* rccl_for(Ctx* c) {
+    std::string why;
+    const Rccl* R = rccl(&why);
+    if (!R && c) c->err = why;
+    return R;
 }
 
 }  // namespace
@@ -58,14 +124,18 @@ extern "C" {
 
 int dmx_comm_unique_id(uint8_t* id) {
     if (!id) return DMX_E_INVALID;
+    const Rccl* R = rccl();
+    if (!R) return DMX_E_UNSUPPORTED;
     ncclUniqueId u;
-    if (ncclGetUniqueId(&u) != ncclSuccess) return DMX_E_HIP;
+    if (R->GetUniqueId(&u) != ncclSuccess) return DMX_E_HIP;
     std::memcpy(id, &u, sizeof(u));
     return DMX_OK;
 }
 
 int dmx_comm_init_rank(dmx_ctx* c, const uint8_t* id, int n_ranks, int rank) {
     if (!c || !id || n_ranks <= 0 || rank < 0 || rank >= n_ranks) return DMX_E_INVALID;
+    const Rccl* R = rccl_for(c);
+    if (!R) return DMX_E_UNSUPPORTED;
     comm_release(c);
     if (hipSetDevice(c->device) != hipSuccess) {
         c->err = "dmx_comm_init_rank: hipSetDevice failed";
@@ -74,7 +144,7 @@ int dmx_comm_init_rank(dmx_ctx* c, const uint8_t* id, int n_ranks, int rank) {
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     ncclComm_t comm = nullptr;
-    const ncclResult_t r = ncclCommInitRank(&comm, n_ranks, u, rank);
+    const ncclResult_t r = R->CommInitRank(&comm, n_ranks, u, rank);
     if (r != ncclSuccess) return nccl_fail(c, "ncclCommInitRank", r);
     c->comm = comm;
     c->comm_ranks = n_ranks;
@@ -96,9 +166,11 @@ int dmx_comm_init_all(dmx_ctx* const* ctxs, int n_ctx) {
         ctxs[0]->err = "dmx_comm_init_all: contexts must be on distinct devices";
         return DMX_E_UNSUPPORTED;
     }
+    const Rccl* R = rccl_for(ctxs[0]);
+    if (!R) return DMX_E_UNSUPPORTED;
     for (int k = 0; k < n_ctx; ++k) comm_release(ctxs[k]);
     ncclComm_t comms[64] = {};
-    const ncclResult_t r = ncclCommInitAll(comms, n_ctx, devlist);
+    const ncclResult_t r = R->CommInitAll(comms, n_ctx, devlist);
     if (r != ncclSuccess) return nccl_fail(ctxs[0], "ncclCommInitAll", r);
     const uint64_t group = ++g_group;
     for (int k = 0; k < n_ctx; ++k) {
@@ -130,8 +202,8 @@ int dmx_allreduce_counts(dmx_ctx* c, uint64_t* out, size_t n_out) {
     // idempotent per exec: a second call returns the summed counts without summing them again
     // (every rank follows the same call sequence, so either all ranks reduce or none does)
     if (!c->counts_reduced) {
-        const ncclResult_t r = ncclAllReduce(c->d_counts, c->d_counts, c->n_counts, ncclUint64,
-                                             ncclSum, c->comm, c->stream);
+        const ncclResult_t r = rccl()->AllReduce(c->d_counts, c->d_counts, c->n_counts,
+                                                 ncclUint64, ncclSum, c->comm, c->stream);
         if (r != ncclSuccess) return nccl_fail(c, "ncclAllReduce", r);
         c->counts_reduced = true;
     }
@@ -166,13 +238,14 @@ int allreduce_counts_group(dmx_ctx* const* ctxs, int n_ctx, uint64_t* out, size_
         ctxs[0]->err = "counts buffer too small";
         return DMX_E_INVALID;
     }
-    ncclResult_t r = ncclGroupStart();
+    const Rccl* R = rccl();   // loaded: every context here has a communicator
+    ncclResult_t r = R->GroupStart();
     for (int k = 0; k < n_ctx && r == ncclSuccess; ++k) {
         Ctx* c = ctxs[k];
         hipSetDevice(c->device);
-        r = ncclAllReduce(c->d_counts, c->d_counts, nc, ncclUint64, ncclSum, c->comm, c->stream);
+        r = R->AllReduce(c->d_counts, c->d_counts, nc, ncclUint64, ncclSum, c->comm, c->stream);
     }
-    const ncclResult_t r2 = ncclGroupEnd();
+    const ncclResult_t r2 = R->GroupEnd();
     if (r != ncclSuccess) return nccl_fail(ctxs[0], "ncclAllReduce", r);
     if (r2 != ncclSuccess) return nccl_fail(ctxs[0], "ncclGroupEnd", r2);
     for (int k = 0; k < n_ctx; ++k) {

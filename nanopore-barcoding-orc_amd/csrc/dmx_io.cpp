@@ -91,6 +91,9 @@ double now_s() {
 }
 const bool kIoDebug = getenv("DMX_IO_DEBUG") != nullptr;
 
+// dmx_io_set_memory_budget (0 = none)
+std::atomic<uint64_t> g_mem_budget{0};
+
 int clamp_threads(int t) {
     if (t <= 0) t = (int)std::thread::hardware_concurrency();
     return std::max(1, std::min(t, 64));
@@ -657,6 +660,7 @@ struct ParGzSource : Source {
     int threads = 1;
     size_t chunk = 4u << 20;           // compressed bytes per chunk
     size_t margin = 4u << 20;          // input held past the last chunk's nominal end
+    size_t compact_at = 64u << 20;     // consumed input bytes dropped beyond this much
     std::vector<uint8_t> cbuf;         // compressed input; cn valid bytes, then >= 64 zero bytes
     size_t cn = 0;
     bool raw_eof = false;
@@ -683,17 +687,26 @@ struct ParGzSource : Source {
     std::vector<Chunk> ch;
 
     explicit ParGzSource(std::unique_ptr<Source> r, int nth) : raw(std::move(r)), threads(nth) {
+        // with a memory budget: a round's working set (compressed input ~2x, 16-bit outputs of
+        // ~3.5x the compressed bytes, the round's output) is about 12 x threads x chunk; keep
+        // it near budget / 16
+        if (const uint64_t b = g_mem_budget.load())
+            chunk = std::min<size_t>(chunk, std::max<size_t>(256u << 10,
+                                                             b / (192u * (uint64_t)std::max(1, nth))));
         if (const char* e = getenv("DMX_INFLATE_CHUNK_KB")) {
             const long kb = atol(e);
             if (kb > 0) chunk = (size_t)kb << 10;
         }
-        margin = std::max<size_t>(4u << 20, chunk);
+        margin = std::max<size_t>(g_mem_budget.load() ? std::min<size_t>(4u << 20, 4 * chunk)
+                                                       : (4u << 20), chunk);
+        if (const uint64_t b = g_mem_budget.load())
+            compact_at = std::min<size_t>(compact_at, std::max<size_t>(4u << 20, b / 64));
     }
     size_t chunk_hint() const override { return 1u << 30; }
 
     bool fill(size_t need) {   // cbuf holds >= need bytes from pos / 8 (or all of the input)
         const size_t from = (size_t)(pos >> 3);
-        if (from > (64u << 20) && from * 2 > cn) {   // drop consumed input
+        if (from > compact_at && from * 2 > cn) {   // drop consumed input
             cbuf.erase(cbuf.begin(), cbuf.begin() + (ptrdiff_t)from);
             cn -= from;
             pos -= (uint64_t)from * 8;
@@ -1011,6 +1024,8 @@ struct AheadSource : Source {
     size_t cpos = 0;
 
     explicit AheadSource(std::unique_ptr<Source> s) : in(std::move(s)) {
+        if (const uint64_t b = g_mem_budget.load())   // two blocks in flight: <= budget / 16
+            blk = std::min<size_t>(blk, std::max<size_t>(4u << 20, b / 32));
         if (const char* e = getenv("DMX_INFLATE_AHEAD_KB")) {   // tests: many small blocks
             const long kb = atol(e);
             if (kb > 0) blk = (size_t)kb << 10;
@@ -1141,9 +1156,13 @@ struct BigPool {
         v.clear();
     }
     void give(V& v) {
-        if (v.capacity() * sizeof(typename V::value_type) < kMinBytes) return;
+        const size_t b = v.capacity() * sizeof(typename V::value_type);
+        if (b < kMinBytes) return;
+        const uint64_t budget = g_mem_budget.load();
         std::lock_guard<std::mutex> g(mu);
-        if (keep.size() < kKeep) {
+        size_t held = 0;
+        for (const V& k : keep) held += k.capacity() * sizeof(typename V::value_type);
+        if (keep.size() < kKeep && (!budget || held + b <= budget / 32)) {
             keep.emplace_back();
             keep.back().swap(v);
         }
@@ -1555,6 +1574,8 @@ extern "C" {
 
 int dmx_io_abi_version(void) { return DMX_IO_ABI_VERSION; }
 
+uint64_t dmx_io_set_memory_budget(uint64_t bytes) { return g_mem_budget.exchange(bytes); }
+
 int dmx_reader_open(const char* path, size_t batch_bytes, int threads, dmx_reader** out) {
     if (!path || !out) return -1;
     *out = nullptr;
@@ -1769,7 +1790,7 @@ bool gzip_member(const uint8_t* src, size_t n, int level, Bytes& out) {
         const size_t hdr = 24;
         out.resize(base + hdr + dmxz::huff_bound(n) + 16);
         uint8_t* h = out.data() + base;
-        const uint8_t fixed[12] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, (uint8_t)(level == 1 ? 4 : 0), 3, 12, 0};
+        const uint8_t fixed[12] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, (uint8_t)(level == 1 ? 4 : level >= 9 ? 2 : 0), 3, 12, 0};
         memcpy(h, fixed, 12);
         h[12] = 'D';
         h[13] = 'X';

@@ -212,7 +212,8 @@ def build_parser():
     p.add_argument("-t", dest="threads", type=int, default=8)
     p.add_argument("-m", dest="method", default="edlib")
     p.add_argument("--device", type=int, default=None)
-    p.add_argument("--batch-mb", type=int, default=256)
+    p.add_argument("--batch-mb", type=int, default=0,
+                   help="reader batch size (default: 256, less under a memory budget)")
     p.add_argument("input")
     p.add_argument("output", nargs="?", default="-")
     return p
@@ -249,7 +250,8 @@ def run(argv=None) -> int:
     sink = None
     t0 = time.perf_counter()
     try:
-        with nio.Reader(args.input, args.batch_mb << 20, threads=args.threads) as reader:
+        batch = (args.batch_mb << 20) if args.batch_mb > 0 else nio.batch_bytes_for_budget()
+        with nio.Reader(args.input, batch, threads=args.threads) as reader:
             for batch in reader:
                 try:
                     if sink is None:

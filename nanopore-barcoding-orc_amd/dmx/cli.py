@@ -281,13 +281,14 @@ def _batch_bytes(args) -> int:
     mb = args.batch_mb or int(os.environ.get("DMX_BATCH_MB", "0") or 0)
     if mb > 0:
         return mb << 20
+    cap = nio.batch_bytes_for_budget(256 << 20)   # a memory budget (a SLURM --mem) lowers it
     try:
         size = os.path.getsize(args.input)
     except OSError:
-        return 256 << 20
+        return cap
     if args.input.endswith(".gz"):
         size *= 2                     # FASTQ deflates to about half
-    return int(min(256 << 20, max(32 << 20, size // 4)))
+    return int(min(cap, max(32 << 20, size // 4)))
 
 
 def _devices(args) -> list:

@@ -42,9 +42,10 @@ PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VISIBILITY_ENV = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
                   "GPU_DEVICE_ORDINAL")
 # variables that decide which libdmx / libdmx_io build a process loads (read once at import by
-# dmx/lib.py and dmx/nio.py, so a server cannot switch them per request): a call that sets them
-# (A/B or sanitizer builds) gets a server of its own
-LIBRARY_ENV = ("DMX_LIBDMX", "DMX_LIBDIR", "DMX_DEBUG_BOUNDS")
+# dmx/lib.py and dmx/nio.py, so a server cannot switch them per request), and the memory budget
+# libdmx_io's buffers are sized to at load (nio.memory_budget_bytes): a call that sets them (A/B
+# or sanitizer builds, a budget) gets a server of its own
+LIBRARY_ENV = ("DMX_LIBDMX", "DMX_LIBDIR", "DMX_DEBUG_BOUNDS", "DMX_MEM_BUDGET_MB")
 
 
 def socket_path(env=None) -> str:

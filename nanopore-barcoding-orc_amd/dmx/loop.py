@@ -95,7 +95,9 @@ def build_parser():
     p.add_argument("--compression-level", type=int,
                    default=int(os.environ.get("DMX_COMPRESSION_LEVEL", "5") or 5))
     p.add_argument("-Z", dest="zlevel1", action="store_true")
-    p.add_argument("--batch-mb", type=int, default=int(os.environ.get("DMX_BATCH_MB", "256")))
+    p.add_argument("--batch-mb", type=int, default=int(os.environ.get("DMX_BATCH_MB", "0") or 0),
+                   help="reader batch size (default: 256, less under a memory budget: "
+                        "nio.batch_bytes_for_budget)")
     p.add_argument("--device", type=int, default=None)
     # 01 -> 02 fused: INFILE is the raw reads; reorient them as 01_pychopper.sh does, write its
     # outputs, and demultiplex its PASS records straight from the resident batch
@@ -246,7 +248,8 @@ def run(argv=None) -> int:
     n2_out = np.zeros(len(n1), np.int64)
     totals = np.zeros((len(n1) + 1, len(n2) + 1), dtype=np.int64)   # device bin counts
     try:
-        with nio.Reader(infile, args.batch_mb << 20, threads=args.threads) as reader:
+        batch = (args.batch_mb << 20) if args.batch_mb > 0 else nio.batch_bytes_for_budget()
+        with nio.Reader(infile, batch, threads=args.threads) as reader:
             while True:
                 tw = time.perf_counter()
                 batch = reader.next()

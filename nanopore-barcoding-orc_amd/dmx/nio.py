@@ -23,7 +23,8 @@ IO_EXPORTS = ["dmx_io_abi_version", "dmx_reader_open", "dmx_reader_next", "dmx_r
               "dmx_sink_close", "dmx_sink_error", "dmx_sink_free", "dmx_sink_write_rows",
               "dmx_batch_mean_qual", "dmx_io_gzip", "dmx_sink_retain", "dmx_io_retained_bytes",
               "dmx_io_drop_retained", "dmx_sink_retain_output", "dmx_reader_in_memory",
-              "dmx_io_inflate", "dmx_sink_write_rows2", "dmx_batch_pack_views"]
+              "dmx_io_inflate", "dmx_sink_write_rows2", "dmx_batch_pack_views",
+              "dmx_io_set_memory_budget"]
 
 
 class _CBatch(ctypes.Structure):
@@ -78,8 +79,11 @@ def load() -> ctypes.CDLL:
     L.dmx_sink_write_rows2.argtypes = [P, ctypes.POINTER(_CBatch), c_size] + [P] * 9
     L.dmx_batch_pack_views.argtypes = [ctypes.POINTER(_CBatch), c_size, P, P, P, P, c_int,
                                        P, P, P, P, c_size]
+    L.dmx_io_set_memory_budget.argtypes = [ctypes.c_uint64]
+    L.dmx_io_set_memory_budget.restype = ctypes.c_uint64
     if L.dmx_io_abi_version() != 1:
         raise DmxError("libdmx_io ABI mismatch")
+    L.dmx_io_set_memory_budget(int(memory_budget_bytes() or 0))
     _io = L
     return L
 
@@ -242,6 +246,39 @@ def _read_int(path: str):
         return None
 
 
+def memory_budget_bytes():
+    """The job's memory limit, which the readers' and writers' buffers are sized to
+    (dmx_io_set_memory_budget, batch_bytes_for_budget): DMX_MEM_BUDGET_MB when set, else the
+    cgroup's limit (v2 memory.max, v1 limit_in_bytes; a SLURM job's --mem: 02_cutadapt_loop.sh
+    runs under --mem=4G, 01_pychopper.sh under 2G), else None (no limit)."""
+    env = os.environ.get("DMX_MEM_BUDGET_MB", "").strip()
+    if env:
+        mb = int(env)
+        return (mb << 20) if mb > 0 else None
+    for lim in ("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory/memory.limit_in_bytes"):
+        v = _read_int(lim)
+        if v is not None and v < (1 << 60):
+            return v
+    return None
+
+
+# fixed part of a process's peak: the HIP runtime holds ~0.9 GB of anonymous memory after its
+# first device operations and pageable copies (tools/microbench/rss_hip.hip), plus the
+# interpreter, numpy and the inflate / pool buffers; and the batch-sized buffers alive at once
+# in the fused --reorient pipeline (reader queue, the batch in flight, the writers' render and
+# compressed copies, the reoriented views): profiles/r5_rss_probe*.json
+_FIXED_BYTES = 1200 << 20
+_BATCHES_ALIVE = 16
+
+
+def batch_bytes_for_budget(default: int = 256 << 20) -> int:
+    """Reader batch size under memory_budget_bytes(): (budget - fixed) / 16, 32 MB .. default."""
+    b = memory_budget_bytes()
+    if not b:
+        return default
+    return int(min(default, max(32 << 20, (b - _FIXED_BYTES) // _BATCHES_ALIVE)))
+
+
 def peak_rss_mb() -> float:
     """This process's peak resident set (VmHWM, MB): what a SLURM job's --mem limit meets.
     0.0 where /proc is not readable."""
@@ -275,7 +312,36 @@ def available_memory_bytes():
         if limit is not None and used is not None and limit < (1 << 60):
             cands.append(max(0, limit - used))
             break
+    env = os.environ.get("DMX_MEM_BUDGET_MB", "").strip()
+    if env and int(env) > 0:   # a stated budget: what this process does not hold yet
+        cands.append(max(0, (int(env) << 20) - _rss_bytes()))
     return min(cands) if cands else None
+
+
+def rss_parts_mb() -> dict:
+    """Current resident set by kind (MB): anonymous memory (what a cgroup limit cannot
+    reclaim), file-backed pages (shared libraries, reclaimable) and shmem."""
+    out = {}
+    try:
+        with open("/proc/self/status") as fh:
+            for line in fh:
+                k = line.split(":")[0]
+                if k in ("RssAnon", "RssFile", "RssShmem"):
+                    out[k] = int(line.split()[1]) / 1024
+    except (OSError, ValueError, IndexError):
+        pass
+    return out
+
+
+def _rss_bytes() -> int:
+    try:
+        with open("/proc/self/status") as fh:
+            for line in fh:
+                if line.startswith("VmRSS:"):
+                    return int(line.split()[1]) * 1024
+    except (OSError, ValueError, IndexError):
+        pass
+    return 0
 
 
 def default_retain_bytes(cap_mb=None) -> int:

@@ -99,7 +99,12 @@ def main():
     ap.add_argument("--calls-input", choices=["single", "members"], default="single",
                     help="round-1 input of the 13 calls: the single-member .gz (what "
                          "02_cutadapt_loop.sh reads, pychopped_<ds>.gz) or our multi-member .gz")
+    ap.add_argument("--mem-budget-mb", type=int, default=0,
+                    help="DMX_MEM_BUDGET_MB for the timed commands (a SLURM job's --mem: 4096 "
+                         "for 02_cutadapt_loop.sh, 2048 for 01_pychopper.sh)")
     a = ap.parse_args()
+    if a.mem_budget_mb:
+        os.environ["DMX_MEM_BUDGET_MB"] = str(a.mem_budget_mb)
     wd = a.workdir or tempfile.mkdtemp(prefix="dmx_e2e_")
     pych = os.path.join(wd, "pychopped")
     os.makedirs(pych, exist_ok=True)
@@ -125,6 +130,7 @@ def main():
     raw_bytes, gz_bytes = os.path.getsize(plain), os.path.getsize(gz)
     env = dict(os.environ)
     res = {"workload": a.workload, "reads": a.reads, "threads": a.threads,
+           "mem_budget_mb": a.mem_budget_mb or None,
            "input_fastq_bytes": raw_bytes, "input_gz_bytes": gz_bytes, "gen_s": round(gen_s, 1)}
 
     if a.pychopper:   # 01_pychopper.sh:45-57, PASS to a file as the script's redirect does

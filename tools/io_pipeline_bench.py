@@ -37,8 +37,9 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 N_OUT = 13
 
 
-def child(mode: str, src: str, outdir: str, threads: int, level: int):
+def child(mode: str, src: str, outdir: str, threads: int, level: int, batch_mb: int = 0):
     from dmx import nio
+    batch = (batch_mb << 20) if batch_mb > 0 else nio.batch_bytes_for_budget()
     t = time.perf_counter()
     waits = 0.0
     sink = None
@@ -47,7 +48,7 @@ def child(mode: str, src: str, outdir: str, threads: int, level: int):
         sink = nio.Sink([os.path.join(outdir, f"o{k}.fastq.gz") for k in range(N_OUT)], False,
                         level, threads=threads)
     n = base = 0
-    with nio.Reader(src, 256 << 20, threads=threads) as r:
+    with nio.Reader(src, batch, threads=threads) as r:
         while True:
             tw = time.perf_counter()
             b = r.next()
@@ -83,13 +84,15 @@ def main():
     ap.add_argument("--workload", default="c2")
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--level", type=int, default=5)
+    ap.add_argument("--batch-mb", type=int, default=0,
+                    help="default: 256, less under DMX_MEM_BUDGET_MB (nio.batch_bytes_for_budget)")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--modes", default="inflate,compress,pipeline")
     ap.add_argument("--keep", action="store_true", help="keep the generated inputs")
     ap.add_argument("--child", nargs=3, metavar=("MODE", "SRC", "OUTDIR"))
     a = ap.parse_args()
     if a.child:
-        child(a.child[0], a.child[1], a.child[2], a.threads, a.level)
+        child(a.child[0], a.child[1], a.child[2], a.threads, a.level, a.batch_mb)
         return
     from dmx import synth
     from e2e_bench import write_fastq
@@ -112,13 +115,15 @@ def main():
             fo.write(c.flush())
         with open(stamp, "w") as fh:
             fh.write(tag)
-    res = {"reads": a.reads, "threads": a.threads, "level": a.level,
+    res = {"reads": a.reads, "threads": a.threads, "level": a.level, "batch_mb": a.batch_mb,
+           "mem_budget_mb": os.environ.get("DMX_MEM_BUDGET_MB", ""),
            "fastq_bytes": os.path.getsize(plain), "gz_single_bytes": os.path.getsize(gz1)}
     env = dict(os.environ)
     for mode in a.modes.split(","):
         src = plain if mode == "compress" else gz1
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--threads",
-                            str(a.threads), "--level", str(a.level), "--child", mode, src,
+                            str(a.threads), "--level", str(a.level), "--batch-mb", str(a.batch_mb),
+                            "--child", mode, src,
                             os.path.join(wd, "out_" + mode)], check=True, env=env,
                            stdout=subprocess.PIPE, text=True)
         res[mode] = json.loads(p.stdout.strip().splitlines()[-1])
