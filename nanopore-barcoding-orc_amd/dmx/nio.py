@@ -267,12 +267,13 @@ def memory_budget_bytes():
 # interpreter, numpy and the inflate / pool buffers; and the batch-sized buffers alive at once
 # in the fused --reorient pipeline (reader queue, the batch in flight, the writers' render and
 # compressed copies, the reoriented views): profiles/r5_rss_probe*.json
-_FIXED_BYTES = 1200 << 20
-_BATCHES_ALIVE = 16
+_FIXED_BYTES = 1300 << 20
+_BATCHES_ALIVE = 20
 
 
 def batch_bytes_for_budget(default: int = 256 << 20) -> int:
-    """Reader batch size under memory_budget_bytes(): (budget - fixed) / 16, 32 MB .. default."""
+    """Reader batch size under memory_budget_bytes(): (budget - 1300 MB) / 20, 32 MB .. default
+    (2G: 37 MB, 4G: 140 MB)."""
     b = memory_budget_bytes()
     if not b:
         return default

@@ -117,7 +117,7 @@ def test_reader_empty_and_errors(tmp_path):
 @pytest.mark.parametrize("fasta_out", [False, True])
 def test_sink_matches_python_render(tmp_path, fasta_out, level):
     """Rendered records, inflated by Python's gzip (zlib) at -Z (1: Huffman-only members) and at
-    cutadapt's default level 5 (libdeflate members), and at 9."""
+    cutadapt's default level 5 and at 9 (record-aware members, csrc/dmx_deflate.h fq_deflate)."""
     recs, text = _records(2500, seed=2)
     (tmp_path / "in.fq").write_text(text)
     rng = np.random.default_rng(5)
@@ -162,8 +162,9 @@ def test_sink_matches_python_render(tmp_path, fasta_out, level):
 
 def test_default_level_is_cutadapts_and_smaller_than_z(tmp_path):
     """cutadapt 4.9's --compression-level default (5) is the drop-in's default; -Z (level 1) is
-    Huffman-only.  At 5 the members are within a few percent of zlib's level 5 on the same
-    1 MiB pieces (libdeflate), and smaller than at -Z."""
+    Huffman-only.  At 5 the members (record-aware encoder) are no more than a few percent
+    larger than zlib's level 5 on the same 1 MiB pieces of these short-header, random-quality
+    records (and 10 % smaller on nanopore-style FASTQ: the test below), and smaller than at -Z."""
     from dmx import cli
     args = cli.build_parser().parse_args(["-g", "ACGT", "-o", "x.fq.gz", "in.fq"])
     assert args.compression_level == 5 and not args.zlevel1
@@ -172,7 +173,7 @@ def test_default_level_is_cutadapts_and_smaller_than_z(tmp_path):
     z5 = sum(len(zlib.compress(p, 5)) for p in pieces)
     d5 = sum(len(nio.gzip_member(p, 5)) for p in pieces)
     d1 = sum(len(nio.gzip_member(p, 1)) for p in pieces)
-    assert abs(d5 - z5) / z5 < 0.05
+    assert d5 < 1.05 * z5
     assert d5 < d1
 
 
@@ -699,3 +700,36 @@ def test_rows2_segment_names_with_rc_suffixes(tmp_path):
         b.free()
     s.close()
     assert open(out).read() == "".join(exp)
+
+
+def test_memory_budget_sizes_the_buffers(monkeypatch):
+    """A job's memory limit (DMX_MEM_BUDGET_MB, else the cgroup's) sizes the reader batches:
+    (budget - 1300 MB) / 20 within 32..256 MB (nio.batch_bytes_for_budget; 02_cutadapt_loop.sh
+    runs under --mem=4G, 01_pychopper.sh under 2G)."""
+    monkeypatch.setenv("DMX_MEM_BUDGET_MB", "2048")
+    assert nio.memory_budget_bytes() == 2048 << 20
+    assert nio.batch_bytes_for_budget() == ((2048 - 1300) << 20) // 20
+    monkeypatch.setenv("DMX_MEM_BUDGET_MB", "4096")
+    assert nio.batch_bytes_for_budget() == ((4096 - 1300) << 20) // 20
+    assert nio.batch_bytes_for_budget(64 << 20) == 64 << 20
+    monkeypatch.setenv("DMX_MEM_BUDGET_MB", "1000")
+    assert nio.batch_bytes_for_budget() == 32 << 20
+    monkeypatch.setenv("DMX_MEM_BUDGET_MB", "100000")
+    assert nio.batch_bytes_for_budget() == 256 << 20
+    avail = nio.available_memory_bytes()
+    assert avail is not None and avail <= 100000 << 20
+
+
+def test_single_member_gzip_under_a_memory_budget(tmp_path):
+    """Under a small budget the speculative inflate cuts 256 KiB chunks and the read-ahead blocks
+    and buffer pools shrink (dmx_io_set_memory_budget); the records are the same."""
+    import zlib
+    L = nio.load()
+    recs, text = _records(6000, seed=21)
+    c = zlib.compressobj(6, zlib.DEFLATED, 31)
+    (tmp_path / "one.fq.gz").write_bytes(c.compress(text.encode()) + c.flush())
+    prev = L.dmx_io_set_memory_budget(64 << 20)
+    try:
+        assert _read_all(tmp_path / "one.fq.gz", batch_bytes=256 << 10, threads=4) == recs
+    finally:
+        L.dmx_io_set_memory_budget(prev)
