@@ -362,9 +362,12 @@ struct ShardMap {
     }
 };
 
-#ifndef DMX_WAVE_CAND_CAP   // rare: cells of earlier 64-column segments (16 from round 5:
-#define DMX_WAVE_CAND_CAP 16   // the window scan's per-lane vector rows need the LDS)
+#ifndef DMX_WSCAN_LANE_ROWS   // window-scan per-lane match-vector rows (A/B, off: see wscan_task)
+#define DMX_WSCAN_LANE_ROWS 0
 #endif
+#ifndef DMX_WAVE_CAND_CAP   // rare: cells of earlier 64-column segments (16 with the window
+#define DMX_WAVE_CAND_CAP (DMX_WSCAN_LANE_ROWS ? 16 : 32)   // scan's per-lane rows, to make room
+#endif   // in LDS; 32 vs 16: 46.51 vs 46.85 ms, profiles/r5_ab_wscan_waves_candcap.txt)
 #ifndef DMX_WAVE_CAND_FLUSH
 #define DMX_WAVE_CAND_FLUSH (DMX_WAVE_CAND_CAP / 2)
 #endif
@@ -2243,9 +2246,6 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
 // 5, profiles/r5_ab_wscan_lane_rows.txt): conflict cycles per LDS instruction 1.94 / 2.01 ->
 // 0.62 / 0.83, window scan time unchanged (3.64 / 2.18 vs 3.62 / 2.16 ms): LDS waits are 0.1 %
 // of its wave cycles, it waits on its global gathers.  Off by default (10 KB more LDS).
-#ifndef DMX_WSCAN_LANE_ROWS
-#define DMX_WSCAN_LANE_ROWS 0
-#endif
 constexpr int kLaneRows = 5;
 
 template <bool BAND, class ClStage, class Sink>
@@ -2288,7 +2288,9 @@ __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, 
 }
 
 // Occupancy floor for the window scan (register budget 512 / waves): at 129 VGPRs the compiler
-// drops to 3 waves per SIMD, measured 7 % slower on the whole step.
+// drops to 3 waves per SIMD, measured 7 % slower on the whole step.  Round 5: 4 waves spill 31
+// VGPRs, 3 waves need 153 and spill none, and are still slower (window scan 3.62 / 2.16 ->
+// 3.85 / 2.38 ms, profiles/r5_ab_wscan_waves_candcap.txt).
 #ifndef DMX_WSCAN_WAVES
 #define DMX_WSCAN_WAVES 4
 #endif
