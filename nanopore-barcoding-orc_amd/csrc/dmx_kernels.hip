@@ -1507,7 +1507,10 @@ constexpr int kSortBins = 64;                // counting-sort bins of 4 columns 
 constexpr int kSortShift = 2;
 static_assert(kSortGroup % kScanBlock == 0, "sort group");
 
-__global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
+#ifndef DMX_VERIFY_WAVES
+#define DMX_VERIFY_WAVES 1   // occupancy floor (1: the compiler's choice, 5 waves at 96 VGPRs)
+#endif
+__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_VERIFY_WAVES))) void verify_kernel(RoundArgs R) {
     __shared__ Window s_w[kStageCap];
     __shared__ uint32_t s_wc, s_wb;
     __shared__ int8_t s_pf[72];
@@ -1531,6 +1534,9 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
     // order of their column range, as the screen and the window scan do.
 #ifndef DMX_VERIFY_SORT
 #define DMX_VERIFY_SORT 1
+#endif
+#ifndef DMX_VERIFY_PREFETCH
+#define DMX_VERIFY_PREFETCH 0
 #endif
     const bool sorted = DMX_VERIFY_SORT && front;
     __shared__ uint32_t s_ord[kSortGroup];
@@ -1570,10 +1576,22 @@ __global__ __launch_bounds__(kScanBlock) void verify_kernel(RoundArgs R) {
         }
         __syncthreads();
       }
+      // DMX_VERIFY_PREFETCH (A/B, off): the next stride's window record is loaded before this
+      // stride's scan.  Measured slower: 108 VGPRs drop verify to 4 waves, and forcing 5 spills
+      // (verify 1.39 / 1.44 -> 1.47 / 1.51 ms, profiles/r5_ab_verify_prefetch.txt)
+      Window wn{};
+      if (DMX_VERIFY_PREFETCH && threadIdx.x < gn)
+          wn = R.win[sm.phys(gb + (sorted ? s_ord[threadIdx.x] : threadIdx.x))];
       for (uint32_t sb = 0; sb < gn; sb += kScanBlock) {   // block-uniform
         const uint32_t li = sb + threadIdx.x;
+        Window wcur{};
+        if (DMX_VERIFY_PREFETCH) {
+            wcur = wn;
+            const uint32_t ln = li + kScanBlock;
+            if (ln < gn) wn = R.win[sm.phys(gb + (sorted ? s_ord[ln] : ln))];
+        }
         if (li < gn) {
-            Window w = R.win[sm.phys(gb + (sorted ? s_ord[li] : li))];
+            Window w = DMX_VERIFY_PREFETCH ? wcur : R.win[sm.phys(gb + (sorted ? s_ord[li] : li))];
             const int len = (int)w.len;
             const bool rows_free = (front && (int)w.j1 <= P->max_mk) || w.bmin == 255;
             // column ranges the prefix block must be evaluated on
