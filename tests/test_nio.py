@@ -733,3 +733,37 @@ def test_single_member_gzip_under_a_memory_budget(tmp_path):
         assert _read_all(tmp_path / "one.fq.gz", batch_bytes=256 << 10, threads=4) == recs
     finally:
         L.dmx_io_set_memory_budget(prev)
+
+
+def test_record_aware_gzip_random_documents():
+    """Seeded random documents for fq_deflate: FASTQ/FASTA-shaped lines mixed with arbitrary
+    ones, CRLF, '@' / '>' / '+' in odd places, long and empty lines, repeated headers at random
+    distances, and cuts at random offsets; every member inflates with zlib to its input."""
+    import zlib
+    rng = np.random.default_rng(2024)
+    alph = [b"ACGT", b"ACGTN", bytes(range(33, 75)), b"@>+\n\r ", bytes(range(256))]
+    heads = [b"@" + bytes(rng.integers(33, 127, int(rng.integers(1, 400)), dtype=np.uint8))
+             for _ in range(6)]
+    for case in range(150):
+        parts = []
+        for _ in range(int(rng.integers(1, 120))):
+            kind = int(rng.integers(0, 6))
+            if kind == 0:
+                parts.append(heads[int(rng.integers(len(heads)))] + b"%d\n" % int(rng.integers(1e6)))
+            elif kind == 1:
+                a = alph[int(rng.integers(0, 2))]
+                parts.append(bytes(rng.choice(list(a), int(rng.integers(0, 3000)))) + b"\n")
+            elif kind == 2:
+                parts.append(b"+\n" if rng.random() < 0.8 else b"+x\r\n")
+            elif kind == 3:
+                parts.append(bytes(rng.choice(list(alph[2]), int(rng.integers(0, 3000)))) + b"\n")
+            elif kind == 4:
+                parts.append(bytes(rng.choice(list(alph[3]), int(rng.integers(0, 20)))))
+            else:
+                parts.append(bytes(rng.integers(0, 256, int(rng.integers(0, 500)), dtype=np.uint8)))
+        doc = b"".join(parts)
+        if len(doc) > 10 and rng.random() < 0.5:
+            a = int(rng.integers(0, len(doc)))
+            doc = doc[a:a + int(rng.integers(1, len(doc) - a + 1))]
+        level = int(rng.integers(2, 10))
+        assert zlib.decompress(nio.gzip_member(doc, level), 31) == doc, (case, level)
