@@ -193,10 +193,57 @@ struct Source {
 struct FdSource : Source {
     int fd = -1;
     bool own = false;
+    int threads = 1;        // regular files: reads of >= 8 MB as parallel preads
+    int kind = 0;           // 0 unknown, 1 regular file (preads at `off`), 2 other (read(2))
+    int64_t off = 0, size = 0;
     ~FdSource() override {
         if (own && fd >= 0) ::close(fd);
     }
     long read(uint8_t* dst, size_t cap) override {
+        if (kind == 0) {
+            struct stat st;
+            kind = 2;
+            if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
+                const off_t at = lseek(fd, 0, SEEK_CUR);
+                if (at >= 0) {
+                    kind = 1;
+                    off = (int64_t)at;
+                    size = (int64_t)st.st_size;
+                }
+            }
+        }
+        if (kind == 1) {   // the kernel's page-cache copy of a large read on the pool
+            if (off >= size) {
+                struct stat st;
+                if (fstat(fd, &st) == 0) size = (int64_t)st.st_size;
+                if (off >= size) return 0;
+            }
+            const size_t k = (size_t)std::min<int64_t>((int64_t)cap, size - off);
+            const int nc = std::max(1, (int)std::min<size_t>((size_t)threads, k >> 22));
+            std::atomic<bool> bad{false};
+            std::atomic<int> eno{0};
+            auto slice = [&](int t) {
+                const size_t a = k * (size_t)t / (size_t)nc, b = k * (size_t)(t + 1) / (size_t)nc;
+                for (size_t x = a; x < b && !bad;) {
+                    const ssize_t n = ::pread(fd, dst + x, b - x, (off_t)(off + (int64_t)x));
+                    if (n < 0 && errno == EINTR) continue;
+                    if (n <= 0) {   // error, or the file shrank under us
+                        eno = n < 0 ? errno : EIO;
+                        bad = true;
+                        break;
+                    }
+                    x += (size_t)n;
+                }
+            };
+            if (nc > 1) parallel(nc, slice);
+            else slice(0);
+            if (bad) {
+                err = std::string("read: ") + strerror(eno.load());
+                return -1;
+            }
+            off += (int64_t)k;
+            return (long)k;
+        }
         size_t got = 0;
         while (got < cap) {
             const ssize_t n = ::read(fd, dst + got, cap - got);
@@ -672,6 +719,7 @@ struct ParGzSource : Source {
     uint64_t msize = 0;
     Bytes pend;                        // decoded output not yet delivered
     size_t ppos = 0;
+    double ratio = 2.5;                // output / compressed bytes of the last round (FASTQ)
 
     struct Chunk {
         uint64_t nominal = 0, stop = 0, start = 0, end = 0;
@@ -781,17 +829,27 @@ struct ParGzSource : Source {
     // One round; 1 = done (output appended), 0 = retry with more input, -1 = error.
     int round(uint8_t* dst, size_t cap, size_t& wrote) {
         const int nth = std::max(1, threads);
-        if (!fill((size_t)nth * chunk + margin)) return -1;
+        // a round's output goes straight into the caller's buffer when it fits; otherwise it
+        // waits in `pend` and reaches the caller by a serial copy (on the box: ~25 % of a
+        // 16-thread round).  So the chunks are sized for the round to fit `cap` at the last
+        // round's output ratio (down to chunk / 8).
+        size_t chunk_r = chunk;
+        if (nth > 1 && cap < ((size_t)1 << 40)) {
+            const double fit = (double)cap / ((double)nth * ratio * 1.15);
+            chunk_r = std::min(chunk, std::max<size_t>(std::max<size_t>(chunk / 8, 64u << 10),
+                                                       (size_t)fit));
+        }
+        if (!fill((size_t)nth * chunk_r + margin)) return -1;
         const dmxi::In in{cbuf.data(), cn, raw_eof};
         const uint64_t p0 = pos;
         const size_t b0 = (size_t)(p0 >> 3);
         const size_t avail = cn - b0;
-        // chunks of `chunk` bytes; at the end of the input the rest is split evenly (chunks of
-        // at least chunk / 4) so the last round keeps the threads busy too
-        size_t nch = 1, cs = chunk;
+        // chunks of chunk_r bytes; at the end of the input the rest is split evenly (chunks of
+        // at least chunk_r / 4) so the last round keeps the threads busy too
+        size_t nch = 1, cs = chunk_r;
         if (nth > 1) {
             const size_t usable = raw_eof ? avail : (avail > margin ? avail - margin : 0);
-            const size_t minc = std::max<size_t>(chunk / 4, 64u << 10);
+            const size_t minc = std::max<size_t>(chunk_r / 4, 64u << 10);
             nch = std::max<size_t>(1, std::min<size_t>((size_t)nth, (usable + minc - 1) / minc));
             if (raw_eof) cs = std::max<size_t>(minc, (usable + nch - 1) / nch);
             nch = std::max<size_t>(1, std::min(nch, usable / std::max<size_t>(cs, 1) +
@@ -965,6 +1023,8 @@ struct ParGzSource : Source {
                     total / 1e6, t1 - t0, mf, md, t2 - t1, now_s() - t2, redo);
         }
         const Chunk& last = ch[nch - 1];
+        if (last.end > p0 && total > 0)   // output / compressed ratio, for the next round's size
+            ratio = std::max(1.0, (double)total / ((double)(last.end - p0) / 8.0));
         pos = last.end;
         at_member = last.atm_out;
         done = last.st == dmxi::Stop::kEnd;
@@ -992,9 +1052,11 @@ struct ParGzSource : Source {
                 ppos = 0;
             }
         }
-        while (got < cap && !done) {
+        // one round per call (a partly filled buffer is a valid read): a second round into the
+        // rest of the buffer would be cut small or spill into `pend`
+        while (got == 0 && !done) {
             size_t w = 0;
-            const int r = round(dst + got, cap - got, w);
+            const int r = round(dst, cap, w);
             if (r < 0) return -1;
             got += w;
         }
@@ -1023,7 +1085,9 @@ struct AheadSource : Source {
     Blk cur;
     size_t cpos = 0;
 
-    explicit AheadSource(std::unique_ptr<Source> s) : in(std::move(s)) {
+    int threads = 1;   // the copy into the caller's buffer
+
+    explicit AheadSource(std::unique_ptr<Source> s, int nth) : in(std::move(s)), threads(nth) {
         if (const uint64_t b = g_mem_budget.load())   // two blocks in flight: <= budget / 16
             blk = std::min<size_t>(blk, std::max<size_t>(4u << 20, b / 32));
         if (const char* e = getenv("DMX_INFLATE_AHEAD_KB")) {   // tests: many small blocks
@@ -1095,7 +1159,18 @@ struct AheadSource : Source {
                 cv.notify_all();
             }
             const size_t k = std::min(cap - got, cur.n - cpos);
-            memcpy(dst + got, cur.p.get() + cpos, k);
+            // a round's ~60 MB: the copy into the batch runs on the pool (a serial copy was
+            // ~7 ms of every 30 ms inflate round on the box)
+            const int nc = (int)std::min<size_t>((size_t)threads, k >> 22);
+            uint8_t* d = dst + got;
+            const uint8_t* sp = cur.p.get() + cpos;
+            if (nc > 1)
+                parallel(nc, [&](int t) {
+                    const size_t a = k * (size_t)t / (size_t)nc, b = k * (size_t)(t + 1) / (size_t)nc;
+                    memcpy(d + a, sp + a, b - a);
+                });
+            else
+                memcpy(d, sp, k);
             cpos += k;
             got += k;
         }
@@ -1107,7 +1182,8 @@ struct AheadSource : Source {
 // inflate on the reader's thread).
 std::unique_ptr<Source> read_ahead(std::unique_ptr<Source> p, int threads) {
     const char* a = getenv("DMX_INFLATE_AHEAD");
-    if (threads > 1 && !(a && a[0] == '0')) return std::make_unique<AheadSource>(std::move(p));
+    if (threads > 1 && !(a && a[0] == '0'))
+        return std::make_unique<AheadSource>(std::move(p), threads);
     return p;
 }
 
@@ -1596,6 +1672,7 @@ int dmx_reader_open(const char* path, size_t batch_bytes, int threads, dmx_reade
         }
     }
     auto fd = std::make_unique<FdSource>();
+    fd->threads = clamp_threads(threads);
     if (!strcmp(path, "-")) {
         fd->fd = 0;
     } else {
