@@ -565,7 +565,9 @@ inline void lz_freq(const uint8_t* src, size_t a, size_t b, const LzMatch* m, si
 //  - mixed: blocks of ~256 KiB, one table each (short reads, FASTA without headers, text that
 //    is not FASTQ).
 inline size_t fq_deflate(const uint8_t* src, size_t n, uint8_t* out) {
-    if (n == 0) return huff_deflate(src, 0, out);
+    // positions are 32-bit (the writers' members are <= 1 MiB); a larger single member from
+    // dmx_io_gzip gets the Huffman-only stream
+    if (n == 0 || n >= ((size_t)1 << 31)) return huff_deflate(src, n, out);
     thread_local std::vector<LzMatch> ms;
     thread_local std::vector<std::pair<uint32_t, uint32_t>> sq;
     fq_scan(src, n, ms, sq);
