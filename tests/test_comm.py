@@ -95,3 +95,37 @@ def test_allreduce_without_communicator_is_refused(c2x24):
         ctx.exec()
         with pytest.raises(lib.DmxError, match=r"\(-5\)"):
             ctx.allreduce_counts()
+
+
+def test_comm_in_a_torch_process_uses_its_rccl():
+    """bench.py's multi-GPU path imports torch (which maps its own librccl.so, soname
+    librccl.so.1) before libdmx opens RCCL at its first communicator (csrc/dmx_comm.cpp): the
+    dlopen must resolve to that already-mapped copy, and a single-rank communicator must sum
+    the counts.  Run in a child process so this process's RCCL state does not matter."""
+    import os
+    import subprocess
+    import sys
+    code = r"""
+import os, sys, json
+sys.path.insert(0, os.path.join(%r, "nanopore-barcoding-orc_amd"))
+import torch
+from dmx import lib, synth
+d = synth.generate("c2", n=5000, seed=4)
+with lib.Context(0) as ctx:
+    ctx.set_panel(0, d["sp5"], lib.DMX_FRONT | lib.DMX_RC)
+    ctx.set_panel(1, d["sp27"], lib.DMX_BACK | lib.DMX_RC)
+    ctx.set_mode(lib.MODE_TWO_ROUND)
+    ctx.comm_init_rank(lib.comm_unique_id(), 1, 0)
+    ctx.load(lib.pack(d["blob"], d["offsets"], d["lengths"]))
+    ctx.exec()
+    local = ctx.counts().tolist()
+    reduced = ctx.allreduce_counts().tolist()
+maps = [l.split()[-1] for l in open("/proc/self/maps") if "librccl" in l]
+print(json.dumps({"same": local == reduced, "n": sum(local), "rccl": sorted(set(maps))}))
+""" % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = __import__("json").loads(out.stdout.strip().splitlines()[-1])
+    assert r["same"] and r["n"] > 0
+    assert len(r["rccl"]) == 1, r["rccl"]   # one RCCL mapped: torch's
