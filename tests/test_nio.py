@@ -752,13 +752,16 @@ def test_record_aware_gzip_random_documents():
                 parts.append(heads[int(rng.integers(len(heads)))] + b"%d\n" % int(rng.integers(1e6)))
             elif kind == 1:
                 a = alph[int(rng.integers(0, 2))]
-                parts.append(bytes(rng.choice(list(a), int(rng.integers(0, 3000)))) + b"\n")
+                parts.append(rng.choice(list(a), int(rng.integers(0, 3000))).astype(np.uint8)
+                             .tobytes() + b"\n")
             elif kind == 2:
                 parts.append(b"+\n" if rng.random() < 0.8 else b"+x\r\n")
             elif kind == 3:
-                parts.append(bytes(rng.choice(list(alph[2]), int(rng.integers(0, 3000)))) + b"\n")
+                parts.append(rng.choice(list(alph[2]), int(rng.integers(0, 3000)))
+                             .astype(np.uint8).tobytes() + b"\n")
             elif kind == 4:
-                parts.append(bytes(rng.choice(list(alph[3]), int(rng.integers(0, 20)))))
+                parts.append(rng.choice(list(alph[3]), int(rng.integers(0, 20)))
+                             .astype(np.uint8).tobytes())
             else:
                 parts.append(bytes(rng.integers(0, 256, int(rng.integers(0, 500)), dtype=np.uint8)))
         doc = b"".join(parts)
@@ -767,3 +770,30 @@ def test_record_aware_gzip_random_documents():
             doc = doc[a:a + int(rng.integers(1, len(doc) - a + 1))]
         level = int(rng.integers(2, 10))
         assert zlib.decompress(nio.gzip_member(doc, level), 31) == doc, (case, level)
+
+
+def test_large_reads_take_the_parallel_paths(tmp_path):
+    """Reads of >= 8 MB from a regular file go out as parallel preads, read-ahead blocks of
+    >= 8 MB are copied to the batch by several threads, and single-member inflate rounds are
+    sized to the read-ahead block (csrc/dmx_io.cpp FdSource, AheadSource, ParGzSource): a
+    ~40 MB FASTQ, plain and as one zlib member, read with 4 threads and 16 MB batches gives
+    the records in order."""
+    import zlib
+    rng = np.random.default_rng(31)
+    recs = []
+    parts = []
+    i = 0
+    while sum(map(len, parts)) < (40 << 20):
+        n = int(rng.integers(200, 4000))
+        s = rng.choice(list(b"ACGT"), n).astype(np.uint8).tobytes().decode()
+        q = bytes((rng.integers(0, 41, n) + 33).astype(np.uint8)).decode()
+        h = f"r{i} ch={i % 512}"
+        recs.append((h, s, q))
+        parts.append(f"@{h}\n{s}\n+\n{q}\n".encode())
+        i += 1
+    text = b"".join(parts)
+    (tmp_path / "big.fastq").write_bytes(text)
+    c = zlib.compressobj(1, zlib.DEFLATED, 31)
+    (tmp_path / "big.fastq.gz").write_bytes(c.compress(text) + c.flush())
+    for name in ("big.fastq", "big.fastq.gz"):
+        assert _read_all(tmp_path / name, batch_bytes=16 << 20, threads=4) == recs, name
