@@ -288,3 +288,38 @@ def test_loop_two_name_template(tmp_path):
     assert total > 0.5 * len(seqs)
     # same file set otherwise: no default-named round-2 file in the templated runs
     assert not glob.glob(f"{runs['n1n2']}/SP27/SP27_*_SP5_*")
+
+
+def test_large_single_member_input_parallel_io_equals_sequential(tmp_path):
+    """A ~60 MB single-member .gz round-1 input (02_cutadapt_loop.sh:64-72) through the parallel
+    I/O paths (speculative inflate with rounds sized to the read-ahead block, parallel preads
+    and block copies, record-aware level-5 members on 8 threads) gives the same records and
+    report counts as the sequential paths (DMX_SEQ_INFLATE=1, -j 1, 4 MB batches)."""
+    import zlib
+    d = synth.generate("c2", n=25000, seed=21)
+    seqs = synth.to_strings(d)
+    rng = np.random.default_rng(5)
+    names = [f"r{i} runid=abc ch={i % 512}" for i in range(len(seqs))]
+    quals = random_quals(rng, [len(s) for s in seqs])
+    text = "".join(f"@{n}\n{s}\n+\n{q}\n" for n, s, q in zip(names, seqs, quals)).encode()
+    infile = str(tmp_path / "pychopped_big.fastq.gz")
+    c = zlib.compressobj(1, zlib.DEFLATED, 31)
+    with open(infile, "wb") as fh:
+        fh.write(c.compress(text) + c.flush())
+    outs = {}
+    for tag, extra, env_add in (("par", ["-j", "8"], {}),
+                                ("seq", ["-j", "1"], {"DMX_SEQ_INFLATE": "1",
+                                                      "DMX_BATCH_MB": "4"})):
+        od = tmp_path / tag
+        od.mkdir()
+        env = dict(os.environ, DMX_DAEMON="0", **env_add)
+        subprocess.run([CLI, "--action=trim", "-e", "0.1", "--rc", *extra,
+                        "-g", f"file:{panel.SP5_FASTA}", "-o", f"{od}/{{name}}_big.fastq.gz",
+                        infile, f"--json={od}/report.json"], check=True, env=env,
+                       stdout=subprocess.DEVNULL)
+        files = sorted(os.path.basename(f) for f in glob.glob(f"{od}/*_big.fastq.gz"))
+        outs[tag] = ({f: read_fastq(f"{od}/{f}") for f in files},
+                     json.load(open(f"{od}/report.json"))["read_counts"])
+    assert outs["par"][0] == outs["seq"][0]
+    assert outs["par"][1] == outs["seq"][1]
+    assert sum(len(v) for v in outs["par"][0].values()) == len(seqs)
