@@ -323,3 +323,41 @@ def test_large_single_member_input_parallel_io_equals_sequential(tmp_path):
     assert outs["par"][0] == outs["seq"][0]
     assert outs["par"][1] == outs["seq"][1]
     assert sum(len(v) for v in outs["par"][0].values()) == len(seqs)
+
+
+def test_fused_reorient_under_a_memory_budget_equals_unbudgeted(tmp_path):
+    """dmx-demux-loop --reorient (01 -> 02 fused) under DMX_MEM_BUDGET_MB=1400 (32 MB batches,
+    256 KiB inflate chunks, small read-ahead blocks and buffer pools; nio.batch_bytes_for_budget,
+    dmx_io_set_memory_budget) writes the same pychopper and demultiplexed records as without a
+    budget, from an ordinary single-member .gz of raw (unoriented) reads."""
+    import zlib
+    d = synth.generate("c2", n=20000, seed=23)
+    seqs = synth.to_strings(d)
+    rng = np.random.default_rng(23)
+    flip = rng.random(len(seqs)) < 0.5     # raw reads: either orientation
+    comp = str.maketrans("ACGTN", "TGCAN")
+    seqs = [s.translate(comp)[::-1] if f else s for s, f in zip(seqs, flip)]
+    names = [f"r{i} runid=abc ch={i % 512}" for i in range(len(seqs))]
+    quals = random_quals(rng, [len(s) for s in seqs])
+    text = "".join(f"@{n}\n{s}\n+\n{q}\n" for n, s, q in zip(names, seqs, quals)).encode()
+    raw = tmp_path / "raw.fastq.gz"
+    c = zlib.compressobj(1, zlib.DEFLATED, 31)
+    raw.write_bytes(c.compress(text) + c.flush())
+    runs = {}
+    for tag, env_add in (("free", {}), ("budget", {"DMX_MEM_BUDGET_MB": "1400"})):
+        od = tmp_path / tag
+        env = dict(os.environ, **env_add)
+        env.pop("DMX_BATCH_MB", None)
+        subprocess.run([LOOP, str(raw), "--reorient", "--pychopper-dir", str(od / "pych"),
+                        "-j", "8", "--outdir", str(od / "demux")], check=True, env=env,
+                       stdout=subprocess.DEVNULL)
+        runs[tag] = od
+    got = {}
+    for tag, od in runs.items():
+        files = sorted(p.relative_to(od) for p in od.rglob("*") if p.is_file()
+                       and (p.name.endswith(".fastq") or p.name.endswith(".fastq.gz")))
+        got[tag] = {str(f): read_fastq(str(od / f)) for f in files}
+    assert got["free"].keys() == got["budget"].keys() and len(got["free"]) > 10
+    for f in got["free"]:
+        assert got["free"][f] == got["budget"][f], f
+    assert sum(len(v) for k, v in got["free"].items() if "demux" in k) > 0.5 * len(seqs)
