@@ -157,41 +157,42 @@ def run(argv=None, keep_contexts: bool = False) -> int:
         _unsupported("--rc with linked adapters is not implemented")
 
     _phase("args", marks)
-    devices = _devices(args)
-    if keep_contexts:   # the server's contexts (panels and mode are set again below)
-        ctxs = cached_group(devices)
-    else:
-        ctxs = lib.open_group(devices)
-    _phase("open", marks)
-    for ctx in ctxs:
-        _configure(ctx, ads, linked, args)
-    _phase("panel", marks)
-    level = 1 if args.zlevel1 else args.compression_level
-
-    demux = "{name}" in args.output
-    fasta_out = fastx.is_fasta_path(args.output.replace("{name}", "x"))
-    names = [a.name for a in ads]
-    if demux:   # cutadapt creates every demultiplexed output, also when it stays empty
-        paths = [args.output.replace("{name}", nm) for nm in names]
-        if not args.discard_untrimmed:
-            paths.append(args.output.replace("{name}", "unknown"))
-        unmatched_to = -1 if args.discard_untrimmed else len(names)
-    else:
-        paths = [args.output] + ([args.untrimmed_output] if args.untrimmed_output else [])
-        unmatched_to = 1 if args.untrimmed_output else (-1 if args.discard_untrimmed else 0)
-
-    stats = Stats(ads)
-    stats.rc_mode = bool(args.rc)
-    stats.min_overlap = args.overlap
-    t0 = time.perf_counter()
-    a1 = len(ads) if linked else 0
-    totals = np.zeros((len(ads) + 1, a1 + 1), dtype=np.int64)
+    # the reader's producer thread starts on the first batch while the device contexts open
     reader = nio.Reader(args.input, _batch_bytes(args), threads=args.cores)
-    # the resident server keeps gzip outputs' text for the script's next calls, which read the
-    # round-1 bins back (02_cutadapt_loop.sh:91-103); retain_plan says which outputs
-    untrimmed = len(names) if demux and not args.discard_untrimmed else None
-    retain, keep = retain_plan(paths, untrimmed, reader.in_memory, keep_contexts)
     try:
+        devices = _devices(args)
+        if keep_contexts:   # the server's contexts (panels and mode are set again below)
+            ctxs = cached_group(devices)
+        else:
+            ctxs = lib.open_group(devices)
+        _phase("open", marks)
+        for ctx in ctxs:
+            _configure(ctx, ads, linked, args)
+        _phase("panel", marks)
+        level = 1 if args.zlevel1 else args.compression_level
+
+        demux = "{name}" in args.output
+        fasta_out = fastx.is_fasta_path(args.output.replace("{name}", "x"))
+        names = [a.name for a in ads]
+        if demux:   # cutadapt creates every demultiplexed output, also when it stays empty
+            paths = [args.output.replace("{name}", nm) for nm in names]
+            if not args.discard_untrimmed:
+                paths.append(args.output.replace("{name}", "unknown"))
+            unmatched_to = -1 if args.discard_untrimmed else len(names)
+        else:
+            paths = [args.output] + ([args.untrimmed_output] if args.untrimmed_output else [])
+            unmatched_to = 1 if args.untrimmed_output else (-1 if args.discard_untrimmed else 0)
+
+        stats = Stats(ads)
+        stats.rc_mode = bool(args.rc)
+        stats.min_overlap = args.overlap
+        t0 = time.perf_counter()
+        a1 = len(ads) if linked else 0
+        totals = np.zeros((len(ads) + 1, a1 + 1), dtype=np.int64)
+        # the resident server keeps gzip outputs' text for the script's next calls, which read the
+        # round-1 bins back (02_cutadapt_loop.sh:91-103); retain_plan says which outputs
+        untrimmed = len(names) if demux and not args.discard_untrimmed else None
+        retain, keep = retain_plan(paths, untrimmed, reader.in_memory, keep_contexts)
         sink = nio.Sink(paths, fasta_out, level, threads=args.cores, retain_bytes=retain)
     except BaseException:
         reader.close()

@@ -37,7 +37,7 @@ import time
 import numpy as np
 
 from . import __version__, lib, nio, panel
-from .cli import _devices
+from .cli import _EXEC_TO_IMPORT, _T_IMPORT, _devices
 from . import report
 from .report import Stats
 
@@ -199,12 +199,6 @@ def run(argv=None) -> int:
     ads1, ads2 = aset1.adapters, aset2.adapters
     n1, n2 = [a.name for a in ads1], [a.name for a in ads2]
 
-    ctxs = lib.open_group(_devices(args))
-    for ctx in ctxs:
-        ctx.set_panel(0, [a.seq for a in ads1], lib.DMX_FRONT | lib.DMX_RC, args.e_rate, 3)
-        ctx.set_panel(1, [a.seq for a in ads2], lib.DMX_BACK | lib.DMX_RC, args.e_rate, 3)
-        ctx.set_mode(lib.MODE_TWO_ROUND)
-
     # outputs: round 1 = one file per SP5 adapter (+ unknown); round 2 = per (SP5, SP27) pair
     keep2 = [j for j, nm in enumerate(n2) if args.no_cleanup or nm not in INVALID_SP27]
     p1 = [f"{outdir}/SP5/{nm}_{ds}.fastq.gz" for nm in n1]
@@ -225,6 +219,21 @@ def run(argv=None) -> int:
     for d in sorted({os.path.dirname(x) for x in p2}):
         os.makedirs(d, exist_ok=True)
 
+    marks = [("setup", time.perf_counter() - _T_IMPORT)]   # DMX_PROFILE_IO phase marks
+    # the reader's producer thread starts on the first batch while the device contexts open
+    batch = (args.batch_mb << 20) if args.batch_mb > 0 else nio.batch_bytes_for_budget()
+    reader = nio.Reader(infile, batch, threads=args.threads)
+    try:
+        ctxs = lib.open_group(_devices(args))
+    except BaseException:
+        reader.close()
+        raise
+    marks.append(("open", time.perf_counter() - _T_IMPORT))
+    for ctx in ctxs:
+        ctx.set_panel(0, [a.seq for a in ads1], lib.DMX_FRONT | lib.DMX_RC, args.e_rate, 3)
+        ctx.set_panel(1, [a.seq for a in ads2], lib.DMX_BACK | lib.DMX_RC, args.e_rate, 3)
+        ctx.set_mode(lib.MODE_TWO_ROUND)
+
     st1 = Stats(ads1)
     st1.rc_mode = True
     st2 = []
@@ -236,6 +245,7 @@ def run(argv=None) -> int:
     if args.reorient:
         reo = Reorienter(args, pych_dir, base)
     t0 = time.perf_counter()
+    marks.append(("outputs", t0 - _T_IMPORT))
     print("Round 1: Demultiplexing with SP5 adapters...")
     print("Round 2: Demultiplexing with SP27 adapters (fused with round 1)...")
     level = 1 if args.zlevel1 else args.compression_level
@@ -248,81 +258,79 @@ def run(argv=None) -> int:
     n2_out = np.zeros(len(n1), np.int64)
     totals = np.zeros((len(n1) + 1, len(n2) + 1), dtype=np.int64)   # device bin counts
     try:
-        batch = (args.batch_mb << 20) if args.batch_mb > 0 else nio.batch_bytes_for_budget()
-        with nio.Reader(infile, batch, threads=args.threads) as reader:
-            while True:
+        while True:
+            tw = time.perf_counter()
+            batch = reader.next()
+            prof["read_wait"] += time.perf_counter() - tw
+            if batch is None:
+                break
+            try:
+                if not len(batch):
+                    continue
                 tw = time.perf_counter()
-                batch = reader.next()
-                prof["read_wait"] += time.perf_counter() - tw
-                if batch is None:
-                    break
-                try:
-                    if not len(batch):
+                views = None
+                packed, lens = batch.packed, batch.lens
+                if reo is not None:   # the PASS records of 01_pychopper.sh, as views
+                    views = reo.batch(batch)
+                    tp = time.perf_counter()
+                    prof["reo"] += tp - tw
+                    packed = batch.pack_views(views[0], views[1], views[2], views[3],
+                                              threads=args.threads)
+                    prof["pack"] += time.perf_counter() - tp
+                    lens = packed.lengths
+                    if not len(lens):
                         continue
-                    tw = time.perf_counter()
-                    views = None
-                    packed, lens = batch.packed, batch.lens
-                    if reo is not None:   # the PASS records of 01_pychopper.sh, as views
-                        views = reo.batch(batch)
-                        tp = time.perf_counter()
-                        prof["reo"] += tp - tw
-                        packed = batch.pack_views(views[0], views[1], views[2], views[3],
-                                                  threads=args.threads)
-                        prof["pack"] += time.perf_counter() - tp
-                        lens = packed.lengths
-                        if not len(lens):
-                            continue
-                    res, cnt = lib.run_batch(ctxs, packed)
-                    totals += lib.bin_totals(cnt, len(n1), len(n2))
-                    prof["gpu"] += time.perf_counter() - tw
-                    tw = time.perf_counter()
-                    (s1, e1, o1), (s2, e2, o2, nrc2) = plan_rounds(res, lens)
-                    b1 = res["bin1"].astype(np.int64)
-                    b2 = res["bin2"].astype(np.int64)
-                    m1 = b1 >= 0
-                    idx1 = np.where(m1, b1, len(n1) if args.no_cleanup else -1)
-                    # unmatched in round 1 is written untrimmed to unknown (--no-cleanup only)
-                    s1w = np.where(m1, s1, 0)
-                    o1w = o1.astype(np.uint8)   # an unmatched read may still be taken RC'd
-                    if views is None:
-                        sink1.write(batch, idx1, s1w, e1, o1w, o1w)
-                    else:
-                        x, y, t = view_coords(views[1], views[2], views[3], s1w, e1, o1w)
-                        sink1.write_rows2(batch, views[0], idx1, x, y, t, views[1], views[2],
-                                          views[3], o1w)
-                    idx2 = np.where(m1, out2[np.maximum(b1, 0), b2 + 1], -1)
-                    # round-2 unknown: the round-1 output record, untrimmed by round 2
-                    m2 = b2 >= 0
-                    # unmatched in round 2 but taken reverse-complemented: RC of the round-1
-                    # record T1 = orient(read, rc1)[s1:n], i.e. orient(read, !rc1)[0 : n - s1]
-                    u2rc = ~m2 & (res["rc2"] == 1)
-                    s2w = np.where(m2, s2, np.where(u2rc, 0, s1))
-                    e2w = np.where(m2, e2, np.where(u2rc, e1 - s1, e1))
-                    o2w = np.where(m2, o2, np.where(u2rc, 1 - o1, o1)).astype(np.uint8)
-                    n2w = np.where(m2, nrc2, o1 + u2rc).astype(np.uint8)
-                    if views is None:
-                        sink2.write(batch, idx2, s2w, e2w, o2w, n2w)
-                    else:
-                        x, y, t = view_coords(views[1], views[2], views[3], s2w, e2w, o2w)
-                        sink2.write_rows2(batch, views[0], idx2, x, y, t, views[1], views[2],
-                                          views[3], n2w)
-                    _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w,
-                                 bp2_out, n2_out, packed)
-                    prof["plan_write"] += time.perf_counter() - tw
-                finally:
-                    batch.free()
+                res, cnt = lib.run_batch(ctxs, packed)
+                totals += lib.bin_totals(cnt, len(n1), len(n2))
+                prof["gpu"] += time.perf_counter() - tw
+                tw = time.perf_counter()
+                (s1, e1, o1), (s2, e2, o2, nrc2) = plan_rounds(res, lens)
+                b1 = res["bin1"].astype(np.int64)
+                b2 = res["bin2"].astype(np.int64)
+                m1 = b1 >= 0
+                idx1 = np.where(m1, b1, len(n1) if args.no_cleanup else -1)
+                # unmatched in round 1 is written untrimmed to unknown (--no-cleanup only)
+                s1w = np.where(m1, s1, 0)
+                o1w = o1.astype(np.uint8)   # an unmatched read may still be taken RC'd
+                if views is None:
+                    sink1.write(batch, idx1, s1w, e1, o1w, o1w)
+                else:
+                    x, y, t = view_coords(views[1], views[2], views[3], s1w, e1, o1w)
+                    sink1.write_rows2(batch, views[0], idx1, x, y, t, views[1], views[2],
+                                      views[3], o1w)
+                idx2 = np.where(m1, out2[np.maximum(b1, 0), b2 + 1], -1)
+                # round-2 unknown: the round-1 output record, untrimmed by round 2
+                m2 = b2 >= 0
+                # unmatched in round 2 but taken reverse-complemented: RC of the round-1
+                # record T1 = orient(read, rc1)[s1:n], i.e. orient(read, !rc1)[0 : n - s1]
+                u2rc = ~m2 & (res["rc2"] == 1)
+                s2w = np.where(m2, s2, np.where(u2rc, 0, s1))
+                e2w = np.where(m2, e2, np.where(u2rc, e1 - s1, e1))
+                o2w = np.where(m2, o2, np.where(u2rc, 1 - o1, o1)).astype(np.uint8)
+                n2w = np.where(m2, nrc2, o1 + u2rc).astype(np.uint8)
+                if views is None:
+                    sink2.write(batch, idx2, s2w, e2w, o2w, n2w)
+                else:
+                    x, y, t = view_coords(views[1], views[2], views[3], s2w, e2w, o2w)
+                    sink2.write_rows2(batch, views[0], idx2, x, y, t, views[1], views[2],
+                                      views[3], n2w)
+                _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w,
+                             bp2_out, n2_out, packed)
+                prof["plan_write"] += time.perf_counter() - tw
+            finally:
+                batch.free()
     finally:
         tw = time.perf_counter()
+        marks.append(("loop", tw - _T_IMPORT))
+        reader.close()
         sink1.close()
         sink2.close()
         if reo is not None:
             reo.close()
         prof["drain"] += time.perf_counter() - tw
+        marks.append(("drain", time.perf_counter() - _T_IMPORT))
     if reo is not None:
         prof.update({"reo_" + k: v for k, v in reo.prof.items()})
-    if os.environ.get("DMX_PROFILE_IO"):
-        print("io profile (s): " + ", ".join(f"{k} {v:.3f}" for k, v in prof.items()) +
-              f"; peak_rss_mb {nio.peak_rss_mb():.0f}", file=sys.stderr)
     # the devices' (SP5, SP27) bin counts (RCCL-summed over GPUs) vs the per-read results
     st1.check_totals(totals[1:, :].sum(axis=1))
     for i, s in enumerate(st2):
@@ -338,8 +346,15 @@ def run(argv=None) -> int:
         st2[i].write_json(f"{outdir}/SP27/{ident}_{ds}.json",
                           argv=["dmx-demux-loop"] + argv, cores=args.threads,
                           in_path=f"{outdir}/SP5/{ident}_{ds}.fastq.gz", error_rate=args.e_rate)
+    marks.append(("reports", time.perf_counter() - _T_IMPORT))
     for ctx in ctxs:
         ctx.close()
+    marks.append(("close", time.perf_counter() - _T_IMPORT))
+    if os.environ.get("DMX_PROFILE_IO"):   # phases: seconds since the module import
+        print("io profile (s): " + ", ".join(f"{k} {v:.3f}" for k, v in prof.items()) +
+              f"; peak_rss_mb {nio.peak_rss_mb():.0f}; phases " +
+              " ".join(f"{k}={v:.3f}" for k, v in marks) +
+              f" exec_to_import={_EXEC_TO_IMPORT:.2f}", file=sys.stderr)
     print("Demultiplexing complete!")
     print(f"Finished in {time.perf_counter() - t0:.3f} s on {len(ctxs)} GPU(s): "
           f"{st1.n_in:,} reads, {st1.n_with_adapter:,} with an SP5 adapter")
@@ -451,24 +466,38 @@ def _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w, bp2_out, n2_
                                   np.where(two, p, np.where(p >= 0, s1[hit_all] + p, -1)))
         adj = np.full(n, 4, np.int64)
         adj[hit_all] = codes
+    # one stable sort groups the reads of every SP5 bin (ascending read index inside a bin, as
+    # a boolean mask of the bin would select them); per-bin sums are differences of cumsums
+    sel = np.nonzero(m1)[0]
+    grp = sel[np.argsort(b1[sel], kind="stable")]
+    edge = np.searchsorted(b1[grp], np.arange(len(st2) + 1))
+
+    def per_bin(v):
+        cs = np.concatenate(([0], np.cumsum(np.asarray(v, np.int64)[grp])))
+        return cs[edge[1:]] - cs[edge[:-1]]
+
+    bp_in = per_bin(len1)
+    n_rc = per_bin(rc2)
+    bp_out = per_bin(np.where(m2, e2w - s2w, len1))
+    r2 = res["m2_rstart"].astype(np.int64)
+    err2 = res["m2_errors"].astype(np.int64)
     for i, s in enumerate(st2):
-        sel = m1 & (b1 == i)
-        if not sel.any():
+        g = grp[edge[i]:edge[i + 1]]
+        if not len(g):
             continue
-        s.n_in += int(sel.sum())
-        s.bp_in += int(len1[sel].sum())
-        hit = sel & m2
-        s.n_with_adapter += int(hit.sum())
-        s.n_rc += int(rc2[sel].sum())
+        s.n_in += len(g)
+        s.bp_in += int(bp_in[i])
+        hit = g[m2[g]]
+        s.n_with_adapter += len(hit)
+        s.n_rc += int(n_rc[i])
         s.add_counts(b2[hit], rc2[hit], len(s.adapters))
-        s.add_matches(b2[hit], "back", len1[hit] - res["m2_rstart"].astype(np.int64)[hit],
-                      res["m2_errors"].astype(np.int64)[hit])
+        s.add_matches(b2[hit], "back", len1[hit] - r2[hit], err2[hit])
         if adj is not None:
             s.add_adjacent(b2[hit], adj[hit])
         # reads the per-call cutadapt would write (all of them: unknown included), before the
         # script's cleanup deletes files
-        n2_out[i] += int(sel.sum())
-        bp2_out[i] += int(np.where(m2, e2w - s2w, len1)[sel].sum())
+        n2_out[i] += len(g)
+        bp2_out[i] += int(bp_out[i])
 
 
 def main():
