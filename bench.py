@@ -623,7 +623,8 @@ def main():
 
     stage = {k: 0.0 for k in ("scan0", "resolve0", "finalize0", "scan1", "resolve1",
                               "finalize1", "total", "filter0", "verify0", "filter1", "verify1",
-                              "screen0", "wscan0", "screen1", "wscan1")}
+                              "screen0", "wscan0", "screen1", "wscan1", "pieces0",
+                              "pieces1")}
     clusters = np.zeros(2)
     windows = np.zeros(2)
     windows_raw = np.zeros(2)

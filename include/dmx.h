@@ -184,14 +184,16 @@ int dmx_counts(dmx_ctx* ctx, uint64_t* out_counts, size_t n_out);
  * context's stream (order: scan0, resolve0, finalize0, scan1, resolve1, finalize1, total, then
  * the parts of scan0/scan1 spent in the shared-suffix filter and the prefix verification:
  * filter0, verify0, filter1, verify1, then the index screen and the window scan:
- * screen0, wscan0, screen1, wscan1 — pass n_stage = 15 to receive them all), and
- * counts[n_counts <= 12] = {candidate clusters r0, r1, filter windows kept for the window scan
+ * screen0, wscan0, screen1, wscan1, then the piece screen's part of filter0 / filter1:
+ * pieces0, pieces1 — pass n_stage = 17 to receive them all), and
+ * counts[n_counts <= 14] = {candidate clusters r0, r1, filter windows kept for the window scan
  * r0, r1, candidate cells (band mode) or clusters resolved after pruning (ring mode) r0, r1,
  * band DPs / tracebacks r0, r1, filter windows before prefix verification r0, r1, (window
- * piece, adapter) tasks passed by the index screen r0, r1}, and flags
- * (bit0 cluster overflow, bit1 exactness-check violation, bit2 filter-window overflow, bit3
- * candidate-cell overflow, bit4 filter step bucket out of range (a build-knob invariant, see
- * kStepsPerBucket), bit5 a bounds violation (DMX_DEBUG_BOUNDS builds); must be 0). */
+ * piece, adapter) tasks passed by the index screen r0, r1, filter tasks of the piece screen
+ * r0, r1}, and flags
+ * (bit0 cluster overflow, bit1 exactness-check violation, bit2 filter-window / task overflow,
+ * bit3 candidate-cell overflow, bit4 a filter invariant (step bucket or piece-screen cell range)
+ * violated, bit5 a bounds violation (DMX_DEBUG_BOUNDS builds); must be 0). */
 int dmx_stats(dmx_ctx* ctx, float* stage_ms, int n_stage, uint64_t* counts, int n_counts,
               int* flags);
 

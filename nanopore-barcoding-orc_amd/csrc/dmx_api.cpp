@@ -12,8 +12,11 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <thread>
+#include <tuple>
+#include <utility>
 #include <vector>
 
 #include "dmx_internal.h"
@@ -134,8 +137,10 @@ int ensure_pipeline(Ctx* c) {
         if ((rc = dev_alloc(c, &c->d_win, want_win))) return rc;
         if ((rc = dev_alloc(c, &c->d_win2, want_win))) return rc;
         if ((rc = dev_alloc(c, &c->d_tasks, 4 * want_win))) return rc;
+        if ((rc = dev_alloc(c, &c->d_ftask, want_win))) return rc;
         c->win_cap = want_win;
         c->task_cap = 4 * want_win;
+        c->ftask_cap = want_win;
     }
     const size_t nc = counts_size(c);
     if (c->n_counts != nc) {
@@ -158,9 +163,9 @@ hipError_t read_counters(Ctx* c, uint32_t* cnt, int* ovf) {
     if (e != hipSuccess) return e;
     int o = 0;
     for (int x = 0; x < kShLists; ++x) {
-        const bool cand = x >= kShCand;
-        const uint32_t scap = (uint32_t)((cand ? c->cand_cap : x >= kShTasks ? c->task_cap
-                                                                            : c->win_cap) /
+        const bool cand = x >= kShCand && x < kShFtask;
+        const uint32_t scap = (uint32_t)((cand ? c->cand_cap : x >= kShFtask ? c->ftask_cap
+                                          : x >= kShTasks ? c->task_cap : c->win_cap) /
                                          kShards);
         uint64_t t = 0;
         for (int s = 0; s < kShards; ++s) {
@@ -169,7 +174,8 @@ hipError_t read_counters(Ctx* c, uint32_t* cnt, int* ovf) {
             if (v > scap) o |= cand ? 8 : 4;
         }
         const int slot = x < kShWin2 ? 4 + x : x < kShTasks ? 10 + (x - kShWin2)
-                       : x < kShCand ? 12 + (x - kShTasks) : 6 + (x - kShCand);
+                       : x < kShCand ? 12 + (x - kShTasks) : x < kShFtask ? 6 + (x - kShCand)
+                       : 14 + (x - kShFtask);
         cnt[slot] = (uint32_t)t;
     }
     if (ovf) *ovf = o;
@@ -194,8 +200,10 @@ int grow_windows(Ctx* c) {
     if ((rc = dev_alloc(c, &c->d_win, want))) return rc;
     if ((rc = dev_alloc(c, &c->d_win2, want))) return rc;
     if ((rc = dev_alloc(c, &c->d_tasks, 4 * want))) return rc;
+    if ((rc = dev_alloc(c, &c->d_ftask, want))) return rc;
     c->win_cap = want;
     c->task_cap = 4 * want;
+    c->ftask_cap = want;
     return DMX_OK;
 }
 
@@ -279,6 +287,8 @@ int dmx_open(int device, dmx_ctx** out) {
     c->no_filter = nf && nf[0] == '1';
     const char* nv = std::getenv("DMX_NO_VERIFY");
     c->no_verify = nv && nv[0] == '1';
+    const char* np = std::getenv("DMX_NO_PIECES");   // A/B: the full filter pass
+    c->no_pieces = np && np[0] == '1';
     const char* rs = std::getenv("DMX_RESOLVE");
     c->force_ring = rs && std::strcmp(rs, "ring") == 0;
     const char* ns = std::getenv("DMX_NO_SCREEN");   // A/B: no index screen before the
@@ -291,7 +301,10 @@ int dmx_open(int device, dmx_ctx** out) {
         return DMX_E_HIP;
     }
     for (auto& e : c->ev) hipEventCreate(&e);
-    for (int r = 0; r < 2; ++r) hipMalloc((void**)&c->d_panel[r], sizeof(DevPanel));
+    for (int r = 0; r < 2; ++r) {
+        hipMalloc((void**)&c->d_panel[r], sizeof(DevPanel));
+        hipMalloc((void**)&c->d_pieces[r], sizeof(DevPieces));
+    }
     hipMalloc((void**)&c->d_counters, 32 * sizeof(uint32_t));
     hipMalloc((void**)&c->d_shard, kShLists * kShards * kShardStride * sizeof(uint32_t));
     *out = c;
@@ -307,7 +320,9 @@ void dmx_close(dmx_ctx* c) {
     void* bufs[] = {c->d_seq_alloc, c->d_nmask_alloc,     c->d_offs,     c->d_lens,      c->d_res,
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
                     c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_tasks, c->d_counters, c->d_shard,
-                    c->d_counts,    c->d_panel[0],  c->d_panel[1]};
+                    c->d_counts,    c->d_panel[0],  c->d_panel[1], c->d_pieces[0], c->d_pieces[1],
+                    c->d_ftask, c->d_flat_bad, c->d_sbf, c->d_read_item, c->d_cells[0],
+                    c->d_cells[1]};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (int r = 0; r < 2; ++r)
@@ -355,6 +370,145 @@ int dmx_set_panel_mixed(dmx_ctx* c, int round, const char* const* seqs, const in
         if (wheres[a] != DMX_FRONT && wheres[a] != DMX_BACK) return DMX_E_INVALID;
     return set_panel_impl(c, round, seqs, lens, wheres, n, max_errors, min_overlap,
                           DMX_FRONT | (rc ? DMX_RC : 0));
+}
+
+// Piece screen tables (dmx_device.h DevPieces).  Adapter a of an ACGT panel
+// with K_a = acc[m_a] >= 0 (the largest accepted cost of an alignment covering all m_a rows) is
+// cut into K_a + 1 disjoint row pieces of near-equal length (at most 16 nt each: a piece may be
+// any sub-range of its rows).  An accepted full alignment has <= K_a edits, so some piece is
+// aligned without one: an exact copy in the read, after which the alignment ends within
+// (m_a - r1) +- K_a columns (r1 = the piece's end row).  Pieces are deduplicated per
+// (codes, length, orientation) with the union of their end ranges; every piece contributes its
+// 8-mers at offsets 0 .. s-1 (s = the sampling stride), so a copy starting anywhere has one of
+// them at a sampled position.  Off (piece_step 0) for IUPAC panels, pieces shorter than 8 nt,
+// tables that do not fit, or DMX_NO_PIECES=1.
+static void build_pieces(const Ctx* c, const char* const* seqs, const int* lens, int n,
+                         HostPanel& hp) {
+    hp.piece_step = 0;
+    DevPieces& Q = hp.pieces;
+    memset(&Q, 0, sizeof(Q));
+    if (!hp.filter || c->no_pieces) return;
+    struct Pc {
+        uint32_t val;
+        int len, o, dlo, dhi;
+    };
+    std::vector<Pc> pcs;
+    auto code = [](char ch) -> int {
+        switch (ch) {
+            case 'A': return 0;
+            case 'C': return 1;
+            case 'G': return 2;
+            case 'T': return 3;
+            default: return -1;
+        }
+    };
+    int minlen = 64;
+    for (int a = 0; a < n; ++a) {
+        const int m = lens[a];
+        for (int i = 0; i < m; ++i)
+            if (code(seqs[a][i]) < 0) return;   // IUPAC adapter: the full filter pass
+        const int K = hp.ad[a].acc[m];
+        if (K < 0) continue;                    // never accepted with every row aligned
+        const int np = K + 1;
+        if (m / np < kPieceK) return;
+        for (int p = 0; p < np; ++p) {
+            const int r0 = p * m / np, r1 = (p + 1) * m / np;
+            const int len = std::min(16, r1 - r0), re = r0 + len;
+            minlen = std::min(minlen, len);
+            for (int o = 0; o < hp.n_orient; ++o) {
+                uint32_t v = 0;
+                for (int i = 0; i < len; ++i) {
+                    // orientation 1: the reverse complement, as it appears in the view-0 codes
+                    const int cd = o == 0 ? code(seqs[a][r0 + i]) : 3 - code(seqs[a][re - 1 - i]);
+                    v |= (uint32_t)cd << (2 * i);
+                }
+                pcs.push_back({v, len, o, (m - re) - K, (m - re) + K});
+            }
+        }
+    }
+    // dedup by (codes, length, orientation), union of the end ranges
+    std::sort(pcs.begin(), pcs.end(), [](const Pc& x, const Pc& y) {
+        return std::make_tuple(x.val, x.len, x.o) < std::make_tuple(y.val, y.len, y.o);
+    });
+    std::vector<Pc> uq;
+    for (const Pc& p : pcs) {
+        if (!uq.empty() && uq.back().val == p.val && uq.back().len == p.len && uq.back().o == p.o) {
+            uq.back().dlo = std::min(uq.back().dlo, p.dlo);
+            uq.back().dhi = std::max(uq.back().dhi, p.dhi);
+        } else {
+            uq.push_back(p);
+        }
+    }
+    if (uq.empty() || (int)uq.size() > kMaxPieceEntries) return;
+    int step = minlen - kPieceK + 1 >= 4 ? 4 : (minlen - kPieceK + 1 >= 2 ? 2 : 1);
+    if (const char* e = std::getenv("DMX_PIECE_STEP"))   // A/B: a denser sampling
+        step = std::min(step, std::max(1, std::atoi(e)));
+    while (step > 1 && (int)uq.size() * step > kMaxPieceEntries) step /= 2;
+    if ((int)uq.size() * step > kMaxPieceEntries) return;
+    // Sampled offsets: any `step` consecutive offsets j0 .. j0+step-1 of a piece cover every copy
+    // (one of its 8-mers sits at a sampled position).  Per piece take the window whose 8-mers the
+    // fewest other pieces share (pieces of different adapters that overlap a shared constant
+    // block share 8-mers, and every entry of a key is checked on each sampled hit of it).
+    std::map<uint32_t, int> mult;
+    for (const Pc& x : uq)
+        for (int off = 0; off + kPieceK <= x.len; ++off) ++mult[(x.val >> (2 * off)) & 0xFFFFu];
+    std::vector<std::pair<uint32_t, uint64_t>> ents;   // (8-mer, entry)
+    int lo_off = 1 << 20, dlo_min = 0, len_max = 0, dhi_max = 0;
+    bool any1 = false;
+    for (const Pc& x : uq) {
+        int best = 0, bcost = 1 << 30;
+        for (int j0 = 0; j0 + step - 1 + kPieceK <= x.len; ++j0) {
+            int cost = 0;
+            for (int off = j0; off < j0 + step; ++off) cost += mult[(x.val >> (2 * off)) & 0xFFFFu];
+            if (cost < bcost) bcost = cost, best = j0;
+        }
+        for (int off = best; off < best + step; ++off)
+            ents.push_back({(x.val >> (2 * off)) & 0xFFFFu,
+                            piece_entry(x.val, x.len, x.o, off, x.dlo, x.dhi)});
+        if (x.o == 0) {
+            lo_off = std::min(lo_off, x.len + x.dlo - 1);
+        } else {
+            dlo_min = any1 ? std::min(dlo_min, x.dlo) : x.dlo;
+            any1 = true;
+        }
+        len_max = std::max(len_max, x.len);
+        dhi_max = std::max(dhi_max, x.dhi);
+    }
+    std::sort(ents.begin(), ents.end());
+    int nk = 0;
+    for (size_t e = 0; e < ents.size(); ++e) {
+        if (e == 0 || ents[e].first != ents[e - 1].first) {
+            Q.key[nk++] = (uint32_t)e;
+            Q.bitmap[ents[e].first >> 5] |= 1u << (ents[e].first & 31);
+        }
+        Q.key[nk - 1] += 1u << 16;
+        Q.entry[e] = ents[e].second;
+    }
+    for (int w = 0, r = 0; w < kPieceBitmapWords; ++w) {
+        Q.rank_base[w] = (uint16_t)r;
+        r += __builtin_popcount(Q.bitmap[w]);
+    }
+    int reach = 0;   // FRONT: alignments entering at column 0 (rows skipped) end before it
+    if (hp.ad[0].where == kFront)
+        for (int a = 0; a < n; ++a)
+            for (int L = 1; L <= (int)hp.ad[a].m; ++L)
+                if (hp.ad[a].acc[L] >= 0) reach = std::max(reach, L + (int)hp.ad[a].acc[L]);
+    // every cell a part can mark lies within 64 cells of its mask base (pscreen_kernel)
+    int pmax = (992 - std::max(len_max + dhi_max, dhi_max - dlo_min)) / 16 * 16;
+    pmax = std::min(pmax, 768);
+    if (const char* e = std::getenv("DMX_PIECE_PART"))   // A/B: positions per screen lane
+        pmax = std::min(pmax, std::max(64, std::atoi(e) / 16 * 16));
+    if (pmax < 64) return;
+    Q.on = 1;
+    Q.step = step;
+    Q.n_pieces = (int)uq.size();
+    Q.n_keys = nk;
+    Q.n_entries = (int)ents.size();
+    Q.front_reach = reach;
+    Q.part_max = pmax;
+    Q.lo_off = std::max(0, lo_off == (1 << 20) ? 0 : lo_off);
+    Q.dlo_min = dlo_min;
+    hp.piece_step = step;
 }
 
 // The host and device forms of a panel (parser.py / adapters.py rules above), the filter /
@@ -554,6 +708,7 @@ static int build_panel(Ctx* c, const char* const* seqs, const int* lens, const i
     // loaders accept (>= kMinOffset nt, >= kMinTail nt before the end): the deepest warm-up
     // before a view (index screen, edge bands), clamped at -kViewReachPre, and the block loads
     // past it.  Adapters of <= 64 nt always fit; the check keeps it explicit.
+    build_pieces(c, seqs, lens, n, hp);
     hp.reach = panel_reach(hp, dp);
     if (hp.reach.need_pre > kGuardNt || hp.reach.need_post > kGuardNt) {
         c->err = "panel: the kernels' reach around a view (" + std::to_string(hp.reach.pre) +
@@ -584,6 +739,8 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
     c->band_wide[round] = kkmax > 5;   // list 1 (costs 4..kk): 11 diagonals cover kk <= 5
     CK(hipSetDevice(c->device));
     CK(hipMemcpy(c->d_panel[round], &dp, sizeof(dp), hipMemcpyHostToDevice));
+    if (hp.piece_step)
+        CK(hipMemcpy(c->d_pieces[round], &hp.pieces, sizeof(DevPieces), hipMemcpyHostToDevice));
     return DMX_OK;
 }
 
@@ -691,6 +848,7 @@ int load_impl(dmx_ctx* c, const uint32_t* seq2b, const MaskSrc& mask, const uint
     }
     c->n_reads = n_reads;
     c->n_words = n_words;
+    c->flat_dirty = true;
     CK(hipMemcpyAsync(c->d_seq, seq2b, n_words * 4, hipMemcpyHostToDevice, c->stream));
     if ((rc = upload_mask(c, mask, 0, nmw, c->stream))) return rc;
     if (n_reads) {
@@ -771,6 +929,7 @@ int dmx_exec(dmx_ctx* c) {
     const size_t slots0 = c->mode == DMX_MODE_LINKED ? c->n_reads * (size_t)c->panel[0].n
                                                      : c->n_reads * (c->orient_slot[0] ? 2 : 1);
     CK(hipMemsetAsync(c->d_winner[0], 0xFF, slots0 * sizeof(unsigned long long), st));
+    if ((rc = prepare_flat(c, st))) return rc;
     if ((rc = launch_round(c, 0, st))) return rc;
     if ((rc = launch_finalize(c, 0, st))) return rc;
     if (c->mode != DMX_MODE_SINGLE) {
@@ -833,7 +992,7 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
     CK(hipSetDevice(c->device));
     CK(hipStreamSynchronize(c->stream));
     const int rounds = c->mode == DMX_MODE_SINGLE ? 1 : 2;
-    float t[15] = {};
+    float t[17] = {};
     for (int r = 0; r < rounds; ++r) {
         hipEventElapsedTime(&t[3 * r + 0], c->ev[3 * r + 0], c->ev[3 * r + 1]);
         hipEventElapsedTime(&t[3 * r + 1], c->ev[3 * r + 1], c->ev[3 * r + 2]);
@@ -844,22 +1003,24 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
             hipEventElapsedTime(&t[8 + 2 * r], c->ev[9 + 2 * r], c->ev[10 + 2 * r]);
             hipEventElapsedTime(&t[11 + 2 * r], c->ev[10 + 2 * r], c->ev[13 + r]);
             hipEventElapsedTime(&t[12 + 2 * r], c->ev[13 + r], c->ev[3 * r + 1]);
+            if (c->panel[r].piece_step)   // the piece screen's share of the filter stage
+                hipEventElapsedTime(&t[15 + r], c->ev[3 * r + 0], c->ev[15 + r]);
         }
     }
     hipEventElapsedTime(&t[6], c->ev[8], c->ev[6 + rounds - 1]);
-    for (int i = 0; i < n_stage && i < 15; ++i) stage_ms[i] = t[i];
+    for (int i = 0; i < n_stage && i < 17; ++i) stage_ms[i] = t[i];
     uint32_t cnt[32];
     int list_ovf = 0;
     CK(read_counters(c, cnt, &list_ovf));
     if (getenv("DMX_DEBUG_STATS"))
         fprintf(stderr,
-                "dmx stats: windows raw %u %u verified %u %u screened tasks %u %u "
-                "(by 3' cells only %u %u) cand %u %u %u %u\n",
-                cnt[4], cnt[5], cnt[10], cnt[11], cnt[12], cnt[13], cnt[19], cnt[23], cnt[6],
-                cnt[7], cnt[8], cnt[9]);
+                "dmx stats: filter tasks %u %u windows raw %u %u verified %u %u screened tasks "
+                "%u %u (by 3' cells only %u %u) cand %u %u %u %u\n",
+                cnt[14], cnt[15], cnt[4], cnt[5], cnt[10], cnt[11], cnt[12], cnt[13], cnt[19],
+                cnt[23], cnt[6], cnt[7], cnt[8], cnt[9]);
     if (counts) {
         const bool b0 = c->band_ok[0] && !c->force_ring, b1 = c->band_ok[1] && !c->force_ring;
-        const uint64_t v[12] = {cnt[0],
+        const uint64_t v[14] = {cnt[0],
                                 cnt[1],
                                 c->panel[0].verify ? cnt[10] : cnt[4],
                                 c->panel[1].verify ? cnt[11] : cnt[5],
@@ -870,8 +1031,10 @@ int dmx_stats(dmx_ctx* c, float* stage_ms, int n_stage, uint64_t* counts, int n_
                                 cnt[4],
                                 cnt[5],
                                 cnt[12],
-                                cnt[13]};
-        for (int i = 0; i < n_counts && i < 12; ++i) counts[i] = v[i];
+                                cnt[13],
+                                cnt[14],
+                                cnt[15]};
+        for (int i = 0; i < n_counts && i < 14; ++i) counts[i] = v[i];
     }
     if (flags) {
         int f = (int)cnt[3];
@@ -945,6 +1108,7 @@ void swap_inputs(Ctx* c) {
     std::swap(c->d_exc, c->alt.exc);
     std::swap(c->exc_cap, c->alt.exc_cap);
     std::swap(c->n_words, c->alt.n_words);
+    c->flat_dirty = true;
     c->d_seq = c->d_seq_alloc + kGuardWords;
     c->d_nmask = c->d_nmask_alloc + kGuardWords;
 }
@@ -1125,7 +1289,7 @@ int run_chunked(dmx_ctx* c, const uint32_t* seq2b, const MaskSrc& nmask,
             if ((rc = dmx_stats(c, ms, 7, cl, 8, &flags))) return rc;
             if (flags & 18) {
                 c->err = (flags & 2) ? "internal: traceback left the exact window (please report)"
-                                     : "internal: filter step bucket out of range (please report)";
+                                     : "internal: filter task invariant violated (please report)";
                 return DMX_E_STATE;
             }
             if (!(flags & 13)) break;
@@ -1209,7 +1373,7 @@ int run_impl(dmx_ctx* c, const uint32_t* seq2b, const MaskSrc& mask, const uint6
         if ((rc = dmx_stats(c, ms, 7, cl, 8, &flags))) return rc;
         if (flags & 18) {
             c->err = (flags & 2) ? "internal: traceback left the exact window (please report)"
-                                 : "internal: filter step bucket out of range (please report)";
+                                 : "internal: filter task invariant violated (please report)";
             return DMX_E_STATE;
         }
         if (!(flags & 13)) return dmx_fetch(c, out);

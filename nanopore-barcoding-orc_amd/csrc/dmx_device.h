@@ -117,7 +117,71 @@ constexpr int kStageCap = 256;    // LDS staging of emitted records per block
 #endif
 constexpr int kShards = DMX_SHARDS;
 constexpr int kShardStride = 32;   // u32 words between counters: one 128-B line each
-enum ShardList { kShWin = 0, kShWin2 = 2, kShTasks = 4, kShCand = 6, kShLists = 10 };
+enum ShardList { kShWin = 0, kShWin2 = 2, kShTasks = 4, kShCand = 6, kShFtask = 10, kShLists = 12 };
+
+// ---------------------------------------------------------------------------------------------
+// Piece screen.  Every adapter a of an ACGT panel is cut into K_a + 1 disjoint
+// row pieces, K_a = acc[m_a] (the largest cost of an accepted alignment covering all m_a rows).
+// An alignment of all rows with <= K_a edits leaves at least one piece without an edit, i.e. an
+// exact copy of that piece in the read, and it ends at column e + (m_a - r1) +- K_a where e is the
+// position after the copy and r1 the piece's end row.  The screen finds exact copies of the
+// pieces (and of their reverse complements, for the other orientation) and sends the shared-suffix
+// filter only to the 16-position cells where such an alignment can end, plus the FRONT
+// partial-alignment cells at the view start; a 3' view's last-column window is emitted directly.
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxPieces = 1024;         // distinct (piece, orientation) records
+constexpr int kMaxPieceEntries = 2048;   // (sampled 8-mer, piece, offset) entries
+constexpr int kPieceK = 8;               // sampled k-mer length (a 64 Ki-bit LDS bitmap)
+constexpr int kPieceBitmapWords = 1 << (2 * kPieceK - 5);
+
+// An entry of the piece table (one per (piece, sampled offset)), packed in 64 bits: the piece's
+// 2-bit codes in view-0 read order (nt i at bits 2i; orientation 1: the reverse complement),
+// its length, orientation, the sampled 8-mer's offset inside it, and the range of alignment end
+// columns after the copy (dlo, dhi; + 128).
+__host__ __device__ inline uint64_t piece_entry(uint32_t val, int len, int o, int off, int dlo,
+                                                int dhi) {
+    return (uint64_t)val | ((uint64_t)len << 32) | ((uint64_t)o << 37) | ((uint64_t)off << 38) |
+           ((uint64_t)(dlo + 128) << 40) | ((uint64_t)(dhi + 128) << 48);
+}
+
+struct DevPieces {
+    int32_t on;            // 1: the piece screen replaces the full filter pass
+    int32_t step;          // sampling stride s: an 8-mer every s positions (pieces >= 8 + s - 1)
+    int32_t n_pieces, n_keys, n_entries;
+    int32_t front_reach;   // FRONT: positions [0, front_reach) hold partial (column-0) alignments
+    int32_t part_max;      // view positions per screen lane (multiple of 16)
+    int32_t lo_off;        // min over orientation-0 pieces of len + dlo - 1 (>= 0)
+    int32_t dlo_min;       // min over orientation-1 pieces of dlo
+    int32_t pad[3];
+    // the LDS image (pscreen_kernel copies it whole): bitmap, rank base, keys, entries
+    uint32_t bitmap[kPieceBitmapWords];       // bit K: some entry samples the 8-mer K
+    uint16_t rank_base[kPieceBitmapWords];    // set bits before each word: 8-mer -> key index
+    uint32_t key[kMaxPieceEntries];           // key r (increasing 8-mer): first entry | count << 16
+    uint64_t entry[kMaxPieceEntries];         // piece_entry(), grouped by key
+};
+constexpr int kPieceLdsFixed = kPieceBitmapWords * 6;   // bitmap + rank base, bytes
+
+// One filter task of the piece screen: view positions [p0, p0 + span) of (item, o); columns
+// p0 + hoff + 1 .. are reported (the positions before are the restricted-start warm-up); fresh:
+// p0 = 0 with the panel's own column 0 (careful per-column thresholds, like segment 0).  The
+// oriented view travels with the task (the filter needs no dependent loads).
+struct FTask {
+    uint32_t item;
+    uint32_t p0;
+    uint16_t span;
+    uint8_t hoff;
+    uint8_t flags;   // bit 0: orientation, bit 1: fresh, bit 2: the view's strand
+    uint32_t n, start, len;   // the read's length; the oriented view
+    uint64_t off;             // the read's first nt
+};
+static_assert(sizeof(FTask) == 32, "FTask layout");
+
+// Flat piece scan: a sorted, non-overlapping batch is scanned as one stream of
+// 4096-nt superblocks.  sbf[b] = the first read whose end lies past nt 4096 b; cell bitmaps: one
+// bit per 16 nt of the packed batch and per view orientation (cells never hold two reads of a
+// dmx_pack layout; when they do, a mark only adds filter work).
+constexpr int kSuperNt = 4096;   // nt per wave step: 64 lanes x 64 nt
+constexpr int kCellGuardWords = 4;   // zero words before / after each cell bitmap
 constexpr int kCandStageCap = 128; // per candidate list
 
 // Block-level staging of appended records: lanes append to LDS (LDS atomics), the block then
@@ -244,7 +308,7 @@ enum BoundsBuf : uint32_t {
 enum BoundsKernel : int32_t {
     kKerFilter = 1, kKerVerify, kKerScreen, kKerScreen4, kKerWscan, kKerScan, kKerBand0,
     kKerBand1, kKerSelectCand, kKerResolve, kKerSelect, kKerFin0, kKerFin1, kKerFin0L, kKerFin1L,
-    kKerFin2L, kKerChop, kKerChopBig, kKerChopStart, kKerSelfTest
+    kKerFin2L, kKerChop, kKerChopBig, kKerChopStart, kKerSelfTest, kKerPieces
 };
 constexpr int kBoundsRec = 24;     // d_counters[24..27]: kernel id + 1, buffer, index lo / hi
 

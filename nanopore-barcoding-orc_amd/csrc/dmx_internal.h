@@ -34,6 +34,8 @@ struct HostPanel {
     bool nonpos = false;      // an accepted match may score <= 0 (needs per-orientation winners)
     PanelReach reach;
     DevAdapter ad[kMaxAdapters];
+    int piece_step = 0;       // piece screen sampling stride (0 = off: the full filter pass)
+    DevPieces pieces;         // its tables
 };
 
 struct Ctx {
@@ -43,8 +45,10 @@ struct Ctx {
     int mode = DMX_MODE_SINGLE;
     bool no_filter = false;   // DMX_NO_FILTER=1: always full scans (A/B testing)
     bool no_verify = false;   // DMX_NO_VERIFY=1: skip the shared-prefix window verification
+    bool no_pieces = false;   // DMX_NO_PIECES=1: the full filter pass instead of the piece screen
     HostPanel panel[2];
     DevPanel* d_panel[2] = {nullptr, nullptr};
+    DevPieces* d_pieces[2] = {nullptr, nullptr};
 
     // resident batch
     size_t n_reads = 0, n_words = 0;
@@ -107,11 +111,24 @@ struct Ctx {
     unsigned long long* d_linked = nullptr;
     Window* d_tasks = nullptr;           // index screen survivors (window piece of one adapter)
     size_t task_cap = 0;
+    FTask* d_ftask = nullptr;            // piece screen -> filter tasks
+    size_t ftask_cap = 0;
+    // flat piece scan (prepare_flat): sortedness flag, superblock index, read -> item, cells
+    uint32_t* d_flat_bad = nullptr;
+    uint32_t* d_sbf = nullptr;
+    size_t sbf_cap = 0, n_sb = 0;
+    bool flat_dirty = true;              // a new batch (or input set) since the index was built
+    bool flat_ok_launch = false;         // this exec launches the flat scan
+    uint32_t* d_read_item = nullptr;
+    size_t read_item_cap = 0;
+    uint32_t* d_cells[2] = {nullptr, nullptr};
+    size_t cells_cap = 0, cells_words = 0;
     bool no_screen = false;              // DMX_NO_SCREEN=1: every window runs every adapter
     bool screen_v1 = false;              // DMX_SCREEN_V1=1: one lane per (window, adapter) screen
     size_t n_counts = 0;
-    hipEvent_t ev[15] = {};   // [3r..3r+2] round r stages, [6+r] finalize, [8] start,
-                              // [9+2r] after filter, [10+2r] after verify, [13+r] after screen
+    hipEvent_t ev[17] = {};   // [3r..3r+2] round r stages, [6+r] finalize, [8] start,
+                              // [9+2r] after filter, [10+2r] after verify, [13+r] after screen,
+                              // [15+r] after the piece screen (its filter tasks follow)
     bool executed = false;
     ChopState* chop = nullptr;   // dmx_chop_* state, created by dmx_chop_set
 
@@ -127,6 +144,7 @@ void comm_release(Ctx* c);
 int reset_counts(Ctx* c);      // size d_counts for the current panels/mode and zero it (sync)
 void chop_invalidate(Ctx* c);   // a new dmx_load makes the last dmx_chop_exec's results stale
 int launch_round(Ctx* c, int round, hipStream_t st);
+int prepare_flat(Ctx* c, hipStream_t st);   // the flat piece scan's index (dmx_kernels.hip)
 int launch_finalize(Ctx* c, int round, hipStream_t st);
 // offs[i] -= g0 for a chunk's offsets uploaded as the caller gave them (stream st)
 int launch_rebase_offsets(uint64_t* offs, uint32_t n, uint64_t g0, hipStream_t st);

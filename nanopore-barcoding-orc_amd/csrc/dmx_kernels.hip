@@ -6,6 +6,8 @@
 // oracle/cutadapt_oracle.c; design and exactness argument in DESIGN.md §3.
 //
 // Per round: scan -> resolve -> select -> finalize, all on one HIP stream, no host round trip.
+#include <type_traits>
+
 #include "dmx_device.h"
 #include "dmx_internal.h"
 
@@ -51,6 +53,18 @@ struct RoundArgs {
     uint32_t* task_count;        // [kShards]: shard s at tasks + s * task_scap
     uint32_t task_cap;
     uint32_t task_scap;
+    const DevPieces* pieces;     // piece screen tables
+    FTask* ftask;                // piece screen -> filter tasks
+    uint32_t* ftask_count;       // [kShards]: shard s at ftask + s * ftask_scap
+    uint32_t ftask_scap;
+    // flat piece scan (sorted, non-overlapping batches; *flat_bad != 0: the per-part screen)
+    const uint32_t* flat_bad;
+    const uint32_t* sbf;         // [nsb + 1] first read ending past each superblock's start
+    uint32_t nsb;
+    uint32_t n_words;
+    const uint32_t* read_item;   // round 2: read -> item (~0 = none)
+    uint32_t* cells[2];          // per orientation, kCellGuardWords words before index 0
+    uint32_t n_reads;
 };
 
 // DESIGN.md §3.10.  The filter, the prefix verification and the index screen are necessary
@@ -1484,6 +1498,714 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             }
             if (S.have)
                 st.push(make_window(item, o, tv, S.w1, S.w2, 0, S.wb,
+                                    window_clean(S, S.w1, S.w2, rb)));
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (st.count() > kWaveWinCap / 2) st.flush();
+    }
+    __builtin_amdgcn_wave_barrier();
+    st.flush();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Piece screen: one lane per (item, part) of the item's orientation-0 view.  The
+// lane samples an 8-mer every S positions of the part's codes (view order) and looks it up in an
+// LDS bitmap of the panel's sampled piece 8-mers (both orientations: a piece of orientation 1 is
+// stored reverse complemented, so one pass over the read serves both views).  A hit is checked
+// against every (piece, offset) entry of its 8-mer on the codes held in registers; an exact copy
+// marks the 16-position cells of the view where an alignment containing it can end.  Runs of
+// marked cells (gaps of <= 2 cells filled: a restricted start costs W warm-up positions anyway)
+// become filter tasks; a 3' view's last-column window is emitted here unless a task reaches the
+// view end (the task then emits it, merged with a nearby hit window, as the full filter does).
+// A part owns the piece copies that START in it, so each copy is seen by exactly one lane.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kPsItemsPerBlock = 512;   // items per screen block step (2 per thread)
+#ifndef DMX_PIECE_GRID
+#define DMX_PIECE_GRID (256 * 4)
+#endif
+constexpr uint32_t kPieceGrid = DMX_PIECE_GRID;   // resident blocks (persistent grids)
+#ifndef DMX_SCAN_GRID
+#define DMX_SCAN_GRID (256 * 8)
+#endif
+constexpr uint32_t kScanGrid = DMX_SCAN_GRID;     // the flat scan: 8 waves per SIMD
+
+__device__ __forceinline__ uint32_t ps_view_len(const RoundArgs& R, uint32_t item) {
+    if (R.items) {
+        if (!DMX_BOUND(R.pk.bd, items, item, kBufItem)) return 0u;
+        return R.items[item].len;
+    }
+    if (!DMX_BOUND(R.pk.bd, reads, item, kBufRead)) return 0u;
+    return R.lens[item];
+}
+// positions per part of a view of n positions (a multiple of 16, <= part_max) and the part count
+__device__ __forceinline__ uint32_t ps_part_len(uint32_t n, uint32_t pmax) {
+    const uint32_t np = (n + pmax - 1) / pmax;
+    return np <= 1 ? ((n + 15u) & ~15u) : (((n + np - 1) / np + 15u) & ~15u);
+}
+__device__ __forceinline__ uint32_t ps_parts(uint32_t n, uint32_t pmax, bool front) {
+    if (n == 0) return front ? 0u : 1u;   // an empty 3' view still gets its last-column window
+    const uint32_t pl = ps_part_len(n, pmax);
+    return (n + pl - 1) / pl;
+}
+// v[i] for a lane-varying i in [0, 4] (no indexed registers: a select chain)
+__device__ __forceinline__ uint32_t sel5(uint32_t i, uint32_t v0, uint32_t v1, uint32_t v2,
+                                         uint32_t v3, uint32_t v4) {
+    uint32_t r = i == 4u ? v4 : v3;
+    r = i == 2u ? v2 : r;
+    r = i == 1u ? v1 : r;
+    return i == 0u ? v0 : r;
+}
+// set cells [clo, chi] in a lane's 64-cell mask based at cell `base` (the host sizes parts so
+// that every cell a part can mark fits; a violation sets flag bit 16 and is reported)
+__device__ __forceinline__ void ps_mark(uint64_t& m, int base, int clo, int chi, uint32_t* flags) {
+    const int d0 = clo - base, d1 = chi - base;
+    if (d0 < 0 || d1 > 63) {
+        atomicOr(flags, 16u);
+        return;
+    }
+    m |= ((2ull << (d1 - d0)) - 1ull) << d0;   // d1 - d0 = 63: 2 << 63 wraps to 0, all ones
+}
+// Reserve this lane's `cnt` records of a sharded list with one global atomic per wave (every
+// lane of the wave calls it at the same point); returns the lane's first index in the shard.
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* gcount, uint32_t cnt) {
+    const int lane = (int)(threadIdx.x & 63u);
+    uint32_t x = cnt;   // inclusive scan over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, (unsigned)d, 64);
+        if (lane >= d) x += y;
+    }
+    const uint32_t total = __shfl(x, 63, 64);
+    uint32_t base = 0;
+    if (lane == 0 && total) base = atomicAdd(gcount, total);
+    base = __shfl(base, 0, 64);
+    return base + x - cnt;
+}
+// The filter tasks of marked cells in view order: runs of 16-position cells (cell u covers view
+// positions [16u - delta, 16u - delta + 16), clipped to the view), cut into segments of at most
+// kSegSpan positions with the W-position restricted-start warm-up before each (from the view
+// start: the panel's own column 0, no warm-up).
+struct PsRuns {
+    uint64_t m;
+    int base, delta, n, W, SEG, s, e;
+    __device__ __forceinline__ bool next(FTask& ft, uint32_t item, int o) {
+        while (s >= e) {
+            if (!m) return false;
+            const int u = (int)__builtin_ctzll((unsigned long long)m);
+            const uint64_t r = ~(m >> u);
+            const int run = r ? (int)__builtin_ctzll((unsigned long long)r) : 64 - u;
+            m &= run >= 64 ? 0ull : ~(((1ull << run) - 1ull) << u);
+            s = max(0, 16 * (base + u) - delta);
+            e = min(n, 16 * (base + u + run) - delta);
+        }
+        const int ee = min(e, s + SEG);
+        ft.item = item;
+        if (s < W) {
+            ft.p0 = 0;
+            ft.span = (uint16_t)ee;
+            ft.hoff = 0;
+            ft.flags = (uint8_t)(o | 2);
+        } else {
+            ft.p0 = (uint32_t)(s - W);
+            ft.span = (uint16_t)(ee - s + W);
+            ft.hoff = (uint8_t)W;
+            ft.flags = (uint8_t)o;
+        }
+        s = ee;
+        return true;
+    }
+};
+__device__ __forceinline__ void ftask_view(FTask& ft, const TaskView& tv) {
+    ft.flags |= (uint8_t)((tv.strand & 1u) << 2);
+    ft.n = tv.n;
+    ft.start = tv.start;
+    ft.len = tv.len;
+    ft.off = tv.off;
+}
+// Write one view's filter tasks (two passes: count, one wave reservation, write); returns whether
+// a task reaches the view end.  Every lane of the wave calls it.
+__device__ __forceinline__ bool ps_emit(const RoundArgs& R, FTask* fbuf, uint32_t* fcnt,
+                                        PsRuns rr, uint32_t item, int o, const TaskView& tv) {
+    uint32_t cnt = 0;
+    bool reached = false;
+    {
+        PsRuns c = rr;
+        FTask ft;
+        while (c.next(ft, item, o)) {
+            ++cnt;
+            reached |= (int)(ft.p0 + ft.span) == rr.n;
+        }
+    }
+    uint32_t fi = wave_reserve(fcnt, cnt);
+    FTask ft;
+    while (rr.next(ft, item, o)) {
+        ftask_view(ft, tv);
+        if (fi < R.ftask_scap) fbuf[fi] = ft;
+        else atomicOr(R.flags, 4u);
+        ++fi;
+    }
+    return reached;
+}
+// A 3' view's standalone last-column window (no task reaches the view end), clean when the view
+// holds no N in [n - rb, n) (what the exact stages read for it).  Every lane of the wave calls it.
+__device__ __forceinline__ void ps_lastcol(const RoundArgs& R, Window* wbuf, uint32_t* wcnt,
+                                           bool want, uint32_t item, int o, const TaskView& tv,
+                                           int rb) {
+    Window w;
+    if (want) {
+        const int n = (int)tv.len;
+        bool clean = false;
+        if (rb) {
+            clean = true;
+            for (int p = max(0, n - rb); p < n; p += 32) {
+                uint32_t mk = mask32s(R.pk, tv, p);
+                if (n - p < 32) mk &= (1u << (n - p)) - 1u;
+                clean &= mk == 0u;
+            }
+        }
+        w = make_window(item, o, tv, (uint32_t)n, (uint32_t)n, 1, 255, clean);
+    }
+    const uint32_t wi = wave_reserve(wcnt, want ? 1u : 0u);
+    if (want) {
+        if (wi < R.win_scap) wbuf[wi] = w;
+        else atomicOr(R.flags, 4u);
+    }
+}
+
+// The panel's piece tables -> LDS (dynamic: the fixed bitmap + rank base, then the keys and
+// entries); returns the entry array.
+struct PsTables {
+    uint32_t* bm;
+    uint16_t* rk;
+    uint32_t* key;
+    uint64_t* ent;
+};
+__device__ __forceinline__ PsTables ps_load_tables(const DevPieces* Q, uint8_t* dyn) {
+    PsTables t;
+    const int nk = Q->n_keys, ne = Q->n_entries;
+    t.bm = reinterpret_cast<uint32_t*>(dyn);
+    t.rk = reinterpret_cast<uint16_t*>(dyn + 4 * kPieceBitmapWords);
+    t.key = reinterpret_cast<uint32_t*>(dyn + kPieceLdsFixed);
+    t.ent = reinterpret_cast<uint64_t*>(dyn + kPieceLdsFixed + 8 * ((nk + 1) / 2));
+    for (int x = threadIdx.x; x < kPieceBitmapWords; x += blockDim.x) {
+        t.bm[x] = Q->bitmap[x];
+        t.rk[x] = Q->rank_base[x];
+    }
+    for (int x = threadIdx.x; x < nk; x += blockDim.x) t.key[x] = Q->key[x];
+    for (int x = threadIdx.x; x < ne; x += blockDim.x) t.ent[x] = Q->entry[x];
+    return t;
+}
+// The entries of 8-mer K (which the bitmap holds): [first, first + count) of t.ent
+__device__ __forceinline__ uint32_t ps_key(const PsTables& t, uint32_t K) {
+    const uint32_t wi = K >> 5;
+    const uint32_t rank = (uint32_t)t.rk[wi] + (uint32_t)__popc(t.bm[wi] & ((1u << (K & 31u)) - 1u));
+    return t.key[rank];
+}
+// 8-mer lookups of one 64-position step: w0..w5 = positions [C - 16, C + 80), samples C + qS
+template <int S>
+__device__ __forceinline__ typename std::conditional<S == 1, uint64_t, uint32_t>::type
+ps_lookups(const uint32_t* bm, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
+           uint32_t w5) {
+    using HitT = typename std::conditional<S == 1, uint64_t, uint32_t>::type;
+    HitT hits = 0;
+#if defined(DMX_PS_AB) && DMX_PS_AB >= 2   // timing A/B only (results invalid): no lookups
+    asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4), "v"(w5));
+#else
+    const uint32_t wv6[6] = {w0, w1, w2, w3, w4, w5};
+#pragma unroll
+    for (int q = 0; q < 64 / S; ++q) {
+        const int u = q * S + 16;
+        const uint32_t K = align32(wv6[(u >> 4) + 1], wv6[u >> 4], 2u * (u & 15));
+        const uint32_t word = bm[(K >> 5) & (uint32_t)(kPieceBitmapWords - 1)];
+        hits |= (HitT)__builtin_amdgcn_ubfe(word, K & 31u, 1) << q;
+    }
+#endif
+#if defined(DMX_PS_AB) && DMX_PS_AB >= 1   // timing A/B only: no candidate checks
+    asm volatile("" ::"v"(hits));
+    hits = 0;
+#endif
+    return hits;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-part piece screen (any batch layout; the flat scan below takes sorted, non-overlapping
+// batches): one lane per (item, part) of the item's orientation-0 view; the lane streams its
+// part's codes, looks up the sampled 8-mers, checks hits against their (piece, offset) entries
+// on the codes held in registers, and marks the 16-position cells of the view where an
+// alignment containing a verified copy can end.  A part owns the copies that START in it.
+// ---------------------------------------------------------------------------------------------
+#ifndef DMX_PIECE_WAVES
+#define DMX_PIECE_WAVES 1
+#endif
+template <int S>
+__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_PIECE_WAVES))) void pscreen_kernel(RoundArgs R) {
+    static_assert(S == 1 || S == 2 || S == 4, "sampling stride: 64 positions per step");
+    if (R.flat_bad && *R.flat_bad == 0u) return;   // the flat scan serves this batch
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    __shared__ uint32_t s_pre[kPsItemsPerBlock + 1];
+    __shared__ uint32_t s_sc[kScanBlock];
+    const DevPieces* Q = R.pieces;
+    const DevPanel* P = R.panel;
+    const uint32_t tid = threadIdx.x;
+    const PsTables tb_ = ps_load_tables(Q, s_dyn);
+    const uint32_t n_items = R.items ? *R.n_items_dev : R.n_items;
+    const bool front = P->where == kFront;
+    const uint32_t pmax = (uint32_t)Q->part_max;
+    const int A = P->n_adapters;
+    const int no = P->n_orient;
+    const uint32_t wsh = wave_shard();
+    FTask* const fbuf = R.ftask + wsh * R.ftask_scap;
+    uint32_t* const fcnt = R.ftask_count + wsh * kShardStride;
+    Window* const wbuf = R.win + wsh * R.win_scap;
+    uint32_t* const wcnt = R.win_count + wsh * kShardStride;
+    const int W = P->scan_len + P->kf;
+    const int SEG = kSegSpan - W;
+    const int rb = kCleanHist ? P->clean_reach : 0;
+    const int lo_off = Q->lo_off, dlo_min = Q->dlo_min;
+    const int fcells = (Q->front_reach + 15) >> 4;
+
+    for (uint32_t ib = blockIdx.x * kPsItemsPerBlock; ib < n_items;
+         ib += gridDim.x * kPsItemsPerBlock) {            // block-uniform
+        const uint32_t ni = min(n_items - ib, kPsItemsPerBlock);
+        // parts per item, block-wide exclusive scan (2 items per thread)
+        uint32_t c0 = 0, c1 = 0;
+        if (2 * tid < ni) c0 = ps_parts(ps_view_len(R, ib + 2 * tid), pmax, front);
+        if (2 * tid + 1 < ni) c1 = ps_parts(ps_view_len(R, ib + 2 * tid + 1), pmax, front);
+        __syncthreads();   // the previous step's s_pre / s_sc readers (and the table copy)
+        s_sc[tid] = c0 + c1;
+        __syncthreads();
+        for (uint32_t d = 1; d < kScanBlock; d <<= 1) {
+            const uint32_t x = tid >= d ? s_sc[tid - d] : 0u;
+            __syncthreads();
+            s_sc[tid] += x;
+            __syncthreads();
+        }
+        {
+            const uint32_t ex = s_sc[tid] - c0 - c1;
+            s_pre[2 * tid] = ex;
+            s_pre[2 * tid + 1] = ex + c0;
+        }
+        __syncthreads();
+        const uint32_t T = s_sc[kScanBlock - 1];
+
+        for (uint32_t tb = 0; tb < T; tb += kScanBlock) {
+            const uint32_t t = tb + tid;
+            uint32_t item = 0;
+            int n = 0, a = 0, b = 0;
+            bool act = false;
+            uint64_t m0 = 0, m1 = 0;
+            int base0 = 0, base1 = 0;
+            TaskView tv;
+            if (t < T) {
+                uint32_t lo = 0, hi = ni;              // the last item whose prefix is <= t
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_pre[mid] <= t) lo = mid;
+                    else hi = mid;
+                }
+                item = ib + lo;
+                const uint32_t part = t - s_pre[lo];
+                act = task_view(R, item, 0, A, tv);
+                n = (int)tv.len;
+                const int pl = (int)ps_part_len((uint32_t)n, pmax);
+                a = (int)part * pl;
+                b = min(n, a + pl);
+                base0 = a == 0 ? 0 : (a + lo_off) >> 4;
+                base1 = b == n ? 0 : max(0, n - b + dlo_min) >> 4;
+            }
+            // stream the part: w0..w5 = view positions [a - 16 + 64k, a + 80 + 64k) in step k,
+            // which samples x = a + 64k + q S: the 8-mer of positions [x, x + 8)
+            const int xe = b + S - 1;                  // copies starting in [a, b) are sampled
+            const int nsteps = (act && n > 0) ? (xe - a + 63) / 64 : 0;
+            if (nsteps > 0) {
+                uint32_t w0, w1, w2, w3, w4, w5, nb;
+                fetch16s<false>(R.pk, tv, a - 16, w0, nb);
+                fetch16s<false>(R.pk, tv, a, w1, nb);
+                ViewBlocks<false> B;
+                B.init(R, tv, a + 16);
+                for (int k = 0; k < nsteps; ++k) {
+                    uint32_t vc[4], vn[4];
+                    B.extract(vc, vn, k + 2 < nsteps);
+                    w2 = vc[0];
+                    w3 = vc[1];
+                    w4 = vc[2];
+                    w5 = vc[3];
+                    auto hits = ps_lookups<S>(tb_.bm, w0, w1, w2, w3, w4, w5);
+                    using HitT = decltype(hits);
+                    {
+                        const int lim = xe - (a + 64 * k);     // sampled positions < xe
+                        const int nq = lim >= 64 ? 64 / S : (lim <= 0 ? 0 : (lim + S - 1) / S);
+                        if (nq < 64 / S) hits &= (HitT)((((HitT)1) << nq) - (HitT)1);
+                    }
+                    while (hits) {
+                        const int q = (int)__builtin_ctzll((unsigned long long)hits);
+                        hits &= hits - (HitT)1;
+                        const int u = q * S + 16;
+                        const int x = a + 64 * k + q * S;
+                        const uint32_t ui = (uint32_t)u >> 4;
+                        const uint32_t K = align32(sel5(ui, w1, w2, w3, w4, w5),
+                                                   sel5(ui, w0, w1, w2, w3, w4),
+                                                   2u * ((uint32_t)u & 15u)) & 0xFFFFu;
+                        const uint32_t kr = ps_key(tb_, K);
+                        const int e0 = (int)(kr & 0xFFFFu), e1 = e0 + (int)(kr >> 16);
+                        for (int e = e0; e < e1; ++e) {
+                            const uint64_t ev = tb_.ent[e];
+                            const int len = (int)((ev >> 32) & 31u);
+                            const int off = (int)((ev >> 38) & 3u);
+                            const int g = x - off;
+                            if (g < a || g >= b || g + len > n) continue;
+                            const int ug = u - off;    // 14 .. 79
+                            const uint32_t gi = (uint32_t)ug >> 4;
+                            const uint32_t cw = align32(sel5(gi, w1, w2, w3, w4, w5),
+                                                        sel5(gi, w0, w1, w2, w3, w4),
+                                                        2u * ((uint32_t)ug & 15u));
+                            const uint32_t msk = len >= 16 ? ~0u : ((1u << (2 * len)) - 1u);
+                            if ((cw & msk) != (uint32_t)ev) continue;
+                            const int dlo = (int)((ev >> 40) & 255u) - 128;
+                            const int dhi = (int)((ev >> 48) & 255u) - 128;
+                            const bool o1 = ((ev >> 37) & 1u) != 0;
+                            // orientation 1: the copy sits at view-1 positions [n - g - len,
+                            // n - g), so its alignment ends at view-1 column n - g + d
+                            const int pe = o1 ? n - g : g + len;
+                            const int plo = max(pe + dlo - 1, 0), phi = min(pe + dhi - 1, n - 1);
+                            if (plo > phi) continue;
+                            if (o1) ps_mark(m1, base1, plo >> 4, phi >> 4, R.flags);
+                            else ps_mark(m0, base0, plo >> 4, phi >> 4, R.flags);
+                        }
+                    }
+                    w0 = w4;
+                    w1 = w5;
+                }
+            }
+            // filter tasks per orientation; a 3' view's last-column window unless a task of this
+            // lane reaches the view end (that task emits it, merged as the full filter does)
+            for (int o = 0; o < no; ++o) {
+                PsRuns rr{0ull, o ? base1 : base0, 0, n, W, SEG, 0, 0};
+                bool last = false;
+                TaskView tvo = tv;
+                if (act) {
+                    uint64_t m = o ? m1 : m0;
+                    const bool at_start = o == 0 ? a == 0 : b == n;   // holds view position 0
+                    last = !front && (o == 0 ? b == n : a == 0);      // ... the view's end
+                    if (front && at_start && n > 0)    // partial alignments from column 0
+                        ps_mark(m, rr.base, 0, min(fcells, (n + 15) >> 4) - 1, R.flags);
+                    const int ncell = ((n + 15) >> 4) - rr.base;      // cells inside the view
+                    if (ncell < 64) m &= ncell <= 0 ? 0ull : ((1ull << ncell) - 1ull);
+                    m |= ((m << 1) & (m >> 1)) | ((m << 1) & (m >> 2)) | ((m << 2) & (m >> 1));
+                    rr.m = m;
+                    if (o) task_view(R, item, A, A, tvo);
+                }
+                const bool reached = ps_emit(R, fbuf, fcnt, rr, item, o, tvo);
+                ps_lastcol(R, wbuf, wcnt, last && !reached, item, o, tvo, rb);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Flat piece scan, for batches whose reads are sorted and do not overlap (every
+// dmx_pack layout): waves stride over 4096-nt superblocks of the packed batch, lane l takes nt
+// [4096 b + 64 l, + 64) with one 16-B load (neighbours' words by lane shuffles), so every lane
+// does the same work and the loads are coalesced.  Sampled 8-mer hits go to a per-wave LDS queue
+// and are checked 64 at a time, one per lane: the read holding the copy (superblock index +
+// binary search over read ends), its view (round 2: the read's item), the copy against the
+// entry, then the cells of the view where an alignment containing the copy can end are marked in
+// the orientation's cell bitmap (global atomics).  pcompact_kernel turns the bitmaps into tasks.
+// ---------------------------------------------------------------------------------------------
+constexpr int kPsQueue = 128;   // per-wave candidate queue (<= 63 left + 64 pushed)
+
+// index of the read holding nt X (-1: none), searching the superblock's read range
+__device__ __forceinline__ int flat_read(const RoundArgs& R, uint64_t X) {
+    const uint32_t sb = (uint32_t)(X / kSuperNt);
+    uint32_t lo = R.sbf[sb], hi = R.sbf[min(sb + 1u, R.nsb)];   // first read ending past X in
+    hi = min(hi + 1u, R.n_reads);                               // [lo, hi]
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (R.offs[mid] + R.lens[mid] > X) hi = mid;
+        else lo = mid + 1;
+    }
+    if (lo >= R.n_reads || R.offs[lo] > X || R.offs[lo] + R.lens[lo] <= X) return -1;
+    return (int)lo;
+}
+
+// Check one queued sampled 8-mer (global nt X) against its entries and mark cells.
+__device__ __forceinline__ void flat_check(const RoundArgs& R, const PsTables& tb, uint64_t X,
+                                           int no) {
+    // codes of nt [X - 3, X + 29): every copy sampled at X starts at X - off, off <= 3
+    const uint64_t cw = ((uint64_t)code32(R.pk, (int64_t)X + 13) << 32) |
+                        (uint64_t)code32(R.pk, (int64_t)X - 3);
+    const uint32_t kr = ps_key(tb, (uint32_t)(cw >> 6) & 0xFFFFu);
+    const int r = flat_read(R, X);
+    if (r < 0) return;
+    const uint64_t off_r = R.offs[r];
+    const int nr = (int)R.lens[r];
+    int sg = 0, st = 0, l = nr;   // the item's view (round 1: the whole read, strand 0)
+    if (R.items) {
+        const uint32_t it = R.read_item[r];
+        if (it == ~0u) return;
+        const ItemView v = R.items[it];
+        sg = v.strand;
+        st = (int)v.start;
+        l = (int)v.len;
+    }
+    const int e0 = (int)(kr & 0xFFFFu), e1 = e0 + (int)(kr >> 16);
+    for (int e = e0; e < e1; ++e) {
+        const uint64_t ev = R.pieces->entry[e];   // (L1-resident: a few KB per panel)
+        const int len = (int)((ev >> 32) & 31u);
+        const int off = (int)((ev >> 38) & 3u);
+        const uint32_t msk = len >= 16 ? ~0u : ((1u << (2 * len)) - 1u);
+        if (((uint32_t)(cw >> (2 * (3 - off))) & msk) != (uint32_t)ev) continue;
+        const int tau = (int)((ev >> 37) & 1u);   // 1: the adapter reads reverse complemented
+        const int o = tau ^ sg;                   // the view that holds it forward
+        if (o >= no) continue;
+        const int G = (int)((int64_t)X - off - (int64_t)off_r);   // copy start in the read
+        if (G < 0 || G + len > nr) continue;
+        const int so = o ? nr - st - l : st;      // that view's start on strand tau
+        const int g = tau ? nr - so - G - len : G - so;            // copy start in the view
+        if (g < 0 || g + len > l) continue;
+        const int dlo = (int)((ev >> 40) & 255u) - 128;
+        const int dhi = (int)((ev >> 48) & 255u) - 128;
+        const int plo = max(g + len + dlo - 1, 0), phi = min(g + len + dhi - 1, l - 1);
+        if (plo > phi) continue;
+        // view positions -> nt of the read (strand tau) -> cells
+        int64_t nlo, nhi;
+        if (tau == 0) {
+            nlo = (int64_t)off_r + so + plo;
+            nhi = (int64_t)off_r + so + phi;
+        } else {
+            nlo = (int64_t)off_r + nr - 1 - so - phi;
+            nhi = (int64_t)off_r + nr - 1 - so - plo;
+        }
+        uint32_t* cells = R.cells[o];
+        for (int64_t c = nlo >> 4; c <= (nhi >> 4);) {   // one atomic per bitmap word
+            const int64_t w = c >> 5;
+            const int64_t cend = min(nhi >> 4, (w << 5) + 31);
+            const uint32_t bits = (uint32_t)((((2ull << (cend - c)) - 1ull)) << (c & 31));
+            atomicOr(cells + w, bits);
+            c = cend + 1;
+        }
+    }
+}
+
+template <int S>
+__global__ __launch_bounds__(kScanBlock) void pscan_kernel(RoundArgs R) {
+    static_assert(S == 1 || S == 2 || S == 4, "sampling stride: 64 positions per step");
+    if (*R.flat_bad) return;                          // the per-part screen serves this batch
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    __shared__ uint64_t s_q[kScanBlock / 64][kPsQueue];
+    const PsTables tb = ps_load_tables(R.pieces, s_dyn);
+    __syncthreads();
+    const int lane = (int)(threadIdx.x & 63u);
+    uint64_t* const q = s_q[threadIdx.x >> 6];
+    const int no = R.panel->n_orient;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t qn = 0;                                  // wave-uniform queue count
+    const uint4* sp = reinterpret_cast<const uint4*>(R.pk.seq);
+    const uint32_t nw = gridDim.x * (kScanBlock / 64);
+    const auto drain = [&](uint32_t cnt) {            // check q[0, cnt), keep q[cnt, qn)
+        if (lane < (int)cnt) flat_check(R, tb, q[lane], no);
+        uint64_t keep = 0;
+        const bool mv = lane + (int)cnt < (int)qn;
+        if (mv) keep = q[lane + cnt];
+        __builtin_amdgcn_wave_barrier();
+        if (mv) q[lane] = keep;
+        __builtin_amdgcn_wave_barrier();
+        qn -= cnt;
+    };
+    for (uint32_t sb = blockIdx.x * (kScanBlock / 64) + (threadIdx.x >> 6); sb < R.nsb; sb += nw) {
+        const int64_t wd = (int64_t)sb * (kSuperNt / 16) + 4 * lane;   // the lane's first word
+        const bool live = wd < (int64_t)R.n_words;
+        uint4 c = {0u, 0u, 0u, 0u};
+        if (live) c = sp[wd >> 2];
+        uint32_t w0 = __shfl_up(c.w, 1u, 64), w5 = __shfl_down(c.x, 1u, 64);
+        if (lane == 0) w0 = R.pk.seq[wd - 1];         // (the device guard covers word -1)
+        if (lane == 63) w5 = live ? R.pk.seq[wd + 4] : 0u;
+        auto hits = ps_lookups<S>(tb.bm, w0, c.x, c.y, c.z, c.w, w5);
+        using HitT = decltype(hits);
+        if (!live) hits = 0;
+        const uint64_t C = (uint64_t)wd * 16;         // nt of sample q: C + q S
+        for (;;) {   // push one hit per lane per pass; check 64 whenever they are queued
+            const uint64_t any = __ballot(hits != 0);
+            if (!any) break;
+            if (hits) {
+                const int qq = (int)__builtin_ctzll((unsigned long long)hits);
+                hits &= hits - (HitT)1;
+                q[qn + (uint32_t)__popcll(any & lt)] = C + (uint64_t)(qq * S);
+            }
+            __builtin_amdgcn_wave_barrier();
+            qn += (uint32_t)__popcll(any);
+            if (qn >= 64) drain(64);
+        }
+    }
+    if (qn) drain(qn);
+}
+
+// Flat scan -> filter tasks: one lane per item; per orientation the view's cells in view order
+// (cell u covers view positions [16u - delta, +16)), plus a FRONT panel's partial-alignment cells
+// at the view start; a 3' view's last-column window unless a task reaches the view end.
+__global__ __launch_bounds__(kScanBlock) void pcompact_kernel(RoundArgs R) {
+    if (*R.flat_bad) return;
+    const DevPanel* P = R.panel;
+    const DevPieces* Q = R.pieces;
+    const uint32_t n_items = R.items ? *R.n_items_dev : R.n_items;
+    const bool front = P->where == kFront;
+    const int A = P->n_adapters;
+    const int no = P->n_orient;
+    const int W = P->scan_len + P->kf;
+    const int SEG = kSegSpan - W;
+    const int rb = kCleanHist ? P->clean_reach : 0;
+    const int fr = Q->front_reach;
+    const uint32_t wsh = wave_shard();
+    FTask* const fbuf = R.ftask + wsh * R.ftask_scap;
+    uint32_t* const fcnt = R.ftask_count + wsh * kShardStride;
+    Window* const wbuf = R.win + wsh * R.win_scap;
+    uint32_t* const wcnt = R.win_count + wsh * kShardStride;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n_items; i0 += stride) {   // wave-uniform
+        const uint32_t item = i0 + threadIdx.x;
+        const bool act = item < n_items;
+        for (int o = 0; o < no; ++o) {
+            TaskView tv;
+            int l = 0;
+            if (act) {
+                task_view(R, item, o * A, A, tv);
+                l = (int)tv.len;
+            }
+            // nt of view position 0 and the walk direction through the cells
+            const int64_t p0nt = tv.strand ? (int64_t)tv.off + tv.n - 1 - tv.start
+                                           : (int64_t)tv.off + tv.start;
+            const int delta = act ? (tv.strand ? 15 - (int)(p0nt & 15) : (int)(p0nt & 15)) : 0;
+            const int ncell = act && l > 0 ? (l + delta + 15) >> 4 : 0;   // cells of the view
+            bool reached = false;
+            for (int k0 = 0; __ballot(k0 < ncell); k0 += 64) {
+                uint64_t m = 0;
+                if (k0 < ncell) {
+                    // cells k0 .. k0 + 63 in view order = bitmap cells c0 + u (strand 0) or
+                    // c0 - u (strand 1), c0 = the cell of view position 0
+                    const int64_t c0 = p0nt >> 4;
+                    const int64_t cs = tv.strand ? c0 - k0 - 63 : c0 + k0;   // lowest cell
+                    const uint32_t* cb = R.cells[o];
+                    const int64_t w = cs >> 5;                               // floor
+                    const uint32_t sh = (uint32_t)(cs & 31);
+                    const uint64_t lo = ((uint64_t)cb[w + 1] << 32) | cb[w];
+                    const uint64_t v = sh ? (lo >> sh) | ((uint64_t)cb[w + 2] << (64 - sh)) : lo;
+                    m = tv.strand ? __builtin_bitreverse64(v) : v;
+                    if (front && k0 == 0)               // partial alignments from column 0
+                        m |= (fr + delta + 15) >> 4 >= 64 ? ~0ull
+                                                          : ((1ull << ((fr + delta + 15) >> 4)) - 1ull);
+                    const int left = ncell - k0;
+                    if (left < 64) m &= (1ull << left) - 1ull;
+                    m |= ((m << 1) & (m >> 1)) | ((m << 1) & (m >> 2)) | ((m << 2) & (m >> 1));
+                }
+                PsRuns rr{m, k0, delta, l, W, SEG, 0, 0};
+                reached |= ps_emit(R, fbuf, fcnt, rr, item, o, tv);
+            }
+            ps_lastcol(R, wbuf, wcnt, act && !front && !reached, item, o, tv, rb);
+        }
+    }
+}
+
+// Flat-scan index of the resident batch: flat_bad = 0 iff the reads are sorted by offset and do
+// not overlap; sbf[b] = the first read whose end lies past nt 4096 b (b = 0 .. nsb).
+__global__ void flat_index_kernel(const uint64_t* offs, const uint32_t* lens, uint32_t n_reads,
+                                  uint32_t* sbf, uint32_t nsb, uint32_t* flat_bad) {
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r <= n_reads;
+         r += gridDim.x * blockDim.x) {
+        const uint64_t prev_end = r ? offs[r - 1] + lens[r - 1] : 0ull;
+        const uint64_t end = r < n_reads ? offs[r] + lens[r] : (uint64_t)nsb * kSuperNt + 1;
+        if (r < n_reads && r && offs[r] < prev_end) atomicOr(flat_bad, 1u);
+        // superblocks b with prev_end <= 4096 b < end: read r is the first ending past them
+        const uint64_t b0 = (prev_end + kSuperNt - 1) / kSuperNt;
+        for (uint64_t b = b0; b * kSuperNt < end && b <= nsb; ++b) sbf[b] = r;
+    }
+}
+
+// Round 2 of the flat scan: read -> its item (~0 = none).
+__global__ void read_item_kernel(const ItemView* items, const uint32_t* n_items,
+                                 uint32_t* read_item, uint32_t n_reads) {
+    const uint32_t n = *n_items;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        if (items[i].read < n_reads) read_item[items[i].read] = i;
+}
+
+// The shared-suffix filter over the piece screen's tasks: one lane per task, the same segment
+// scan, windows and last-column rule as filter_kernel (a task is a segment of at most kSegSpan
+// positions; tasks of one view never report the same column twice).
+__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_FILTER_WAVES))) void ftask_kernel(RoundArgs R) {
+    __shared__ uint32_t s_fpeq[8];
+    __shared__ __attribute__((aligned(16))) int8_t s_thr[kScanBlock];
+    __shared__ Window s_win[kScanBlock / 64][kWaveWinCap];
+    __shared__ uint32_t s_wcnt[kScanBlock / 64];
+    __shared__ uint32_t s_spre[kShards + 1];
+    const DevPanel* P = R.panel;
+    const int L = P->scan_len;
+    const int kf = P->kf;
+    if (threadIdx.x < 8) s_fpeq[threadIdx.x] = P->filter_peq[threadIdx.x];
+    if (threadIdx.x < kScanBlock / 64) s_wcnt[threadIdx.x] = 0;
+    {   // per-column hit thresholds near the view start (filter_kernel)
+        const int far0 = min((int)P->kf, (int)P->pf[71]);
+        const int j = (int)threadIdx.x + 1;
+        int t = -1;
+        for (int d = 0; d <= far0; ++d)
+            if (d <= (int)P->pf[min(j + d, 71)]) t = d;
+        s_thr[threadIdx.x] = (int8_t)t;
+    }
+    ShardMap sm{s_spre, 0u};
+    sm.load(R.ftask_count, R.ftask_scap);              // (its barrier covers the above)
+    const uint32_t total = sm.total();
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t wsh = wave_shard();
+    const WaveStage<Window, kWaveWinCap> st{s_win[wv], &s_wcnt[wv], R.win + wsh * R.win_scap,
+                                            R.win_count + wsh * kShardStride, R.win_scap,
+                                            R.flags, 4u};
+    const bool front = P->where == kFront;
+    const int kf_far = min(kf, (int)P->pf[71]);
+    const uint32_t gap = (uint32_t)P->max_mk;
+    const int rb = kCleanHist ? P->clean_reach : 0;
+    const uint32_t pv_rows = L >= 32 ? ~0u : ~0u << (32 - L);
+    for (uint32_t tb = blockIdx.x * kScanBlock; tb < total; tb += gridDim.x * kScanBlock) {
+        const uint32_t ti = tb + threadIdx.x;
+        if (ti < total) {
+            const FTask ft = R.ftask[sm.phys(ti)];
+            const int o = ft.flags & 1;
+            const bool fresh = (ft.flags & 2) != 0;
+            TaskView tv;
+            tv.read = 0;
+            tv.n = ft.n;
+            tv.start = ft.start;
+            tv.len = ft.len;
+            tv.strand = (ft.flags >> 2) & 1u;
+            tv.off = ft.off;
+            tv.o = o;
+            tv.a = 0;
+            const uint32_t P0 = ft.p0;
+            const uint32_t P1 = min(tv.len, P0 + (uint32_t)ft.span);
+            const uint32_t hit_from = fresh ? 0u : P0 + ft.hoff;
+            SegState S;
+            S.pv = (fresh && front) ? 0u : pv_rows;
+            S.mv = 0u;
+            S.e = ((fresh && front) ? 0 : L) - (kf_far + 1);
+            S.have = false;
+            S.w1 = S.w2 = 0;
+            S.wb = 255;
+            filter_segment(R, tv, P0, P1, S, s_fpeq, s_thr, kf_far, gap, hit_from, rb, st,
+                           ft.item, o);
+            const uint32_t len = tv.len;
+            if (!front && P1 == len) {   // the last column, merged with a nearby hit window
+                if (S.have && len - S.w2 <= gap) {
+                    st.push(make_window(ft.item, o, tv, S.w1, len, 1, S.wb,
+                                        window_clean(S, S.w1, len, rb)));
+                } else {
+                    if (S.have)
+                        st.push(make_window(ft.item, o, tv, S.w1, S.w2, 0, S.wb,
+                                            window_clean(S, S.w1, S.w2, rb)));
+                    st.push(make_window(ft.item, o, tv, len, len, 1, 255,
+                                        window_clean(S, len, len, rb)));
+                }
+                S.have = false;
+            }
+            if (S.have)
+                st.push(make_window(ft.item, o, tv, S.w1, S.w2, 0, S.wb,
                                     window_clean(S, S.w1, S.w2, rb)));
         }
         __builtin_amdgcn_wave_barrier();
@@ -3484,7 +4206,7 @@ int bounds_check(Ctx* c, const char* where) {
         "select_cand_kernel", "resolve_kernel", "select_kernel", "finalize0_kernel",
         "finalize1_kernel", "finalize0_linked_kernel", "finalize1_linked_kernel",
         "finalize2_linked_kernel", "chop_kernel", "chop_big_kernel", "chop_start",
-        "bounds_selftest_kernel"};
+        "bounds_selftest_kernel", "pscreen_kernel"};
     static const char* const kBuf[] = {"?", "seq", "nmask", "winner slots", "items", "results",
                                        "counts", "reads", "linked keys", "candidates", "chop"};
     uint32_t rec[4];
@@ -3552,8 +4274,56 @@ int bounds_selftest(Ctx* c, uint32_t* host_out) {
 #endif
 }
 
+// The flat piece scan's index of the resident batch: sortedness flag and
+// superblock -> first read, rebuilt after every load; the cell bitmaps sized to the batch.
+int prepare_flat(Ctx* c, hipStream_t st) {
+    c->flat_ok_launch = false;
+    bool want = false;
+    for (int r = 0; r < 2; ++r)
+        want |= c->panel[r].set && c->panel[r].piece_step && c->panel[r].n_orient == 2 &&
+                (r == 0 || c->mode == DMX_MODE_TWO_ROUND);
+    if (!want || c->n_reads == 0 || std::getenv("DMX_NO_FLAT")) return DMX_OK;
+    const size_t nsb = (c->n_words + kSuperNt / 16 - 1) / (kSuperNt / 16);
+    if (nsb + 1 >= (1ull << 32) || c->n_reads >= (1ull << 31)) return DMX_OK;
+    if (c->sbf_cap < nsb + 1 || !c->d_sbf) {
+        if (c->d_sbf) hipFree(c->d_sbf);
+        c->d_sbf = nullptr;
+        if (hipMalloc((void**)&c->d_sbf, (nsb + 1) * 4) != hipSuccess) return DMX_E_NOMEM;
+        c->sbf_cap = nsb + 1;
+        c->flat_dirty = true;
+    }
+    if (!c->d_flat_bad && hipMalloc((void**)&c->d_flat_bad, 4) != hipSuccess) return DMX_E_NOMEM;
+    const size_t cw = (c->n_words + 31) / 32 + 2 * kCellGuardWords;
+    if (c->cells_cap < cw || !c->d_cells[0]) {
+        for (int o = 0; o < 2; ++o) {
+            if (c->d_cells[o]) hipFree(c->d_cells[o]);
+            c->d_cells[o] = nullptr;
+            if (hipMalloc((void**)&c->d_cells[o], cw * 4) != hipSuccess) return DMX_E_NOMEM;
+        }
+        c->cells_cap = cw;
+    }
+    c->cells_words = cw;
+    if (c->read_item_cap < c->n_reads || !c->d_read_item) {
+        if (c->d_read_item) hipFree(c->d_read_item);
+        c->d_read_item = nullptr;
+        if (hipMalloc((void**)&c->d_read_item, c->n_reads * 4) != hipSuccess) return DMX_E_NOMEM;
+        c->read_item_cap = c->n_reads;
+    }
+    if (c->flat_dirty || c->n_sb != nsb) {
+        hipMemsetAsync(c->d_flat_bad, 0, 4, st);
+        const uint32_t grid = (uint32_t)std::min<size_t>((c->n_reads + 256) / 256, 4096);
+        hipLaunchKernelGGL(flat_index_kernel, dim3(grid), dim3(256), 0, st, c->d_offs, c->d_lens,
+                           (uint32_t)c->n_reads, c->d_sbf, (uint32_t)nsb, c->d_flat_bad);
+        c->n_sb = nsb;
+        c->flat_dirty = false;
+    }
+    c->flat_ok_launch = true;
+    return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
+}
+
 int launch_round(Ctx* c, int round, hipStream_t st) {
     RoundArgs R;
+    R.flat_bad = nullptr;
     R.pk.seq = c->d_seq;
     R.pk.nmask = c->d_nmask;
     R.pk.bd = make_bounds(c, 0);
@@ -3612,13 +4382,75 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     R.task_count = c->d_shard + (kShTasks + round) * kShards * kShardStride;
     R.task_cap = (uint32_t)c->task_cap;
     R.task_scap = (uint32_t)(c->task_cap / kShards);
+    R.pieces = c->d_pieces[round];
+    R.ftask = c->d_ftask;
+    R.ftask_count = c->d_shard + (kShFtask + round) * kShards * kShardStride;
+    R.ftask_scap = (uint32_t)(c->ftask_cap / kShards);
     hipEventRecord(c->ev[round * 3 + 0], st);
     if (hp.filter && !linked) {   // linked primers: short, no shared suffix block; plain scan
-        const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
-        const uint32_t fgrid = (uint32_t)((nviews + kSegViewsPerBlock - 1) / kSegViewsPerBlock);
-        set_kid(R.pk.bd, kKerFilter);
-        if (fgrid > 0) hipLaunchKernelGGL(filter_kernel, dim3(fgrid), dim3(kScanBlock), 0, st, R);
-        DMX_DBG_SYNC("filter_kernel");
+        if (hp.piece_step) {      // piece screen, then the filter on its tasks
+            const DevPieces& Q = hp.pieces;   // LDS image: bitmap + rank base, keys, entries
+            const size_t lds = (size_t)kPieceLdsFixed + 8 * ((Q.n_keys + 1) / 2) +
+                               8 * (size_t)Q.n_entries;
+            const bool flat = c->flat_ok_launch && hp.n_orient == 2;
+            if (flat) {   // the flat scan (its kernels exit when the batch is not sorted)
+                R.flat_bad = c->d_flat_bad;
+                R.sbf = c->d_sbf;
+                R.nsb = (uint32_t)c->n_sb;
+                R.n_words = (uint32_t)c->n_words;
+                R.read_item = c->d_read_item;
+                R.n_reads = (uint32_t)c->n_reads;
+                for (int o = 0; o < 2; ++o) R.cells[o] = c->d_cells[o] + kCellGuardWords;
+                hipMemsetAsync(c->d_cells[0], 0, 4 * c->cells_words, st);
+                hipMemsetAsync(c->d_cells[1], 0, 4 * c->cells_words, st);
+                if (round == 1) {
+                    hipMemsetAsync(c->d_read_item, 0xFF, 4 * c->n_reads, st);
+                    hipLaunchKernelGGL(read_item_kernel, dim3(1024), dim3(256), 0, st, c->d_items,
+                                       c->d_counters + 2, c->d_read_item, (uint32_t)c->n_reads);
+                }
+                const uint32_t sgrid = (uint32_t)std::min<size_t>((c->n_sb + 3) / 4, kScanGrid);
+                set_kid(R.pk.bd, kKerPieces);
+                if (sgrid > 0) {
+                    if (hp.piece_step == 4)
+                        hipLaunchKernelGGL(pscan_kernel<4>, dim3(sgrid), dim3(kScanBlock), lds, st, R);
+                    else if (hp.piece_step == 2)
+                        hipLaunchKernelGGL(pscan_kernel<2>, dim3(sgrid), dim3(kScanBlock), lds, st, R);
+                    else
+                        hipLaunchKernelGGL(pscan_kernel<1>, dim3(sgrid), dim3(kScanBlock), lds, st, R);
+                }
+                DMX_DBG_SYNC("pscan_kernel");
+                const uint32_t cgrid = std::min<uint32_t>((R.n_items + 255) / 256, 2048u);
+                if (cgrid > 0)
+                    hipLaunchKernelGGL(pcompact_kernel, dim3(cgrid), dim3(kScanBlock), 0, st, R);
+                DMX_DBG_SYNC("pcompact_kernel");
+            } else {
+                R.flat_bad = nullptr;
+            }
+            const uint32_t pgrid = (uint32_t)((R.n_items + kPsItemsPerBlock - 1) / kPsItemsPerBlock);
+            const uint32_t grid = std::min<uint32_t>(pgrid, kPieceGrid);
+            set_kid(R.pk.bd, kKerPieces);
+            if (pgrid > 0) {   // the per-part screen (exits at once when the flat scan ran)
+                if (hp.piece_step == 4)
+                    hipLaunchKernelGGL(pscreen_kernel<4>, dim3(grid), dim3(kScanBlock), lds, st, R);
+                else if (hp.piece_step == 2)
+                    hipLaunchKernelGGL(pscreen_kernel<2>, dim3(grid), dim3(kScanBlock), lds, st, R);
+                else
+                    hipLaunchKernelGGL(pscreen_kernel<1>, dim3(grid), dim3(kScanBlock), lds, st, R);
+            }
+            DMX_DBG_SYNC("pscreen_kernel");
+            hipEventRecord(c->ev[15 + round], st);
+            set_kid(R.pk.bd, kKerFilter);
+            hipLaunchKernelGGL(ftask_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
+            DMX_DBG_SYNC("ftask_kernel");
+        } else {
+            const uint64_t nviews = (uint64_t)R.n_items * (uint64_t)hp.n_orient;
+            const uint32_t fgrid =
+                (uint32_t)((nviews + kSegViewsPerBlock - 1) / kSegViewsPerBlock);
+            set_kid(R.pk.bd, kKerFilter);
+            if (fgrid > 0)
+                hipLaunchKernelGGL(filter_kernel, dim3(fgrid), dim3(kScanBlock), 0, st, R);
+            DMX_DBG_SYNC("filter_kernel");
+        }
         hipEventRecord(c->ev[9 + 2 * round], st);
         set_kid(R.pk.bd, kKerVerify);
         if (hp.verify)

@@ -404,18 +404,19 @@ class Context:
         return buf.view(CAND_DTYPE if what in (DBG_CANDS0, DBG_CANDS1) else WINDOW_DTYPE)
 
     def stats(self):
-        ms = (ctypes.c_float * 15)()
-        cl = np.zeros(12, dtype=np.uint64)
+        ms = (ctypes.c_float * 17)()
+        cl = np.zeros(14, dtype=np.uint64)
         fl = ctypes.c_int()
-        self._check(self._L.dmx_stats(self._h, ms, 15, cl.ctypes.data, 12, ctypes.byref(fl)),
+        self._check(self._L.dmx_stats(self._h, ms, 17, cl.ctypes.data, 14, ctypes.byref(fl)),
                     "dmx_stats")
+        # filterN: the whole filter stage (with the piece screen, when on: piecesN is its part)
         names = ["scan0", "resolve0", "finalize0", "scan1", "resolve1", "finalize1", "total",
                  "filter0", "verify0", "filter1", "verify1", "screen0", "wscan0", "screen1",
-                 "wscan1"]
+                 "wscan1", "pieces0", "pieces1"]
         return {"ms": dict(zip(names, list(ms))), "clusters": cl[:2].tolist(),
                 "windows": cl[2:4].tolist(), "resolved": cl[4:6].tolist(),
                 "traces": cl[6:8].tolist(), "windows_raw": cl[8:10].tolist(),
-                "tasks": cl[10:12].tolist(),
+                "tasks": cl[10:12].tolist(), "filter_tasks": cl[12:14].tolist(),
                 "flags": fl.value}
 
 
