@@ -82,6 +82,14 @@ int dmx_set_panel_mixed(dmx_ctx* ctx, int round, const char* const* seqs, const 
                         const int* wheres, int n_adapters, double max_errors, int min_overlap,
                         int rc);
 int dmx_set_mode(dmx_ctx* ctx, int mode);
+/* Host only (no GPU; tests): the piece screen dmx_set_panel would build for
+ * these arguments: out[0..7] = {sampling stride (0 = off: the full filter pass), pieces, sampled
+ * 8-mer keys, entries, FRONT partial-alignment reach, positions per screen lane, min len + dlo - 1
+ * of orientation-0 pieces, min dlo of orientation-1 pieces}; entries (up to cap, may be NULL):
+ * the packed (piece, offset) entries, grouped by 8-mer (dmx_device.h piece_entry). */
+int dmx_panel_pieces(const char* const* seqs, const int* lens, int n_adapters, double max_errors,
+                     int min_overlap, int flags, int32_t* out, int n_out, uint64_t* entries,
+                     int cap);
 /* Host only (no GPU; tests): how far the kernels' gathers reach around a read view for the
  * panel dmx_set_panel (wheres == NULL) or dmx_set_panel_mixed (wheres, flags & DMX_RC) would
  * build from these arguments, in nt: out[0] before view position 0 as the kernels' warm-up

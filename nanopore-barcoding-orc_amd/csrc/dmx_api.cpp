@@ -874,6 +874,28 @@ int dmx_load(dmx_ctx* c, const uint32_t* seq2b, const uint32_t* nmask, const uin
     return load_impl(c, seq2b, m, offsets, lens, n_words, n_reads);
 }
 
+int dmx_panel_pieces(const char* const* seqs, const int* lens, int n, double max_errors,
+                     int min_overlap, int flags, int32_t* out, int n_out, uint64_t* entries,
+                     int cap) {
+    if (!out || n_out < 8) return DMX_E_INVALID;
+    Ctx tmp;   // never opened: build_panel reads only the A/B switches dmx_open would set
+    const char* np = std::getenv("DMX_NO_PIECES");
+    tmp.no_pieces = np && np[0] == '1';
+    HostPanel hp;
+    DevPanel dp;
+    const int rc = build_panel(&tmp, seqs, lens, nullptr, n, max_errors, min_overlap, flags, hp,
+                               dp);
+    for (int i = 0; i < n_out; ++i) out[i] = 0;
+    if (rc != DMX_OK) return rc;
+    const DevPieces& Q = hp.pieces;
+    const int32_t v[8] = {hp.piece_step, Q.n_pieces, Q.n_keys, Q.n_entries, Q.front_reach,
+                          Q.part_max, Q.lo_off, Q.dlo_min};
+    for (int i = 0; i < 8; ++i) out[i] = v[i];
+    if (entries)
+        for (int e = 0; e < Q.n_entries && e < cap; ++e) entries[e] = Q.entry[e];
+    return DMX_OK;
+}
+
 int dmx_panel_reach(const char* const* seqs, const int* lens, const int* wheres, int n,
                     double max_errors, int min_overlap, int flags, int32_t* out, int n_out) {
     if (!out || n_out < 6) return DMX_E_INVALID;

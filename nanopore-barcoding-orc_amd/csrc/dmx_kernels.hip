@@ -1950,7 +1950,7 @@ __device__ __forceinline__ void flat_check(const RoundArgs& R, const PsTables& t
     }
     const int e0 = (int)(kr & 0xFFFFu), e1 = e0 + (int)(kr >> 16);
     for (int e = e0; e < e1; ++e) {
-        const uint64_t ev = R.pieces->entry[e];   // (L1-resident: a few KB per panel)
+        const uint64_t ev = tb.ent[e];
         const int len = (int)((ev >> 32) & 31u);
         const int off = (int)((ev >> 38) & 3u);
         const uint32_t msk = len >= 16 ? ~0u : ((1u << (2 * len)) - 1u);

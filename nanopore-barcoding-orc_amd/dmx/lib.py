@@ -40,7 +40,7 @@ EXPORTS = ["dmx_abi_version", "dmx_open", "dmx_close", "dmx_last_error", "dmx_se
            "dmx_chop_stats", "dmx_comm_unique_id", "dmx_comm_init_rank", "dmx_comm_init_all",
            "dmx_comm_size", "dmx_allreduce_counts", "dmx_debug_fetch", "dmx_run_sparse",
            "dmx_mask_exceptions", "dmx_host_register", "dmx_host_unregister", "dmx_panel_reach",
-           "dmx_debug_bounds_selftest"]
+           "dmx_debug_bounds_selftest", "dmx_panel_pieces"]
 ABI_VERSION = 4
 COMM_ID_BYTES = 128
 
@@ -135,6 +135,9 @@ def load() -> ctypes.CDLL:
         L.dmx_panel_reach.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int), P,
                                       c_int, ctypes.c_double, c_int, c_int, P, c_int]
         L.dmx_debug_bounds_selftest.argtypes = [P, P]
+    if hasattr(L, "dmx_panel_pieces"):
+        L.dmx_panel_pieces.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int),
+                                       c_int, ctypes.c_double, c_int, c_int, P, c_int, P, c_int]
     # DMX_ALLOW_ABI=1: load an older in-tree build for a regression A/B (tools/replay_sweep.py)
     if L.dmx_abi_version() != ABI_VERSION and os.environ.get("DMX_ALLOW_ABI") != "1":
         raise DmxError("libdmx ABI mismatch")
@@ -433,6 +436,29 @@ def panel_reach(seqs, flags: int, max_errors: float = 0.1, min_overlap: int = 3,
                            int(flags), out.ctypes.data, 6)
     return rc, dict(zip(["pre_raw", "pre", "post", "need_pre", "need_post", "guard"],
                         out.tolist()))
+
+
+PIECE_FIELDS = ["step", "pieces", "keys", "entries", "front_reach", "part_max", "lo_off",
+                "dlo_min"]
+
+
+def panel_pieces(seqs, flags: int, max_errors: float = 0.1, min_overlap: int = 3):
+    """Host only: (status, info, entries) of the piece screen dmx_set_panel would build
+    (include/dmx.h dmx_panel_pieces).  entries: dicts of the packed (piece, offset) entries."""
+    L = load()
+    arr = (ctypes.c_char_p * len(seqs))(*[s.encode("ascii") for s in seqs])
+    lens = (ctypes.c_int * len(seqs))(*[len(s) for s in seqs])
+    out = np.zeros(8, dtype=np.int32)
+    ent = np.zeros(4096, dtype=np.uint64)
+    rc = L.dmx_panel_pieces(arr, lens, len(seqs), float(max_errors), int(min_overlap), int(flags),
+                            out.ctypes.data, 8, ent.ctypes.data, len(ent))
+    info = dict(zip(PIECE_FIELDS, out.tolist()))
+    ents = []
+    for v in ent[:info["entries"]].tolist():
+        ents.append({"val": v & 0xFFFFFFFF, "len": (v >> 32) & 31, "o": (v >> 37) & 1,
+                     "off": (v >> 38) & 3, "dlo": ((v >> 40) & 255) - 128,
+                     "dhi": ((v >> 48) & 255) - 128})
+    return rc, info, ents
 
 
 def host_register(arrays) -> list:
