@@ -67,6 +67,8 @@ typedef struct dmx_ctx dmx_ctx;
 int dmx_open(int device, dmx_ctx** out);
 /* Replaces: cutadapt's exit. */
 void dmx_close(dmx_ctx* ctx);
+/* ctx = NULL: the last failure of a call that takes no context (dmx_comm_unique_id: why RCCL
+ * could not be loaded), or "null context". */
 const char* dmx_last_error(dmx_ctx* ctx);
 int dmx_abi_version(void);
 

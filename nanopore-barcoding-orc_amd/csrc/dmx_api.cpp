@@ -222,6 +222,21 @@ int grow_clusters(Ctx* c) {
 
 namespace dmx {
 
+namespace {
+std::mutex g_proc_err_mu;
+std::string g_proc_err;
+}  // namespace
+
+void set_process_error(const std::string& msg) {
+    std::lock_guard<std::mutex> lk(g_proc_err_mu);
+    g_proc_err = msg;
+}
+
+std::string process_error() {
+    std::lock_guard<std::mutex> lk(g_proc_err_mu);
+    return g_proc_err;
+}
+
 // The kernels' reach around a view, per panel.  A 16-position gather at view
 // position p physically loads two aligned u32 words, i.e. view positions [p - 16, p + 32) on
 // either strand; whole-block loads (ViewBlocks: filter, verify) cover [p - 63, p + 64 s + 127]
@@ -342,7 +357,15 @@ void dmx_close(dmx_ctx* c) {
     delete c;
 }
 
-const char* dmx_last_error(dmx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+const char* dmx_last_error(dmx_ctx* c) {
+    if (c) return c->err.c_str();
+    // no context: the last context-free failure (thread-local copy: the pointer stays valid
+    // until this thread's next call)
+    thread_local std::string msg;
+    msg = dmx::process_error();
+    if (msg.empty()) msg = "null context";
+    return msg.c_str();
+}
 
 int dmx_set_mode(dmx_ctx* c, int mode) {
     if (!c) return DMX_E_INVALID;

@@ -124,10 +124,18 @@ extern "C" {
 
 int dmx_comm_unique_id(uint8_t* id) {
     if (!id) return DMX_E_INVALID;
-    const Rccl* R = rccl();
-    if (!R) return DMX_E_UNSUPPORTED;
+    std::string why;   // no context to keep it in: the process-wide message (dmx_last_error(NULL))
+    const Rccl* R = rccl(&why);
+    if (!R) {
+        dmx::set_process_error(why);
+        return DMX_E_UNSUPPORTED;
+    }
     ncclUniqueId u;
-    if (R->GetUniqueId(&u) != ncclSuccess) return DMX_E_HIP;
+    const ncclResult_t r = R->GetUniqueId(&u);
+    if (r != ncclSuccess) {
+        dmx::set_process_error(std::string("ncclGetUniqueId: ") + R->GetErrorString(r));
+        return DMX_E_HIP;
+    }
     std::memcpy(id, &u, sizeof(u));
     return DMX_OK;
 }

@@ -224,7 +224,9 @@ inline size_t huff_deflate(const uint8_t* src, size_t n, uint8_t* out) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Record-aware LZ77 + Huffman: the writers' levels 2..6 (dmx_io.cpp gzip_member).
+// Record-aware LZ77 + Huffman: the writers' levels 2..9 (dmx_io.cpp gzip_member routes every
+// level from 2 to 9 here and ignores the level: -2 and -9 give the same stream;
+// DMX_GZIP_LIBDEFLATE=1 restores per-level output through libdeflate).
 //
 // Split by line type, zlib -5 and Huffman-only compare like this on nanopore-style FASTQ
 // (MinKNOW headers, autocorrelated qualities; profiles/r5_gzip_levels.json): headers 6.4 MB ->

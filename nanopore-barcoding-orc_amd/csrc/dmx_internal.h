@@ -142,6 +142,10 @@ struct Ctx {
 void chop_release(Ctx* c);
 void comm_release(Ctx* c);
 int reset_counts(Ctx* c);      // size d_counts for the current panels/mode and zero it (sync)
+// The last error of a call that has no context to keep it in (dmx_comm_unique_id's RCCL load),
+// returned by dmx_last_error(NULL).
+void set_process_error(const std::string& msg);
+std::string process_error();
 void chop_invalidate(Ctx* c);   // a new dmx_load makes the last dmx_chop_exec's results stale
 int launch_round(Ctx* c, int round, hipStream_t st);
 int prepare_flat(Ctx* c, hipStream_t st);   // the flat piece scan's index (dmx_kernels.hip)

@@ -4,7 +4,7 @@ Drop-in for the reference's one pychopper call:
   pychopper -b M13_seqs_for_pychopper.fa -c M13_config_for_pychopper.txt -k LSK114 -Q 10
             -w RESCUED.fastq -u UNCLASS.fastq -l SHORT.fastq -S STATS.out -p -t 24 -m edlib
             IN.fastq.gz > PASS.fastq
-pychopper 2.7.10 (edlib backend) is not vendored in /root/reference and not installed here: the
+pychopper v2.7.0 (edlib backend) is not vendored in /root/reference and not installed here: the
 semantics are the build's restatement, checked against oracle/chopper.py, parity
 unpinned.  Primer hits and segments come from libdmx (`dmx_chop_*`, HIP; no CPU fallback).
 Per QC-passing read:

@@ -504,7 +504,9 @@ def comm_unique_id() -> bytes:
     with _stdout_to_stderr():
         rc = load().dmx_comm_unique_id(buf)
     if rc != 0:
-        raise DmxError(f"dmx_comm_unique_id failed ({rc})")
+        why = load().dmx_last_error(None)   # the context-free message (e.g. RCCL not loadable)
+        raise DmxError(f"dmx_comm_unique_id failed ({rc}): "
+                       f"{why.decode(errors='replace') if why else 'no message'}")
     return buf.raw
 
 

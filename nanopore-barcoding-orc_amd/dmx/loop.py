@@ -161,6 +161,7 @@ def run(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     args = build_parser().parse_args(argv)
     infile = args.infile
+    base = pych_dir = None
     if args.reorient:   # 01_pychopper.sh:21-31 names; 02 reads pychopped/pychopped_<base>
         base = base_name(infile)
         pych_dir = args.pychopper_dir or os.path.join(os.path.dirname(os.path.abspath(infile)),
@@ -223,11 +224,24 @@ def run(argv=None) -> int:
     # the reader's producer thread starts on the first batch while the device contexts open
     batch = (args.batch_mb << 20) if args.batch_mb > 0 else nio.batch_bytes_for_budget()
     reader = nio.Reader(infile, batch, threads=args.threads)
-    try:
-        ctxs = lib.open_group(_devices(args))
+    ctxs = []
+    try:   # from the reader on: any failure closes whatever is open
+        return _loop_body(args, argv, infile, outdir, ds, demux_in, pych_dir, base, ads1, ads2,
+                          n1, n2, out2, p1, p2, marks, reader, ctxs)
     except BaseException:
         reader.close()
+        for ctx in ctxs:
+            ctx.close()
         raise
+
+
+def _loop_body(args, argv, infile, outdir, ds, demux_in, pych_dir, base, ads1, ads2, n1, n2,
+               out2, p1, p2, marks, reader, ctxs):
+    """The fused loop after the reader is open; `ctxs` is filled in place so that the caller can
+    close the device contexts when anything here raises (sinks and the reorienter are closed
+    below on every path)."""
+    ctxs.extend(lib.open_group(_devices(args)))
+    reo = sink1 = sink2 = None
     marks.append(("open", time.perf_counter() - _T_IMPORT))
     for ctx in ctxs:
         ctx.set_panel(0, [a.seq for a in ads1], lib.DMX_FRONT | lib.DMX_RC, args.e_rate, 3)
@@ -241,16 +255,24 @@ def run(argv=None) -> int:
         s = Stats(ads2)
         s.rc_mode = True
         st2.append(s)
-    reo = None
-    if args.reorient:
-        reo = Reorienter(args, pych_dir, base)
-    t0 = time.perf_counter()
-    marks.append(("outputs", t0 - _T_IMPORT))
-    print("Round 1: Demultiplexing with SP5 adapters...")
-    print("Round 2: Demultiplexing with SP27 adapters (fused with round 1)...")
-    level = 1 if args.zlevel1 else args.compression_level
-    sink1 = nio.Sink(p1, False, level, threads=args.threads)
-    sink2 = nio.Sink(p2, False, level, threads=args.threads)
+    try:
+        if args.reorient:
+            reo = Reorienter(args, pych_dir, base)
+        t0 = time.perf_counter()
+        marks.append(("outputs", t0 - _T_IMPORT))
+        print("Round 1: Demultiplexing with SP5 adapters...")
+        print("Round 2: Demultiplexing with SP27 adapters (fused with round 1)...")
+        level = 1 if args.zlevel1 else args.compression_level
+        sink1 = nio.Sink(p1, False, level, threads=args.threads)
+        sink2 = nio.Sink(p2, False, level, threads=args.threads)
+    except BaseException:
+        for x in (sink1, sink2, reo):
+            if x is not None:
+                try:
+                    x.close()
+                except Exception:   # the original error is the one to report
+                    pass
+        raise
     bp2_out = np.zeros(len(n1), np.int64)
     prof = dict(read_wait=0.0, gpu=0.0, plan_write=0.0, drain=0.0)
     if reo is not None:   # parts of "gpu": pychopper step, view packing

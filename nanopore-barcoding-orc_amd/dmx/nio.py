@@ -246,20 +246,85 @@ def _read_int(path: str):
         return None
 
 
+# Where the cgroup hierarchy is mounted and where this process's membership is listed (module
+# attributes: tests point them at a fake tree).
+CGROUP_ROOT = "/sys/fs/cgroup"
+PROC_CGROUP = "/proc/self/cgroup"
+_NO_LIMIT = 1 << 60   # v1 reports "unlimited" as a huge number
+
+
+def _cgroup_memory_dirs():
+    """(directory, limit file, usage file) of every memory cgroup this process is in, from its
+    own cgroup up to the hierarchy's root: the v2 unified line "0::<path>" and the v1 "memory"
+    controller line of /proc/self/cgroup.  A SLURM job without a cgroup namespace sits in a
+    nested cgroup (…/job_N/step_M/…) whose limit the root files do not show; the root itself
+    is always listed last (a container's own namespace shows "0::/")."""
+    out = []
+    try:
+        with open(PROC_CGROUP) as fh:
+            lines = fh.read().splitlines()
+    except OSError:
+        lines = []
+    for line in lines:
+        parts = line.split(":", 2)
+        if len(parts) != 3:
+            continue
+        hid, ctrls, path = parts
+        if hid == "0" and ctrls == "":
+            root, files = CGROUP_ROOT, ("memory.max", "memory.current")
+        elif "memory" in ctrls.split(","):
+            root, files = os.path.join(CGROUP_ROOT, "memory"), ("memory.limit_in_bytes",
+                                                                 "memory.usage_in_bytes")
+        else:
+            continue
+        rel = [x for x in path.strip().strip("/").split("/") if x and x != ".."]
+        for i in range(len(rel), -1, -1):
+            d = os.path.join(root, *rel[:i])
+            out.append((d, os.path.join(d, files[0]), os.path.join(d, files[1])))
+    # without /proc/self/cgroup: the mount roots, as before
+    out.append((CGROUP_ROOT, os.path.join(CGROUP_ROOT, "memory.max"),
+                os.path.join(CGROUP_ROOT, "memory.current")))
+    out.append((os.path.join(CGROUP_ROOT, "memory"),
+                os.path.join(CGROUP_ROOT, "memory", "memory.limit_in_bytes"),
+                os.path.join(CGROUP_ROOT, "memory", "memory.usage_in_bytes")))
+    return out
+
+
+def _budget_env_mb():
+    """DMX_MEM_BUDGET_MB in MB: a number of MB, or with a SLURM-style suffix K, M, G or T
+    (2048, 2048M, 2G, 1.5G); 0 or empty = unset.  Anything else raises DmxError naming the
+    variable (it would otherwise surface as a bare ValueError on the first I/O call)."""
+    raw = os.environ.get("DMX_MEM_BUDGET_MB", "").strip()
+    if not raw:
+        return None
+    v = raw.upper().rstrip("B")
+    scale = {"K": 1 / 1024, "M": 1, "G": 1024, "T": 1024 * 1024}
+    mult = 1
+    if v and v[-1] in scale:
+        mult = scale[v[-1]]
+        v = v[:-1]
+    try:
+        mb = int(float(v) * mult)
+    except ValueError:
+        raise DmxError(f"DMX_MEM_BUDGET_MB={raw!r}: expected MB, or a size such as 2048M or "
+                       "2G") from None
+    if mb < 0:
+        raise DmxError(f"DMX_MEM_BUDGET_MB={raw!r}: must not be negative")
+    return mb or None
+
+
 def memory_budget_bytes():
     """The job's memory limit, which the readers' and writers' buffers are sized to
     (dmx_io_set_memory_budget, batch_bytes_for_budget): DMX_MEM_BUDGET_MB when set, else the
-    cgroup's limit (v2 memory.max, v1 limit_in_bytes; a SLURM job's --mem: 02_cutadapt_loop.sh
-    runs under --mem=4G, 01_pychopper.sh under 2G), else None (no limit)."""
-    env = os.environ.get("DMX_MEM_BUDGET_MB", "").strip()
-    if env:
-        mb = int(env)
-        return (mb << 20) if mb > 0 else None
-    for lim in ("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory/memory.limit_in_bytes"):
-        v = _read_int(lim)
-        if v is not None and v < (1 << 60):
-            return v
-    return None
+    smallest finite limit of the process's memory cgroups, from its own up to the root (v2
+    memory.max, v1 limit_in_bytes; a SLURM job's --mem: 02_cutadapt_loop.sh runs under --mem=4G,
+    01_pychopper.sh under 2G), else None (no limit)."""
+    mb = _budget_env_mb()
+    if mb:
+        return mb << 20
+    lims = [v for _, lim, _ in _cgroup_memory_dirs()
+            for v in [_read_int(lim)] if v is not None and v < _NO_LIMIT]
+    return min(lims) if lims else None
 
 
 # fixed part of a process's peak: the HIP runtime holds ~0.9 GB of anonymous memory after its
@@ -294,9 +359,10 @@ def peak_rss_mb() -> float:
 
 
 def available_memory_bytes():
-    """Memory this process can still take: the smaller of MemAvailable (/proc/meminfo) and the
-    cgroup's limit minus its usage (v2 memory.max / memory.current, or v1 limit / usage; a
-    SLURM job's --mem lands there).  None when neither is readable."""
+    """Memory this process can still take: the smallest of MemAvailable (/proc/meminfo) and, for
+    every memory cgroup of the process from its own up to the root, the limit minus the usage
+    (v2 memory.max / memory.current, or v1 limit / usage; a SLURM job's --mem lands in a nested
+    one).  None when nothing is readable."""
     cands = []
     try:
         with open("/proc/meminfo") as fh:
@@ -306,16 +372,13 @@ def available_memory_bytes():
                     break
     except (OSError, ValueError, IndexError):
         pass
-    for lim, cur in (("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory.current"),
-                     ("/sys/fs/cgroup/memory/memory.limit_in_bytes",
-                      "/sys/fs/cgroup/memory/memory.usage_in_bytes")):
+    for _, lim, cur in _cgroup_memory_dirs():   # every cgroup up to the root: the tightest
         limit, used = _read_int(lim), _read_int(cur)
-        if limit is not None and used is not None and limit < (1 << 60):
+        if limit is not None and used is not None and limit < _NO_LIMIT:
             cands.append(max(0, limit - used))
-            break
-    env = os.environ.get("DMX_MEM_BUDGET_MB", "").strip()
-    if env and int(env) > 0:   # a stated budget: what this process does not hold yet
-        cands.append(max(0, (int(env) << 20) - _rss_bytes()))
+    mb = _budget_env_mb()
+    if mb:   # a stated budget: what this process does not hold yet
+        cands.append(max(0, (mb << 20) - _rss_bytes()))
     return min(cands) if cands else None
 
 

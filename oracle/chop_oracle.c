@@ -1,7 +1,7 @@
 /*
  * ORACLE — TEST INFRASTRUCTURE ONLY.  Plain-DP restatement of the primer-hit search of the
  * pychopper-style read reorientation (scripts/01_pychopper.sh:45-57: `pychopper -m edlib -b
- * M13_seqs_for_pychopper.fa -c M13_config_for_pychopper.txt -p ...`).  pychopper 2.7.10 and
+ * M13_seqs_for_pychopper.fa -c M13_config_for_pychopper.txt -p ...`).  pychopper v2.7.0 and
  * edlib are not vendored in /root/reference and not installed here: PARITY UNPINNED.  The
  * semantics below are the build's definition, restated from edlib's documented
  * HW ("infix") mode; oracle/chopper.py carries the segmentation / classification half.

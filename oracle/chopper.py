@@ -4,7 +4,7 @@ reorientation of scripts/01_pychopper.sh:45-57:
     pychopper -b M13_seqs_for_pychopper.fa -c M13_config_for_pychopper.txt -k LSK114 -Q 10
               -w RESCUED -u UNCLASS -l SHORT -S STATS -p -t 24 -m edlib IN > PASS
 
-pychopper 2.7.10 and edlib are not vendored in /root/reference and not installed here, and the
+pychopper v2.7.0 and edlib are not vendored in /root/reference and not installed here, and the
 reference holds no pychopper output: PARITY UNPINNED.  The semantics are the build's definition
 (DESIGN.md §8d), restated from edlib's HW ("infix") alignment mode and pychopper's documented
 options:
@@ -35,10 +35,10 @@ options:
             QC-passing reads (ties -> the smaller cutoff)
 
 [UNVERIFIED] choices (RULES below; the build implements the first reading of each, the drop-in
-and the kernels follow it): every choice pychopper 2.7.10's source would settle has a switch with
+and the kernels follow it): every choice pychopper v2.7.0's source would settle has a switch with
 one alternative reading, and tools/pychopper_cases.py holds one small case per switch whose
 outputs differ between the two readings (tests/test_chop.py checks that they do).
-tools/parity_vs_pychopper.sh runs those cases through a real pychopper 2.7.x wherever one is
+tools/parity_vs_pychopper.sh runs those cases through a real pychopper v2.7.0 wherever one is
 installed and diffs the outputs against the drop-in's: a DIFF names the switch to flip.
   tune_grid    autotune grid: linspace(0.1, 0.6, -L) | "0.0-0.5": linspace(0.0, 0.5, -L)
   tune_sample  autotune reads: the first -Y QC-passing reads | "stride": -Y reads spread evenly
@@ -49,6 +49,10 @@ installed and diffs the outputs against the drop-in's: a DIFF names the switch t
                most segments, then greatest summed length
   naming       segment records: "{start}:{stop}|{id} strand=+|-{comment}" | "nostrand":
                "{start}:{stop}|{id}{comment}" (the strand only implied by the orientation)
+Version target: pychopper v2.7.0, the version the reference pins (/root/reference/README.md:6).
+Neither its source nor its documentation is available offline in this image, so no reading
+above is settled by a v2.7.0 text: all five stay open switches until the parity hook runs on a
+real v2.7.0 (tools/parity_vs_pychopper.sh refuses any other version unless told otherwise).
 The `-k LSK114` kit is not a switch: with -b, -c, -m, -Q and -p given (01_pychopper.sh:45-57)
 the restatement reads it as unused, and the reference holds no LSK114 primer or parameter file
 that an alternative reading could draw on, so no case can separate it (parity unpinned).

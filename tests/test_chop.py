@@ -1,6 +1,6 @@
 """pychopper-style read reorientation (scripts/01_pychopper.sh:45-57): libdmx's `dmx_chop_*`
 (HIP) and the drop-in `bin/pychopper`, checked against the CPU restatement (oracle/chop_oracle.c
-+ oracle/chopper.py).  Parity unpinned: pychopper 2.7.10 / edlib are not installed and the
++ oracle/chopper.py).  Parity unpinned: pychopper v2.7.0 / edlib are not installed and the
 reference ships no pychopper output."""
 import os
 import subprocess
@@ -503,7 +503,7 @@ def test_unverified_pychopper_cases_tell_the_readings_apart():
     sample, autotune criterion, best-path score, record naming) has a case in
     tools/pychopper_cases.py whose outputs differ between the build's reading and the
     alternative one, so tools/parity_vs_pychopper.sh can settle each against a real
-    pychopper 2.7.x; flipping one switch leaves the other cases' distinctions to their own."""
+    pychopper v2.7.0; flipping one switch leaves the other cases' distinctions to their own."""
     pc = _pychopper_cases()
     assert set(v[0] for v in pc.CASES.values()) == set(ochop.DEFAULT_RULES)
     for name in pc.CASES:
@@ -519,7 +519,7 @@ def test_unverified_pychopper_cases_tell_the_readings_apart():
 def test_unverified_pychopper_cases_match_the_default_readings(tmp_path):
     """The drop-in (bin/pychopper) on every [UNVERIFIED] case: outputs and tuned cutoff equal
     the oracle's default readings (what tools/parity_vs_pychopper.sh compares with a real
-    pychopper 2.7.x)."""
+    pychopper v2.7.0)."""
     pc = _pychopper_cases()
     cases = tmp_path / "cases"
     pc.write(str(cases))

@@ -36,3 +36,53 @@ def test_cli_refuses_two_name_template_and_names_the_loop(tmp_path):
                        env=dict(os.environ, DMX_DAEMON="0"))
     assert r.returncode == 2
     assert "dmx-demux-loop" in r.stderr and "--template" in r.stderr
+
+
+def test_loop_closes_reader_and_contexts_when_setup_fails(tmp_path, monkeypatch):
+    """ADVICE r5: the reader (and its producer thread) is opened before the device contexts;
+    a failure in any later setup step (here the round-2 sink) must close the reader, every
+    sink already open and every context, not leave the reader inflating in the background."""
+    from dmx import lib, nio
+    fq = tmp_path / "reads.fastq"
+    fq.write_text("@r1\nACGTACGTACGT\n+\nIIIIIIIIIIII\n")
+    events = []
+
+    class FakeReader:
+        def __init__(self, *a, **k):
+            events.append("reader open")
+
+        def close(self):
+            events.append("reader close")
+
+    class FakeCtx:
+        def set_panel(self, *a, **k):
+            pass
+
+        def set_mode(self, *a):
+            pass
+
+        def close(self):
+            events.append("ctx close")
+
+    class FakeSink:
+        n = 0
+
+        def __init__(self, *a, **k):
+            FakeSink.n += 1
+            if FakeSink.n == 2:
+                raise lib.DmxError("sink failed")
+            events.append("sink open")
+
+        def close(self):
+            events.append("sink close")
+
+    monkeypatch.setattr(nio, "Reader", FakeReader)
+    monkeypatch.setattr(nio, "Sink", FakeSink)
+    monkeypatch.setattr(lib, "open_group", lambda devs: [FakeCtx(), FakeCtx()])
+    monkeypatch.setattr(loop, "_devices", lambda args: [0, 1])
+    import pytest
+    with pytest.raises(lib.DmxError, match="sink failed"):
+        loop.run([str(fq), "--outdir", str(tmp_path / "out")])
+    assert events.count("reader close") == 1
+    assert events.count("ctx close") == 2
+    assert events.count("sink close") == events.count("sink open") == 1

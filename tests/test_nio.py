@@ -797,3 +797,64 @@ def test_large_reads_take_the_parallel_paths(tmp_path):
     (tmp_path / "big.fastq.gz").write_bytes(c.compress(text) + c.flush())
     for name in ("big.fastq", "big.fastq.gz"):
         assert _read_all(tmp_path / name, batch_bytes=16 << 20, threads=4) == recs, name
+
+
+def _fake_cgroup(tmp_path, monkeypatch, proc_line, files):
+    root = tmp_path / "cg"
+    for rel, val in files.items():
+        p = root / rel
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(val)
+    proc = tmp_path / "proc_cgroup"
+    proc.write_text(proc_line + "\n")
+    monkeypatch.setattr(nio, "CGROUP_ROOT", str(root))
+    monkeypatch.setattr(nio, "PROC_CGROUP", str(proc))
+    monkeypatch.delenv("DMX_MEM_BUDGET_MB", raising=False)
+
+
+def test_memory_budget_from_a_nested_v2_cgroup(tmp_path, monkeypatch):
+    """a SLURM step without a cgroup namespace sits in a nested cgroup; its job's
+    --mem is the memory.max of an ancestor, which the mount root does not show."""
+    job = "system.slice/slurmstepd.scope/job_5"
+    _fake_cgroup(tmp_path, monkeypatch, f"0::/{job}/step_0/user/task_0", {
+        f"{job}/memory.max": str(4 << 30), f"{job}/memory.current": str(1 << 30),
+        f"{job}/step_0/memory.max": "max", f"{job}/step_0/memory.current": str(1 << 30),
+        f"{job}/step_0/user/task_0/memory.max": "max",
+        f"{job}/step_0/user/task_0/memory.current": str(1 << 30),
+        "memory.current": str(9 << 30)})
+    assert nio.memory_budget_bytes() == 4 << 30
+    assert nio.available_memory_bytes() <= 3 << 30
+    assert nio.batch_bytes_for_budget() == (int((4 << 30) - (1300 << 20)) // 20)
+
+
+def test_memory_budget_from_a_nested_v1_cgroup(tmp_path, monkeypatch):
+    _fake_cgroup(tmp_path, monkeypatch, "7:memory:/slurm/uid_1/job_7/step_batch", {
+        "memory/memory.limit_in_bytes": "9223372036854771712",   # v1 "unlimited"
+        "memory/slurm/uid_1/job_7/memory.limit_in_bytes": str(2 << 30),
+        "memory/slurm/uid_1/job_7/memory.usage_in_bytes": str(512 << 20),
+        "memory/slurm/uid_1/job_7/step_batch/memory.limit_in_bytes": "9223372036854771712"})
+    assert nio.memory_budget_bytes() == 2 << 30
+    assert nio.available_memory_bytes() <= (2 << 30) - (512 << 20)
+
+
+def test_memory_budget_without_limits(tmp_path, monkeypatch):
+    _fake_cgroup(tmp_path, monkeypatch, "0::/", {"memory.current": "1000"})
+    assert nio.memory_budget_bytes() is None
+
+
+@pytest.mark.parametrize("val,mb", [("2048", 2048), ("2048M", 2048), ("2G", 2048),
+                                    ("1.5G", 1536), ("4096MB", 4096), ("0", None), ("", None)])
+def test_memory_budget_env_sizes(monkeypatch, val, mb):
+    monkeypatch.setenv("DMX_MEM_BUDGET_MB", val)
+    if mb is None:
+        monkeypatch.setattr(nio, "PROC_CGROUP", "/nonexistent")
+        monkeypatch.setattr(nio, "CGROUP_ROOT", "/nonexistent")
+        assert nio.memory_budget_bytes() is None
+    else:
+        assert nio.memory_budget_bytes() == mb << 20
+
+
+def test_memory_budget_env_garbage_names_the_variable(monkeypatch):
+    monkeypatch.setenv("DMX_MEM_BUDGET_MB", "lots")
+    with pytest.raises(lib.DmxError, match="DMX_MEM_BUDGET_MB"):
+        nio.memory_budget_bytes()

@@ -1,6 +1,9 @@
 #!/bin/bash
 # Upstream parity hook for the reorientation step: runs
-# ONLY where a real pychopper 2.7.x is installed (not in this image: no network, no package).
+# ONLY where a real pychopper v2.7.0 is installed -- the version the reference pins
+# (/root/reference/README.md:6); not in this image: no network, no package.  Another version is
+# refused (a run on 2.7.10 would "confirm" behaviour the workflow never ran) unless
+# ALLOW_OTHER_PYCHOPPER=1, which runs it with a loud warning in front of every result line.
 # Writes one case per [UNVERIFIED] pychopper choice (tools/pychopper_cases.py: each case's
 # outputs differ between the build's reading and the alternative one), runs every case through
 # the real pychopper and through the drop-in (bin/pychopper), and diffs the four record outputs
@@ -9,8 +12,19 @@
 set -euo pipefail
 REAL=${REAL_PYCHOPPER:-$(command -v pychopper || true)}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-if [ -z "$REAL" ] || [[ "$REAL" == "$ROOT"/* ]] || ! "$REAL" --version 2>&1 | grep -q '2\.7\.'; then
-    echo "SKIPPED: no pychopper 2.7.x on PATH (set REAL_PYCHOPPER)"; exit 0
+if [ -z "$REAL" ] || [[ "$REAL" == "$ROOT"/* ]]; then
+    echo "SKIPPED: no pychopper on PATH (set REAL_PYCHOPPER)"; exit 0
+fi
+VER=$("$REAL" --version 2>&1 | head -1)
+WARN=""
+if ! grep -Eq '(^|[^0-9.])2\.7\.0($|[^0-9])' <<<"$VER"; then
+    if [ "${ALLOW_OTHER_PYCHOPPER:-0}" != 1 ]; then
+        echo "REFUSED: $VER is not pychopper v2.7.0, the version the reference pins (README.md:6);"
+        echo "         set ALLOW_OTHER_PYCHOPPER=1 to run it anyway (results are not a pin)"
+        exit 2
+    fi
+    WARN="WARNING (not v2.7.0: $VER) "
+    echo "${WARN}the reference pins pychopper v2.7.0; these results do not pin its behaviour"
 fi
 W=$(mktemp -d)
 python3 "$ROOT/tools/pychopper_cases.py" "$W/cases"
@@ -28,12 +42,12 @@ done
 while IFS=$'\t' read -r name _ _; do
     for k in pass rescued unclass short; do
         if ! cmp -s "$W/real/${name}_$k.fastq" "$W/dmx/${name}_$k.fastq"; then
-            echo "DIFF ($name switch): ${name}_$k.fastq"; fail=1
+            echo "${WARN}DIFF ($name switch): ${name}_$k.fastq"; fail=1
         fi
     done
     a=$(grep -i cutoff "$W/real/${name}_stats.out" | head -1 | awk '{print $NF}')
     b=$(grep -i cutoff "$W/dmx/${name}_stats.out" | head -1 | awk '{print $NF}')
-    if [ "$a" != "$b" ]; then echo "DIFF ($name switch): cutoff $a vs $b"; fail=1; fi
+    if [ "$a" != "$b" ]; then echo "${WARN}DIFF ($name switch): cutoff $a vs $b"; fail=1; fi
 done < "$W/cases/cases.tsv"
-[ $fail = 0 ] && echo "PARITY OK: every [UNVERIFIED] pychopper case identical to $("$REAL" --version 2>&1 | head -1)"
+[ $fail = 0 ] && echo "${WARN}PARITY OK: every [UNVERIFIED] pychopper case identical to $VER"
 exit $fail
