@@ -1,6 +1,6 @@
 """One small case per pychopper choice the oracle marks [UNVERIFIED] (oracle/chopper.py RULES,
 DESIGN.md §8d), built so that the build's reading and the alternative one give different
-outputs.  tools/parity_vs_pychopper.sh runs every case through a real pychopper 2.7.x (where one
+outputs.  tools/parity_vs_pychopper.sh runs every case through a real pychopper v2.7.0 (where one
 is installed) and through the drop-in (bin/pychopper) and diffs the outputs: a DIFF names the
 switch to flip.  tests/test_chop.py checks, with oracle/chopper.py switched to each alternative
 reading, that every case really tells the readings apart, and (GPU) that the drop-in gives the
