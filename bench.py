@@ -211,24 +211,60 @@ def pmc_traffic(workload: str, reads: int):
     return d[key]["bytes_per_launch"], d[key]["source"]
 
 
-# the two-round pipeline's kernels and the live stage events that time them (per round)
-KERNEL_STAGES = (("dmx::filter_kernel", "filter"), ("dmx::verify_kernel", "verify"),
-                 ("dmx::iscreen4_kernel", "screen"), ("dmx::wscan_kernel<true>", "wscan"),
-                 ("band_cand<0,3>+band_cand<4,5|7>+select_cand", "resolve"))
+# the two-round pipeline's kernels and the live stage events that time them (per round).  With
+# the piece screen the filter stage is the piece screen ("pieces": pscan +
+# pcompact, or the per-part pscreen) followed by the task-driven filter ("ftask"); without it,
+# the full-pass filter_kernel.
+KERNEL_STAGES_PIECES = (("pscan_kernel+pcompact_kernel", "pieces"), ("dmx::ftask_kernel", "ftask"),
+                        ("dmx::verify_kernel", "verify"), ("dmx::iscreen4_kernel", "screen"),
+                        ("dmx::wscan_kernel<true>", "wscan"),
+                        ("band_cand<0,3>+band_cand<4,5|7>+select_cand", "resolve"))
+KERNEL_STAGES_FULL = (("dmx::filter_kernel", "filter"), ("dmx::verify_kernel", "verify"),
+                      ("dmx::iscreen4_kernel", "screen"), ("dmx::wscan_kernel<true>", "wscan"),
+                      ("band_cand<0,3>+band_cand<4,5|7>+select_cand", "resolve"))
 PMC_NAMES = {"filter": ["filter_kernel"], "verify": ["verify_kernel"],
+             "pieces": ["pscan_kernel<1>", "pscan_kernel<2>", "pscan_kernel<4>", "pcompact_kernel",
+                        "pscreen_kernel<1>", "pscreen_kernel<2>", "pscreen_kernel<4>",
+                        "read_view_kernel", "read_item_kernel"],
+             "ftask": ["ftask_kernel"],
              "screen": ["iscreen4_kernel", "iscreen_kernel"], "wscan": ["wscan_kernel<true>"],
              "resolve": ["band_cand_kernel<0, 3>", "band_cand_kernel<4, 5>",
                          "band_cand_kernel<4, 7>", "select_cand_kernel"]}
+# stages timed by HIP events around exactly one kernel (candidates for the roofline's kernel)
+SINGLE_KERNEL = {"filter": "filter_kernel", "ftask": "ftask_kernel", "verify": "verify_kernel",
+                 "screen": "iscreen4_kernel", "wscan": "wscan_kernel<true>"}
 
 
-def kernel_table(workload: str, reads: int, stage: dict, K: int, step_ms: float):
+def stage_split(stage: dict) -> dict:
+    """stage totals with the piece screen's share split out: ftaskN = filterN - piecesN."""
+    out = dict(stage)
+    for r in (0, 1):
+        out[f"ftask{r}"] = max(0.0, stage[f"filter{r}"] - stage.get(f"pieces{r}", 0.0))
+    return out
+
+
+def pmc_kernel_bytes(workload: str, reads: int, kernel: str):
+    """Mean HBM bytes per launch of `kernel` in the committed PMC table (FETCH_SIZE x 2 +
+    WRITE_SIZE, separate passes; profiles/kernel_pmc.json), or None."""
+    pmc = pmc_table(workload, reads)
+    launches = (pmc or {}).get("kernels", {}).get(kernel, [])
+    if not launches:
+        return None, None
+    return (sum(e["hbm_bytes"] for e in launches) / len(launches),
+            f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), {kernel}, mean of the "
+            f"{len(launches)} launches of one step; FETCH_SIZE x2 (gfx950 wide-read correction); "
+            + pmc["source"])
+
+
+def kernel_table(workload: str, reads: int, stage: dict, K: int, step_ms: float,
+                 stages=KERNEL_STAGES_FULL):
     """Per-kernel live time (HIP events around each stage of each round) with, where a committed
     rocprofv3 PMC table exists for this exact workload (profiles/kernel_pmc.json, written by
     tools/kernel_table_from_pmc.py), the VALU issue rate and HBM bytes of the same launches:
     instructions and bytes per launch are properties of the workload, the time is this run's."""
     pmc = pmc_table(workload, reads)
     out = {}
-    for name, st in KERNEL_STAGES:
+    for name, st in stages:
         ms = [stage[f"{st}{r}"] / K for r in (0, 1)]
         ent = {"ms_per_step": round(sum(ms), 3), "ms_per_round": [round(x, 3) for x in ms],
                "share_of_step": round(sum(ms) / step_ms, 4)}
@@ -366,31 +402,51 @@ def chop_line(args, world, K, value, elapsed, ms, lengths, n_hits, n_segs, cutof
 
 
 def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s,
-                   clusters, windows, windows_raw, resolved, traces):
-    # roofline of the dominant kernel: the shared-suffix filter (reads every base of every
-    # view; two launches per step, round 1 over the reads, round 2 over the round-1 tails)
-    filt_ms = (stage["filter0"] + stage["filter1"]) / (2 * K)
+                   clusters, windows, windows_raw, resolved, traces, filter_tasks):
+    st = stage_split(stage)
+    pieces = st.get("pieces0", 0.0) > 0 or st.get("pieces1", 0.0) > 0
+    stages = KERNEL_STAGES_PIECES if pieces else KERNEL_STAGES_FULL
     res = ctx.fetch()
     m2 = res["bin1"] >= 0
     n2 = int(m2.sum())
     len2 = (lengths[m2] - res["m1_rstop"][m2]).astype(np.int64)
-    # roofline.achieved: SURVEY.md §8(d)'s B(read) over the views each filter launch scans
-    # (round 1: every read; round 2: the round-1-trimmed tails), averaged over the two launches
+    # roofline.achieved: SURVEY.md §8(d)'s B(read) over the views each launch of the kernel
+    # processes (round 1: every read; round 2: the round-1-trimmed tails), averaged over the
+    # round-1 and round-2 launches, / that kernel's live average launch time (HIP events)
     sb0, sb1 = survey_bytes(lengths), survey_bytes(len2)
     alg_bytes = (sb0 + sb1) / 2
-    achieved = alg_bytes / (filt_ms / 1e3) / 1e9
-    # this build's layout (1-bit mask, 40-B windows): a second figure, not the roofline's
-    lay0 = filter_layout_bytes(lengths, int(windows_raw[0] / K))
-    lay1 = filter_layout_bytes(len2, int(windows_raw[1] / K))
-    layout_bytes = (lay0 + lay1) / 2
     step_ms = elapsed / K * 1e3
     step_bytes = survey_bytes(lengths)   # §8(d): round 2 reuses the resident read
-    traffic, traffic_src = pmc_traffic(args.workload, args.reads)
+    # the dominant kernel: the single-kernel stage with the largest share of the step
+    single = [k for k in SINGLE_KERNEL if f"{k}0" in st and (k != "filter" or not pieces)
+              and (k != "ftask" or pieces)]
+    dom = max(single, key=lambda k: st[f"{k}0"] + st[f"{k}1"])
+    dom_kernel = SINGLE_KERNEL[dom]
+    dom_ms = (st[f"{dom}0"] + st[f"{dom}1"]) / (2 * K)
+    achieved = alg_bytes / (dom_ms / 1e3) / 1e9
+    traffic, traffic_src = pmc_kernel_bytes(args.workload, args.reads, dom_kernel)
+    if traffic is None and dom_kernel == "filter_kernel":
+        traffic, traffic_src = pmc_traffic(args.workload, args.reads)
+    vi = pmc_valu_insts(args.workload, args.reads, dom_kernel)
+    dom_rate = vi * 64 / ((st[f"{dom}0"] + st[f"{dom}1"]) / K / 1e3) if vi else None
     A0, A1 = ctx.panel_sizes
-    cols = float(lengths.sum()) * 2 + float(len2.sum()) * 2     # filter columns, both strands
-    col_rate = cols / ((stage["filter0"] + stage["filter1"]) / K / 1e3)
-    vi = pmc_valu_insts(args.workload, args.reads, "filter_kernel")
-    ops_col = vi * 64 / cols if vi else None
+    read_stream = None
+    if pieces:   # the piece screen reads every base of every view (the old filter's role)
+        pm = (st["pieces0"] + st["pieces1"]) / (2 * K)
+        ps_traffic = None
+        tr = [pmc_kernel_bytes(args.workload, args.reads, k)[0]
+              for k in ("pscan_kernel<2>", "pscan_kernel<1>", "pscan_kernel<4>")]
+        tr = [t for t in tr if t]
+        if tr:
+            ps_traffic = tr[0]
+        read_stream = {
+            "kernel": "dmx::pscan_kernel + dmx::pcompact_kernel (the piece screen: every base "
+                      "of every view, DESIGN.md §3.12)",
+            "avg_launch_ms": round(pm, 3), "achieved": round(alg_bytes / (pm / 1e3) / 1e9, 3),
+            "frac": round(alg_bytes / (pm / 1e3) / 1e9 / HBM_PEAK_GBS, 6),
+            "pscan_traffic_bytes_per_launch": ps_traffic,
+            "what": "the same §8(d) bytes over the piece screen stage's live time (HIP events "
+                    "from the round start to the filter tasks; its memsets included)"}
     return {
         "metric": METRIC, "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world,
         "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 3),
@@ -410,41 +466,29 @@ def two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, 
                      "algorithmic_bytes_rule": "SURVEY.md §8(d) B(read) = ceil(L/4) + 8 + "
                                                "ceil(L/64) + 24 over the launch's views, mean "
                                                "of the round-1 and round-2 launches",
-                     "layout_bytes_per_launch": round(layout_bytes),
-                     "layout_bytes_rule": "this build's layout: ceil(L/4) + ceil(L/8) (1-bit "
-                                          "mask) + 12 per view + 40 B per emitted window",
                      "traffic_over_algorithmic": (round(traffic / alg_bytes, 3)
                                                   if traffic else None),
-                     "traffic_over_layout": (round(traffic / layout_bytes, 3)
-                                             if traffic else None),
                      "per_step": {"bytes": round(step_bytes), "ms": round(step_ms, 3),
                                   "achieved_gbs": round(step_bytes / (step_ms / 1e3) / 1e9, 3),
                                   "frac": round(step_bytes / (step_ms / 1e3) / 1e9
                                                 / HBM_PEAK_GBS, 6),
                                   "what": "§8(d) bytes of every read once per step (round 2 "
                                           "reuses the resident read) / ms_per_step"},
-                     "kernel": "dmx::filter_kernel", "avg_launch_ms": round(filt_ms, 3),
-                     "share_of_step": round(2 * filt_ms / (elapsed / K * 1e3), 4),
-                     "note": "the dominant kernel (largest share of the step, see 'kernels'); "
-                             "a bit-vector scan, VALU-bound by construction (DESIGN.md §5): "
-                             "roofline.valu gives its issue rate against the VALU peak at the "
-                             "clock it ran at",
-                     "valu": valu_roof(col_rate * ops_col if ops_col else None,
-                                       pmc_clock(args.workload, args.reads, "filter_kernel"),
-                                       "dmx::filter_kernel, both rounds")},
-        "valu": {"filter_columns_per_s": col_rate,
-                 "filter_lane_ops_per_column": ops_col,
-                 "filter_lane_ops_per_s": col_rate * ops_col if ops_col else None,
-                 "frac_of_measured_ceiling": (col_rate * ops_col / VALU_CEILING
-                                              if ops_col else None),
-                 "measured_ceiling_lane_ops_per_s": VALU_CEILING,
-                 "nominal_peak_lane_ops_per_s": VALU_PEAK_TOPS * 1e12,
-                 "source": "ops/column = SQ_INSTS_VALU x 64 of both PMC'd filter launches "
-                           "(profiles/kernel_pmc.json) / their columns; ceiling = "
-                           + VALU_CEILING_WHAT},
-        "kernels": kernel_table(args.workload, args.reads, stage, K, elapsed / K * 1e3),
-        "stage_ms_per_step": {k: round(v / K, 3) for k, v in stage.items()},
+                     "kernel": "dmx::" + dom_kernel, "avg_launch_ms": round(dom_ms, 3),
+                     "share_of_step": round(2 * dom_ms / step_ms, 4),
+                     "note": "the dominant kernel (the single-kernel stage with the largest share "
+                             "of the step, see 'kernels'); integer/bit work, VALU- or "
+                             "latency-bound by construction (DESIGN.md §5): roofline.valu gives "
+                             "its issue rate against the VALU peak at the clock it ran at",
+                     "valu": valu_roof(dom_rate,
+                                       pmc_clock(args.workload, args.reads, dom_kernel),
+                                       f"dmx::{dom_kernel}, both rounds"),
+                     "read_stream": read_stream},
+        "kernels": kernel_table(args.workload, args.reads, st, K, elapsed / K * 1e3, stages),
+        "stage_ms_per_step": {k: round(v / K, 3) for k, v in st.items()},
         "clusters_per_step": (clusters / K).tolist(),
+        "filter_tasks_per_step": (filter_tasks / K).tolist(),
+        "filter_windows_raw_per_step": (windows_raw / K).tolist(),
         "filter_windows_per_step": (windows / K).tolist(),
         "resolved_clusters_per_step": (resolved / K).tolist(),
         "tracebacks_per_step": (traces / K).tolist(),
@@ -630,6 +674,7 @@ def main():
     windows_raw = np.zeros(2)
     resolved = np.zeros(2)
     traces = np.zeros(2)
+    filter_tasks = np.zeros(2)
     barrier_sync()
     t = time.perf_counter()
     counts = None
@@ -647,6 +692,7 @@ def main():
         windows_raw += np.array(st["windows_raw"], dtype=np.float64)
         resolved += np.array(st["resolved"], dtype=np.float64)
         traces += np.array(st["traces"], dtype=np.float64)
+        filter_tasks += np.array(st["filter_tasks"], dtype=np.float64)
         flags |= st["flags"]
         counts = allreduce_counts()
         step_wall.append((time.perf_counter() - ts) * 1e3)
@@ -666,7 +712,7 @@ def main():
         out = linked_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s)
     else:
         out = two_round_line(args, world, K, value, elapsed, stage, lengths, ctx, counts, gen_s,
-                             clusters, windows, windows_raw, resolved, traces)
+                             clusters, windows, windows_raw, resolved, traces, filter_tasks)
     out["step_wall_ms"] = [round(x, 3) for x in step_wall]   # this rank's, for outliers
     pcie = None
     if host_batch is not None and not args.no_pcie:

@@ -20,7 +20,10 @@ import json
 import os
 import sys
 
-KERNELS = ("filter_kernel", "verify_kernel", "iscreen_kernel", "iscreen4_kernel",
+KERNELS = ("filter_kernel", "pscan_kernel<1>", "pscan_kernel<2>", "pscan_kernel<4>",
+           "pcompact_kernel", "pscreen_kernel<1>", "pscreen_kernel<2>", "pscreen_kernel<4>",
+           "ftask_kernel", "read_item_kernel", "read_view_kernel",
+           "verify_kernel", "iscreen_kernel", "iscreen4_kernel",
            "wscan_kernel<true>", "band_cand_kernel<0, 3>", "band_cand_kernel<4, 5>",
            "band_cand_kernel<4, 7>", "select_cand_kernel", "finalize0_kernel", "finalize1_kernel",
            "chop_kernel", "scan_kernel<true>", "finalize0_linked_kernel",
