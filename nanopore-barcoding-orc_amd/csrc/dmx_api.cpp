@@ -336,8 +336,8 @@ void dmx_close(dmx_ctx* c) {
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
                     c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_tasks, c->d_counters, c->d_shard,
                     c->d_counts,    c->d_panel[0],  c->d_panel[1], c->d_pieces[0], c->d_pieces[1],
-                    c->d_ftask, c->d_flat_bad, c->d_sbf, c->d_read_item, c->d_cells[0],
-                    c->d_cells[1]};
+                    c->d_ftask, c->d_pieces_flat, c->d_cells[0], c->d_cells[1], c->d_cells[2],
+                    c->d_cells[3]};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (int r = 0; r < 2; ++r)
@@ -374,6 +374,7 @@ int dmx_set_mode(dmx_ctx* c, int mode) {
         return DMX_E_INVALID;
     }
     c->mode = mode;
+    ++c->panel_gen;
     return DMX_OK;
 }
 
@@ -752,6 +753,7 @@ static int set_panel_impl(dmx_ctx* c, int round, const char* const* seqs, const 
     const int brc = build_panel(c, seqs, lens, wheres, n, max_errors, min_overlap, flags, hp, dp);
     if (brc) return brc;
     c->panel[round] = hp;
+    ++c->panel_gen;
     c->ring_small[round] = hp.ring_small;
     c->band_ok[round] = true;
     int kkmax = 0;
@@ -871,7 +873,6 @@ int load_impl(dmx_ctx* c, const uint32_t* seq2b, const MaskSrc& mask, const uint
     }
     c->n_reads = n_reads;
     c->n_words = n_words;
-    c->flat_dirty = true;
     CK(hipMemcpyAsync(c->d_seq, seq2b, n_words * 4, hipMemcpyHostToDevice, c->stream));
     if ((rc = upload_mask(c, mask, 0, nmw, c->stream))) return rc;
     if (n_reads) {
@@ -1153,7 +1154,6 @@ void swap_inputs(Ctx* c) {
     std::swap(c->d_exc, c->alt.exc);
     std::swap(c->exc_cap, c->alt.exc_cap);
     std::swap(c->n_words, c->alt.n_words);
-    c->flat_dirty = true;
     c->d_seq = c->d_seq_alloc + kGuardWords;
     c->d_nmask = c->d_nmask_alloc + kGuardWords;
 }

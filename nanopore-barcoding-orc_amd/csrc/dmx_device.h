@@ -137,11 +137,13 @@ constexpr int kPieceBitmapWords = 1 << (2 * kPieceK - 5);
 // An entry of the piece table (one per (piece, sampled offset)), packed in 64 bits: the piece's
 // 2-bit codes in view-0 read order (nt i at bits 2i; orientation 1: the reverse complement),
 // its length, orientation, the sampled 8-mer's offset inside it, and the range of alignment end
-// columns after the copy (dlo, dhi; + 128).
+// columns after the copy (dlo, dhi; + 128); the flat scan's combined table tags each entry with
+// its round (bit 56).
 __host__ __device__ inline uint64_t piece_entry(uint32_t val, int len, int o, int off, int dlo,
-                                                int dhi) {
+                                                int dhi, int round = 0) {
     return (uint64_t)val | ((uint64_t)len << 32) | ((uint64_t)o << 37) | ((uint64_t)off << 38) |
-           ((uint64_t)(dlo + 128) << 40) | ((uint64_t)(dhi + 128) << 48);
+           ((uint64_t)(dlo + 128) << 40) | ((uint64_t)(dhi + 128) << 48) |
+           ((uint64_t)round << 56);
 }
 
 struct DevPieces {
@@ -176,10 +178,12 @@ struct FTask {
 };
 static_assert(sizeof(FTask) == 32, "FTask layout");
 
-// Flat piece scan: a sorted, non-overlapping batch is scanned as one stream of
-// 4096-nt superblocks.  sbf[b] = the first read whose end lies past nt 4096 b; cell bitmaps: one
-// bit per 16 nt of the packed batch and per view orientation (cells never hold two reads of a
-// dmx_pack layout; when they do, a mark only adds filter work).
+// Flat piece scan: the packed batch is scanned once per exec as one stream of
+// 4096-nt superblocks against the combined table of every flat round.  Marks live in batch nt
+// coordinates, independent of reads and views: cell bitmap 2 r + t holds one bit per 16 nt for
+// the copies of round r's pieces on strand t, and a view of strand t reads bitmap 2 r + t over its
+// own nt range (a cell shared with a neighbouring read, or a copy across a read boundary, only
+// adds filter work).
 constexpr int kSuperNt = 4096;   // nt per wave step: 64 lanes x 64 nt
 constexpr int kCellGuardWords = 4;   // zero words before / after each cell bitmap
 constexpr int kCandStageCap = 128; // per candidate list

@@ -113,16 +113,18 @@ struct Ctx {
     size_t task_cap = 0;
     FTask* d_ftask = nullptr;            // piece screen -> filter tasks
     size_t ftask_cap = 0;
-    // flat piece scan (prepare_flat): sortedness flag, superblock index, read -> item, cells
-    uint32_t* d_flat_bad = nullptr;
-    uint32_t* d_sbf = nullptr;
-    size_t sbf_cap = 0, n_sb = 0;
-    bool flat_dirty = true;              // a new batch (or input set) since the index was built
-    bool flat_ok_launch = false;         // this exec launches the flat scan
-    uint32_t* d_read_item = nullptr;
-    size_t read_item_cap = 0;
-    uint32_t* d_cells[2] = {nullptr, nullptr};
-    size_t cells_cap = 0, cells_words = 0;
+    // flat piece scan (prepare_flat): one scan of the batch against the flat rounds' combined
+    // table marks cells[2 r + strand] for every flat round r
+    DevPieces* d_pieces_flat = nullptr;
+    int flat_rounds = 0;                 // bit r: round r's screen is the flat scan (this exec)
+    int flat_want = 0;                   // the rounds the combined table was built for
+    int flat_step = 0;                   // its sampling stride (0: no table)
+    size_t flat_lds = 0;                 // its LDS image
+    uint64_t panel_gen = 1;              // bumped by set_panel / set_mode
+    uint64_t flat_gen = 0;               // panel_gen the combined table was built for
+    uint32_t* d_cells[4] = {nullptr, nullptr, nullptr, nullptr};
+    size_t cells_cap[4] = {0, 0, 0, 0};
+    size_t cells_words = 0;
     bool no_screen = false;              // DMX_NO_SCREEN=1: every window runs every adapter
     bool screen_v1 = false;              // DMX_SCREEN_V1=1: one lane per (window, adapter) screen
     size_t n_counts = 0;

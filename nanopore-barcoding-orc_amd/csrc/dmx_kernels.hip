@@ -6,7 +6,12 @@
 // oracle/cutadapt_oracle.c; design and exactness argument in DESIGN.md §3.
 //
 // Per round: scan -> resolve -> select -> finalize, all on one HIP stream, no host round trip.
+#include <algorithm>
+#include <cstring>
+#include <memory>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "dmx_device.h"
 #include "dmx_internal.h"
@@ -57,14 +62,11 @@ struct RoundArgs {
     FTask* ftask;                // piece screen -> filter tasks
     uint32_t* ftask_count;       // [kShards]: shard s at ftask + s * ftask_scap
     uint32_t ftask_scap;
-    // flat piece scan (sorted, non-overlapping batches; *flat_bad != 0: the per-part screen)
-    const uint32_t* flat_bad;
-    const uint32_t* sbf;         // [nsb + 1] first read ending past each superblock's start
-    uint32_t nsb;
+    // flat piece scan: cell bitmaps [2 round + strand], kCellGuardWords words before index 0
     uint32_t n_words;
-    const uint32_t* read_item;   // round 2: read -> item (~0 = none)
-    uint32_t* cells[2];          // per orientation, kCellGuardWords words before index 0
-    uint32_t n_reads;
+    uint32_t nsb;                // 4096-nt superblocks of the packed batch
+    int32_t round;
+    uint32_t* cells[4];
 };
 
 // DESIGN.md §3.10.  The filter, the prefix verification and the index screen are necessary
@@ -1708,7 +1710,7 @@ ps_lookups(const uint32_t* bm, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w
            uint32_t w5) {
     using HitT = typename std::conditional<S == 1, uint64_t, uint32_t>::type;
     HitT hits = 0;
-#if defined(DMX_PS_AB) && DMX_PS_AB >= 2   // timing A/B only (results invalid): no lookups
+#if defined(DMX_PS_AB) && DMX_PS_AB == 2   // timing A/B only (results invalid): no lookups
     asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4), "v"(w5));
 #else
     const uint32_t wv6[6] = {w0, w1, w2, w3, w4, w5};
@@ -1720,7 +1722,7 @@ ps_lookups(const uint32_t* bm, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w
         hits |= (HitT)__builtin_amdgcn_ubfe(word, K & 31u, 1) << q;
     }
 #endif
-#if defined(DMX_PS_AB) && DMX_PS_AB >= 1   // timing A/B only: no candidate checks
+#if defined(DMX_PS_AB) && (DMX_PS_AB == 1 || DMX_PS_AB == 2)   // timing A/B: no checks
     asm volatile("" ::"v"(hits));
     hits = 0;
 #endif
@@ -1740,7 +1742,6 @@ ps_lookups(const uint32_t* bm, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w
 template <int S>
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_PIECE_WAVES))) void pscreen_kernel(RoundArgs R) {
     static_assert(S == 1 || S == 2 || S == 4, "sampling stride: 64 positions per step");
-    if (R.flat_bad && *R.flat_bad == 0u) return;   // the flat scan serves this batch
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     __shared__ uint32_t s_pre[kPsItemsPerBlock + 1];
     __shared__ uint32_t s_sc[kScanBlock];
@@ -1903,115 +1904,94 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
 }
 
 // ---------------------------------------------------------------------------------------------
-// Flat piece scan, for batches whose reads are sorted and do not overlap (every
-// dmx_pack layout): waves stride over 4096-nt superblocks of the packed batch, lane l takes nt
-// [4096 b + 64 l, + 64) with one 16-B load (neighbours' words by lane shuffles), so every lane
-// does the same work and the loads are coalesced.  Sampled 8-mer hits go to a per-wave LDS queue
-// and are checked 64 at a time, one per lane: the read holding the copy (superblock index +
-// binary search over read ends), its view (round 2: the read's item), the copy against the
-// entry, then the cells of the view where an alignment containing the copy can end are marked in
-// the orientation's cell bitmap (global atomics).  pcompact_kernel turns the bitmaps into tasks.
+// Flat piece scan: once per exec, waves stride over 4096-nt superblocks of the
+// packed batch, lane l takes nt [4096 b + 64 l, + 64) with one 16-B load (neighbours' words by lane
+// shuffles), so every lane does the same work and the loads are coalesced.  The table is the
+// combined table of every flat round.  The superblock's words are also kept in LDS; its sampled
+// 8-mer hits are numbered lane by lane (a wave prefix sum) and checked 64 at a time, one per lane:
+// the copy against each entry of the 8-mer (codes from LDS), then the nt where an alignment
+// containing the copy can end are marked in the cell bitmap of the entry's round and copy strand
+// (global atomics).  A lane's hits take adjacent check lanes, so the pieces of one adapter copy,
+// which mark the same cells, sit side by side: a mark its left neighbour already makes is
+// dropped.  No read or view is looked up: the marks are positions of the batch, and
+// pcompact_kernel reads each view's own range of them.
 // ---------------------------------------------------------------------------------------------
-constexpr int kPsQueue = 128;   // per-wave candidate queue (<= 63 left + 64 pushed)
+constexpr int kSbWords = kSuperNt / 16 + 8;   // LDS copy of a superblock: 4 words before, 4 after
 
-// index of the read holding nt X (-1: none), searching the superblock's read range
-__device__ __forceinline__ int flat_read(const RoundArgs& R, uint64_t X) {
-    const uint32_t sb = (uint32_t)(X / kSuperNt);
-    uint32_t lo = R.sbf[sb], hi = R.sbf[min(sb + 1u, R.nsb)];   // first read ending past X in
-    hi = min(hi + 1u, R.n_reads);                               // [lo, hi]
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (R.offs[mid] + R.lens[mid] > X) hi = mid;
-        else lo = mid + 1;
-    }
-    if (lo >= R.n_reads || R.offs[lo] > X || R.offs[lo] + R.lens[lo] <= X) return -1;
-    return (int)lo;
-}
-
-// Check one queued sampled 8-mer (global nt X) against its entries and mark cells.
-__device__ __forceinline__ void flat_check(const RoundArgs& R, const PsTables& tb, uint64_t X,
-                                           int no) {
-    // codes of nt [X - 3, X + 29): every copy sampled at X starts at X - off, off <= 3
-    const uint64_t cw = ((uint64_t)code32(R.pk, (int64_t)X + 13) << 32) |
-                        (uint64_t)code32(R.pk, (int64_t)X - 3);
-    const uint32_t kr = ps_key(tb, (uint32_t)(cw >> 6) & 0xFFFFu);
-    const int r = flat_read(R, X);
-    if (r < 0) return;
-    const uint64_t off_r = R.offs[r];
-    const int nr = (int)R.lens[r];
-    int sg = 0, st = 0, l = nr;   // the item's view (round 1: the whole read, strand 0)
-    if (R.items) {
-        const uint32_t it = R.read_item[r];
-        if (it == ~0u) return;
-        const ItemView v = R.items[it];
-        sg = v.strand;
-        st = (int)v.start;
-        l = (int)v.len;
-    }
-    const int e0 = (int)(kr & 0xFFFFu), e1 = e0 + (int)(kr >> 16);
-    for (int e = e0; e < e1; ++e) {
-        const uint64_t ev = tb.ent[e];
-        const int len = (int)((ev >> 32) & 31u);
-        const int off = (int)((ev >> 38) & 3u);
-        const uint32_t msk = len >= 16 ? ~0u : ((1u << (2 * len)) - 1u);
-        if (((uint32_t)(cw >> (2 * (3 - off))) & msk) != (uint32_t)ev) continue;
-        const int tau = (int)((ev >> 37) & 1u);   // 1: the adapter reads reverse complemented
-        const int o = tau ^ sg;                   // the view that holds it forward
-        if (o >= no) continue;
-        const int G = (int)((int64_t)X - off - (int64_t)off_r);   // copy start in the read
-        if (G < 0 || G + len > nr) continue;
-        const int so = o ? nr - st - l : st;      // that view's start on strand tau
-        const int g = tau ? nr - so - G - len : G - so;            // copy start in the view
-        if (g < 0 || g + len > l) continue;
-        const int dlo = (int)((ev >> 40) & 255u) - 128;
-        const int dhi = (int)((ev >> 48) & 255u) - 128;
-        const int plo = max(g + len + dlo - 1, 0), phi = min(g + len + dhi - 1, l - 1);
-        if (plo > phi) continue;
-        // view positions -> nt of the read (strand tau) -> cells
-        int64_t nlo, nhi;
-        if (tau == 0) {
-            nlo = (int64_t)off_r + so + plo;
-            nhi = (int64_t)off_r + so + phi;
-        } else {
-            nlo = (int64_t)off_r + nr - 1 - so - phi;
-            nhi = (int64_t)off_r + nr - 1 - so - plo;
+// Check one sampled 8-mer (batch nt X; cw = codes of nt [X - 3, X + 29)) against its entries and
+// mark cells.  A copy of a strand-0 piece at nt [x, x + len) ends alignments of a strand-0 view at
+// nt x + len - 1 + [dlo, dhi]; a copy of a strand-1 piece (the reverse complement) ends them, in a
+// strand-1 view that walks the batch backwards, at nt x - [dlo, dhi].  Every lane of the wave
+// calls it (valid: the lane holds a hit).
+__device__ __forceinline__ void flat_check(const RoundArgs& R, const PsTables& tb, uint64_t cw,
+                                           uint64_t X, bool valid) {
+    uint32_t* p1 = nullptr;   // the lane's first mark (deduplicated against the left lane's)
+    uint32_t b1 = 0;
+    if (valid) {
+        const uint32_t kr = ps_key(tb, (uint32_t)(cw >> 6) & 0xFFFFu);
+        const int64_t last = (int64_t)R.n_words * 16 - 1;
+        const int e0 = (int)(kr & 0xFFFFu), e1 = e0 + (int)(kr >> 16);
+        for (int e = e0; e < e1; ++e) {
+            const uint64_t ev = tb.ent[e];
+            const int len = (int)((ev >> 32) & 31u);
+            const int off = (int)((ev >> 38) & 3u);
+            const uint32_t msk = len >= 16 ? ~0u : ((1u << (2 * len)) - 1u);
+            if (((uint32_t)(cw >> (2 * (3 - off))) & msk) != (uint32_t)ev) continue;
+            const int tau = (int)((ev >> 37) & 1u);   // 1: the adapter reads reverse complemented
+            const int dlo = (int)((ev >> 40) & 255u) - 128;
+            const int dhi = (int)((ev >> 48) & 255u) - 128;
+            const int64_t x = (int64_t)X - off;       // the copy's first nt
+            int64_t nlo = tau ? x - dhi : x + len + dlo - 1;
+            int64_t nhi = tau ? x - dlo : x + len + dhi - 1;
+            nlo = nlo < 0 ? 0 : nlo;
+            nhi = nhi > last ? last : nhi;
+            if (nlo > nhi) continue;
+            uint32_t* cells = R.cells[2 * (int)((ev >> 56) & 1u) + tau];
+            for (int64_t c = nlo >> 4; c <= (nhi >> 4);) {   // one atomic per bitmap word
+                const int64_t w = c >> 5;
+                const int64_t cend = min(nhi >> 4, (w << 5) + 31);
+                const uint32_t bits = (uint32_t)((((2ull << (cend - c)) - 1ull)) << (c & 31));
+                if (!p1) {
+                    p1 = cells + w;
+                    b1 = bits;
+                } else {
+#if defined(DMX_PS_AB) && DMX_PS_AB == 3   // timing A/B only: no marks
+                    asm volatile("" ::"v"(bits), "v"(cells + w));
+#else
+                    atomicOr(cells + w, bits);
+#endif
+                }
+                c = cend + 1;
+            }
         }
-        uint32_t* cells = R.cells[o];
-        for (int64_t c = nlo >> 4; c <= (nhi >> 4);) {   // one atomic per bitmap word
-            const int64_t w = c >> 5;
-            const int64_t cend = min(nhi >> 4, (w << 5) + 31);
-            const uint32_t bits = (uint32_t)((((2ull << (cend - c)) - 1ull)) << (c & 31));
-            atomicOr(cells + w, bits);
-            c = cend + 1;
-        }
+    }
+    const uint64_t pa = (uint64_t)p1;
+    const uint64_t pl = ((uint64_t)__shfl_up((uint32_t)(pa >> 32), 1u, 64) << 32) |
+                        (uint64_t)__shfl_up((uint32_t)pa, 1u, 64);
+    const uint32_t bl = __shfl_up(b1, 1u, 64);
+    const bool dup = (threadIdx.x & 63u) != 0u && pl == pa && (bl & b1) == b1;
+    if (p1 && !dup) {
+#if defined(DMX_PS_AB) && DMX_PS_AB == 3
+        asm volatile("" ::"v"(b1), "v"(p1));
+#else
+        atomicOr(p1, b1);
+#endif
     }
 }
 
 template <int S>
 __global__ __launch_bounds__(kScanBlock) void pscan_kernel(RoundArgs R) {
     static_assert(S == 1 || S == 2 || S == 4, "sampling stride: 64 positions per step");
-    if (*R.flat_bad) return;                          // the per-part screen serves this batch
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-    __shared__ uint64_t s_q[kScanBlock / 64][kPsQueue];
+    __shared__ __attribute__((aligned(16))) uint32_t s_sb[kScanBlock / 64][kSbWords];
+    __shared__ uint16_t s_q[kScanBlock / 64][64];
     const PsTables tb = ps_load_tables(R.pieces, s_dyn);
     __syncthreads();
     const int lane = (int)(threadIdx.x & 63u);
-    uint64_t* const q = s_q[threadIdx.x >> 6];
-    const int no = R.panel->n_orient;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t qn = 0;                                  // wave-uniform queue count
+    uint32_t* const sbw = s_sb[threadIdx.x >> 6];   // [4 + k]: word k of the superblock
+    uint16_t* const q = s_q[threadIdx.x >> 6];
     const uint4* sp = reinterpret_cast<const uint4*>(R.pk.seq);
     const uint32_t nw = gridDim.x * (kScanBlock / 64);
-    const auto drain = [&](uint32_t cnt) {            // check q[0, cnt), keep q[cnt, qn)
-        if (lane < (int)cnt) flat_check(R, tb, q[lane], no);
-        uint64_t keep = 0;
-        const bool mv = lane + (int)cnt < (int)qn;
-        if (mv) keep = q[lane + cnt];
-        __builtin_amdgcn_wave_barrier();
-        if (mv) q[lane] = keep;
-        __builtin_amdgcn_wave_barrier();
-        qn -= cnt;
-    };
     for (uint32_t sb = blockIdx.x * (kScanBlock / 64) + (threadIdx.x >> 6); sb < R.nsb; sb += nw) {
         const int64_t wd = (int64_t)sb * (kSuperNt / 16) + 4 * lane;   // the lane's first word
         const bool live = wd < (int64_t)R.n_words;
@@ -2023,28 +2003,46 @@ __global__ __launch_bounds__(kScanBlock) void pscan_kernel(RoundArgs R) {
         auto hits = ps_lookups<S>(tb.bm, w0, c.x, c.y, c.z, c.w, w5);
         using HitT = decltype(hits);
         if (!live) hits = 0;
-        const uint64_t C = (uint64_t)wd * 16;         // nt of sample q: C + q S
-        for (;;) {   // push one hit per lane per pass; check 64 whenever they are queued
-            const uint64_t any = __ballot(hits != 0);
-            if (!any) break;
-            if (hits) {
+        reinterpret_cast<uint4*>(sbw)[1 + lane] = c;
+        if (lane == 0) sbw[3] = w0;
+        if (lane == 63) {
+            sbw[kSbWords - 4] = w5;
+            sbw[kSbWords - 3] = 0u;
+            sbw[kSbWords - 2] = 0u;
+            sbw[kSbWords - 1] = 0u;
+        }
+        uint32_t total;
+        uint32_t idx = wave_excl_scan((uint32_t)__popcll((unsigned long long)hits), total);
+        const uint64_t C0 = (uint64_t)sb * kSuperNt;
+        for (uint32_t base = 0; base < total; base += 64) {   // wave-uniform
+            while (hits && idx < base + 64u) {                 // this lane's hits, in order
                 const int qq = (int)__builtin_ctzll((unsigned long long)hits);
                 hits &= hits - (HitT)1;
-                q[qn + (uint32_t)__popcll(any & lt)] = C + (uint64_t)(qq * S);
+                q[idx - base] = (uint16_t)(lane * 64 + qq * S);
+                ++idx;
             }
             __builtin_amdgcn_wave_barrier();
-            qn += (uint32_t)__popcll(any);
-            if (qn >= 64) drain(64);
+            const bool v = (uint32_t)lane < total - base;
+            const uint32_t p = v ? q[lane] : 0u;
+            // codes of nt [p - 3, p + 29) of the superblock: LDS words 4 + floor((p - 3) / 16) ..
+            const uint32_t t = p + 61u;
+            const uint32_t wi = t >> 4, sh = 2u * (t & 15u);
+            const uint64_t lo = ((uint64_t)sbw[wi + 1] << 32) | sbw[wi];
+            const uint64_t cw = sh ? (lo >> sh) | ((uint64_t)sbw[wi + 2] << (64u - sh)) : lo;
+#if defined(DMX_PS_AB) && DMX_PS_AB == 4   // timing A/B only: queue without checks
+            asm volatile("" ::"v"(cw));
+#else
+            flat_check(R, tb, cw, C0 + p, v);
+#endif
+            __builtin_amdgcn_wave_barrier();
         }
     }
-    if (qn) drain(qn);
 }
 
 // Flat scan -> filter tasks: one lane per item; per orientation the view's cells in view order
 // (cell u covers view positions [16u - delta, +16)), plus a FRONT panel's partial-alignment cells
 // at the view start; a 3' view's last-column window unless a task reaches the view end.
 __global__ __launch_bounds__(kScanBlock) void pcompact_kernel(RoundArgs R) {
-    if (*R.flat_bad) return;
     const DevPanel* P = R.panel;
     const DevPieces* Q = R.pieces;
     const uint32_t n_items = R.items ? *R.n_items_dev : R.n_items;
@@ -2084,7 +2082,7 @@ __global__ __launch_bounds__(kScanBlock) void pcompact_kernel(RoundArgs R) {
                     // c0 - u (strand 1), c0 = the cell of view position 0
                     const int64_t c0 = p0nt >> 4;
                     const int64_t cs = tv.strand ? c0 - k0 - 63 : c0 + k0;   // lowest cell
-                    const uint32_t* cb = R.cells[o];
+                    const uint32_t* cb = R.cells[2 * R.round + (int)tv.strand];
                     const int64_t w = cs >> 5;                               // floor
                     const uint32_t sh = (uint32_t)(cs & 31);
                     const uint64_t lo = ((uint64_t)cb[w + 1] << 32) | cb[w];
@@ -2103,29 +2101,6 @@ __global__ __launch_bounds__(kScanBlock) void pcompact_kernel(RoundArgs R) {
             ps_lastcol(R, wbuf, wcnt, act && !front && !reached, item, o, tv, rb);
         }
     }
-}
-
-// Flat-scan index of the resident batch: flat_bad = 0 iff the reads are sorted by offset and do
-// not overlap; sbf[b] = the first read whose end lies past nt 4096 b (b = 0 .. nsb).
-__global__ void flat_index_kernel(const uint64_t* offs, const uint32_t* lens, uint32_t n_reads,
-                                  uint32_t* sbf, uint32_t nsb, uint32_t* flat_bad) {
-    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r <= n_reads;
-         r += gridDim.x * blockDim.x) {
-        const uint64_t prev_end = r ? offs[r - 1] + lens[r - 1] : 0ull;
-        const uint64_t end = r < n_reads ? offs[r] + lens[r] : (uint64_t)nsb * kSuperNt + 1;
-        if (r < n_reads && r && offs[r] < prev_end) atomicOr(flat_bad, 1u);
-        // superblocks b with prev_end <= 4096 b < end: read r is the first ending past them
-        const uint64_t b0 = (prev_end + kSuperNt - 1) / kSuperNt;
-        for (uint64_t b = b0; b * kSuperNt < end && b <= nsb; ++b) sbf[b] = r;
-    }
-}
-
-// Round 2 of the flat scan: read -> its item (~0 = none).
-__global__ void read_item_kernel(const ItemView* items, const uint32_t* n_items,
-                                 uint32_t* read_item, uint32_t n_reads) {
-    const uint32_t n = *n_items;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        if (items[i].read < n_reads) read_item[items[i].read] = i;
 }
 
 // The shared-suffix filter over the piece screen's tasks: one lane per task, the same segment
@@ -4274,56 +4249,89 @@ int bounds_selftest(Ctx* c, uint32_t* host_out) {
 #endif
 }
 
-// The flat piece scan's index of the resident batch: sortedness flag and
-// superblock -> first read, rebuilt after every load; the cell bitmaps sized to the batch.
+// The flat piece scan: which rounds it serves this exec, their combined table
+// (rebuilt when a panel or the mode changes: every entry of round r tagged with r, the sampling
+// stride the smallest of theirs — a piece's `step` consecutive sampled offsets cover any smaller
+// power-of-two stride too) and two cell bitmaps per flat round sized to the batch.  Rounds whose
+// tables do not fit together, one-orientation panels and DMX_NO_FLAT=1 take the per-part screen.
 int prepare_flat(Ctx* c, hipStream_t st) {
-    c->flat_ok_launch = false;
-    bool want = false;
+    c->flat_rounds = 0;
+    if (c->n_reads == 0 || c->mode == DMX_MODE_LINKED || std::getenv("DMX_NO_FLAT")) return DMX_OK;
+    int want = 0;
     for (int r = 0; r < 2; ++r)
-        want |= c->panel[r].set && c->panel[r].piece_step && c->panel[r].n_orient == 2 &&
-                (r == 0 || c->mode == DMX_MODE_TWO_ROUND);
-    if (!want || c->n_reads == 0 || std::getenv("DMX_NO_FLAT")) return DMX_OK;
+        if ((r == 0 || c->mode == DMX_MODE_TWO_ROUND) && c->panel[r].set && c->panel[r].filter &&
+            c->panel[r].piece_step && c->panel[r].n_orient == 2)
+            want |= 1 << r;
+    if (!want) return DMX_OK;
     const size_t nsb = (c->n_words + kSuperNt / 16 - 1) / (kSuperNt / 16);
-    if (nsb + 1 >= (1ull << 32) || c->n_reads >= (1ull << 31)) return DMX_OK;
-    if (c->sbf_cap < nsb + 1 || !c->d_sbf) {
-        if (c->d_sbf) hipFree(c->d_sbf);
-        c->d_sbf = nullptr;
-        if (hipMalloc((void**)&c->d_sbf, (nsb + 1) * 4) != hipSuccess) return DMX_E_NOMEM;
-        c->sbf_cap = nsb + 1;
-        c->flat_dirty = true;
-    }
-    if (!c->d_flat_bad && hipMalloc((void**)&c->d_flat_bad, 4) != hipSuccess) return DMX_E_NOMEM;
-    const size_t cw = (c->n_words + 31) / 32 + 2 * kCellGuardWords;
-    if (c->cells_cap < cw || !c->d_cells[0]) {
-        for (int o = 0; o < 2; ++o) {
-            if (c->d_cells[o]) hipFree(c->d_cells[o]);
-            c->d_cells[o] = nullptr;
-            if (hipMalloc((void**)&c->d_cells[o], cw * 4) != hipSuccess) return DMX_E_NOMEM;
+    if (nsb >= (1ull << 31) || c->n_words >= (1ull << 31)) return DMX_OK;
+    if (c->flat_gen != c->panel_gen || c->flat_want != want) {
+        c->flat_gen = c->panel_gen;
+        c->flat_want = want;
+        c->flat_step = 0;
+        std::vector<std::pair<uint32_t, uint64_t>> ents;   // (8-mer, tagged entry)
+        int step = 4, npc = 0;
+        for (int r = 0; r < 2; ++r) {
+            if (!(want >> r & 1)) continue;
+            const DevPieces& Q = c->panel[r].pieces;
+            step = std::min(step, (int)Q.step);
+            npc += Q.n_pieces;
+            for (int e = 0; e < Q.n_entries; ++e) {
+                const uint64_t v = Q.entry[e];
+                const int off = (int)((v >> 38) & 3u);
+                ents.push_back({(uint32_t)(v >> (2 * off)) & 0xFFFFu, v | ((uint64_t)r << 56)});
+            }
         }
-        c->cells_cap = cw;
+        if (ents.empty() || ents.size() > (size_t)kMaxPieceEntries) return DMX_OK;
+        std::sort(ents.begin(), ents.end());
+        std::unique_ptr<DevPieces> T(new DevPieces());
+        memset(T.get(), 0, sizeof(DevPieces));
+        int nk = 0;
+        for (size_t e = 0; e < ents.size(); ++e) {
+            if (e == 0 || ents[e].first != ents[e - 1].first) {
+                T->key[nk++] = (uint32_t)e;
+                T->bitmap[ents[e].first >> 5] |= 1u << (ents[e].first & 31);
+            }
+            T->key[nk - 1] += 1u << 16;
+            T->entry[e] = ents[e].second;
+        }
+        for (int w = 0, rk = 0; w < kPieceBitmapWords; ++w) {
+            T->rank_base[w] = (uint16_t)rk;
+            rk += __builtin_popcount(T->bitmap[w]);
+        }
+        T->on = 1;
+        T->step = step;
+        T->n_pieces = npc;
+        T->n_keys = nk;
+        T->n_entries = (int)ents.size();
+        if (!c->d_pieces_flat &&
+            hipMalloc((void**)&c->d_pieces_flat, sizeof(DevPieces)) != hipSuccess)
+            return DMX_E_NOMEM;
+        // the previous exec's scan may still read the old table
+        if (hipStreamSynchronize(st) != hipSuccess ||
+            hipMemcpy(c->d_pieces_flat, T.get(), sizeof(DevPieces), hipMemcpyHostToDevice) !=
+                hipSuccess)
+            return DMX_E_HIP;
+        c->flat_lds = (size_t)kPieceLdsFixed + 8 * ((size_t)(nk + 1) / 2) + 8 * ents.size();
+        c->flat_step = step;
+    }
+    if (!c->flat_step) return DMX_OK;   // the tables do not fit together: the per-part screen
+    const size_t cw = (c->n_words + 31) / 32 + 2 * kCellGuardWords;
+    for (int i = 0; i < 4; ++i) {
+        if (!(want >> (i >> 1) & 1) || (c->d_cells[i] && c->cells_cap[i] >= cw)) continue;
+        if (c->d_cells[i]) hipFree(c->d_cells[i]);
+        c->d_cells[i] = nullptr;
+        c->cells_cap[i] = 0;
+        if (hipMalloc((void**)&c->d_cells[i], cw * 4) != hipSuccess) return DMX_E_NOMEM;
+        c->cells_cap[i] = cw;
     }
     c->cells_words = cw;
-    if (c->read_item_cap < c->n_reads || !c->d_read_item) {
-        if (c->d_read_item) hipFree(c->d_read_item);
-        c->d_read_item = nullptr;
-        if (hipMalloc((void**)&c->d_read_item, c->n_reads * 4) != hipSuccess) return DMX_E_NOMEM;
-        c->read_item_cap = c->n_reads;
-    }
-    if (c->flat_dirty || c->n_sb != nsb) {
-        hipMemsetAsync(c->d_flat_bad, 0, 4, st);
-        const uint32_t grid = (uint32_t)std::min<size_t>((c->n_reads + 256) / 256, 4096);
-        hipLaunchKernelGGL(flat_index_kernel, dim3(grid), dim3(256), 0, st, c->d_offs, c->d_lens,
-                           (uint32_t)c->n_reads, c->d_sbf, (uint32_t)nsb, c->d_flat_bad);
-        c->n_sb = nsb;
-        c->flat_dirty = false;
-    }
-    c->flat_ok_launch = true;
-    return hipGetLastError() == hipSuccess ? DMX_OK : DMX_E_HIP;
+    c->flat_rounds = want;
+    return DMX_OK;
 }
 
 int launch_round(Ctx* c, int round, hipStream_t st) {
     RoundArgs R;
-    R.flat_bad = nullptr;
     R.pk.seq = c->d_seq;
     R.pk.nmask = c->d_nmask;
     R.pk.bd = make_bounds(c, 0);
@@ -4386,58 +4394,55 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     R.ftask = c->d_ftask;
     R.ftask_count = c->d_shard + (kShFtask + round) * kShards * kShardStride;
     R.ftask_scap = (uint32_t)(c->ftask_cap / kShards);
+    R.n_words = (uint32_t)c->n_words;
+    R.nsb = (uint32_t)((c->n_words + kSuperNt / 16 - 1) / (kSuperNt / 16));
+    R.round = round;
+    for (int i = 0; i < 4; ++i)
+        R.cells[i] = (c->flat_rounds >> (i >> 1) & 1) ? c->d_cells[i] + kCellGuardWords : nullptr;
     hipEventRecord(c->ev[round * 3 + 0], st);
+    if (round == 0 && c->flat_rounds) {   // the flat scan: every flat round's marks at once
+        for (int i = 0; i < 4; ++i)
+            if (R.cells[i]) hipMemsetAsync(c->d_cells[i], 0, 4 * c->cells_words, st);
+        RoundArgs S = R;
+        S.pieces = c->d_pieces_flat;
+        const uint32_t sgrid = std::min<uint32_t>((R.nsb + 3) / 4, kScanGrid);
+        const size_t lds = c->flat_lds;
+        set_kid(S.pk.bd, kKerPieces);
+        if (sgrid > 0) {
+            if (c->flat_step == 4)
+                hipLaunchKernelGGL(pscan_kernel<4>, dim3(sgrid), dim3(kScanBlock), lds, st, S);
+            else if (c->flat_step == 2)
+                hipLaunchKernelGGL(pscan_kernel<2>, dim3(sgrid), dim3(kScanBlock), lds, st, S);
+            else
+                hipLaunchKernelGGL(pscan_kernel<1>, dim3(sgrid), dim3(kScanBlock), lds, st, S);
+        }
+        DMX_DBG_SYNC("pscan_kernel");
+    }
     if (hp.filter && !linked) {   // linked primers: short, no shared suffix block; plain scan
         if (hp.piece_step) {      // piece screen, then the filter on its tasks
-            const DevPieces& Q = hp.pieces;   // LDS image: bitmap + rank base, keys, entries
-            const size_t lds = (size_t)kPieceLdsFixed + 8 * ((Q.n_keys + 1) / 2) +
-                               8 * (size_t)Q.n_entries;
-            const bool flat = c->flat_ok_launch && hp.n_orient == 2;
-            if (flat) {   // the flat scan (its kernels exit when the batch is not sorted)
-                R.flat_bad = c->d_flat_bad;
-                R.sbf = c->d_sbf;
-                R.nsb = (uint32_t)c->n_sb;
-                R.n_words = (uint32_t)c->n_words;
-                R.read_item = c->d_read_item;
-                R.n_reads = (uint32_t)c->n_reads;
-                for (int o = 0; o < 2; ++o) R.cells[o] = c->d_cells[o] + kCellGuardWords;
-                hipMemsetAsync(c->d_cells[0], 0, 4 * c->cells_words, st);
-                hipMemsetAsync(c->d_cells[1], 0, 4 * c->cells_words, st);
-                if (round == 1) {
-                    hipMemsetAsync(c->d_read_item, 0xFF, 4 * c->n_reads, st);
-                    hipLaunchKernelGGL(read_item_kernel, dim3(1024), dim3(256), 0, st, c->d_items,
-                                       c->d_counters + 2, c->d_read_item, (uint32_t)c->n_reads);
-                }
-                const uint32_t sgrid = (uint32_t)std::min<size_t>((c->n_sb + 3) / 4, kScanGrid);
-                set_kid(R.pk.bd, kKerPieces);
-                if (sgrid > 0) {
-                    if (hp.piece_step == 4)
-                        hipLaunchKernelGGL(pscan_kernel<4>, dim3(sgrid), dim3(kScanBlock), lds, st, R);
-                    else if (hp.piece_step == 2)
-                        hipLaunchKernelGGL(pscan_kernel<2>, dim3(sgrid), dim3(kScanBlock), lds, st, R);
-                    else
-                        hipLaunchKernelGGL(pscan_kernel<1>, dim3(sgrid), dim3(kScanBlock), lds, st, R);
-                }
-                DMX_DBG_SYNC("pscan_kernel");
+            set_kid(R.pk.bd, kKerPieces);
+            if (c->flat_rounds >> round & 1) {   // the flat scan's marks -> filter tasks
                 const uint32_t cgrid = std::min<uint32_t>((R.n_items + 255) / 256, 2048u);
                 if (cgrid > 0)
                     hipLaunchKernelGGL(pcompact_kernel, dim3(cgrid), dim3(kScanBlock), 0, st, R);
                 DMX_DBG_SYNC("pcompact_kernel");
-            } else {
-                R.flat_bad = nullptr;
+            } else {   // the per-part screen
+                const DevPieces& Q = hp.pieces;   // LDS image: bitmap + rank base, keys, entries
+                const size_t lds = (size_t)kPieceLdsFixed + 8 * ((Q.n_keys + 1) / 2) +
+                                   8 * (size_t)Q.n_entries;
+                const uint32_t pgrid =
+                    (uint32_t)((R.n_items + kPsItemsPerBlock - 1) / kPsItemsPerBlock);
+                const uint32_t grid = std::min<uint32_t>(pgrid, kPieceGrid);
+                if (pgrid > 0) {
+                    if (hp.piece_step == 4)
+                        hipLaunchKernelGGL(pscreen_kernel<4>, dim3(grid), dim3(kScanBlock), lds, st, R);
+                    else if (hp.piece_step == 2)
+                        hipLaunchKernelGGL(pscreen_kernel<2>, dim3(grid), dim3(kScanBlock), lds, st, R);
+                    else
+                        hipLaunchKernelGGL(pscreen_kernel<1>, dim3(grid), dim3(kScanBlock), lds, st, R);
+                }
+                DMX_DBG_SYNC("pscreen_kernel");
             }
-            const uint32_t pgrid = (uint32_t)((R.n_items + kPsItemsPerBlock - 1) / kPsItemsPerBlock);
-            const uint32_t grid = std::min<uint32_t>(pgrid, kPieceGrid);
-            set_kid(R.pk.bd, kKerPieces);
-            if (pgrid > 0) {   // the per-part screen (exits at once when the flat scan ran)
-                if (hp.piece_step == 4)
-                    hipLaunchKernelGGL(pscreen_kernel<4>, dim3(grid), dim3(kScanBlock), lds, st, R);
-                else if (hp.piece_step == 2)
-                    hipLaunchKernelGGL(pscreen_kernel<2>, dim3(grid), dim3(kScanBlock), lds, st, R);
-                else
-                    hipLaunchKernelGGL(pscreen_kernel<1>, dim3(grid), dim3(kScanBlock), lds, st, R);
-            }
-            DMX_DBG_SYNC("pscreen_kernel");
             hipEventRecord(c->ev[15 + round], st);
             set_kid(R.pk.bd, kKerFilter);
             hipLaunchKernelGGL(ftask_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);

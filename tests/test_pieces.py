@@ -3,9 +3,9 @@
 Adversarial reads: every adapter of the 24 x 24 panels with exactly K edits, one in each of K of
 its K + 1 pieces (so exactly one piece survives as an exact copy), for every surviving piece, in
 both read orientations, at the read start, middle and end; partial adapters at both read ends;
-N inside and around the pieces.  The flat scan (sorted batches), the per-part screen (permuted
-batch layouts, and DMX_NO_FLAT=1) and the full filter pass (DMX_NO_PIECES=1) must all equal the
-oracle on every result byte.
+N inside and around the pieces.  The flat scan (dmx_pack layouts, permuted read order, reads
+that overlap in the packed batch), the per-part screen (DMX_NO_FLAT=1) and the full filter pass
+(DMX_NO_PIECES=1) must all equal the oracle on every result byte.
 """
 import numpy as np
 import pytest
@@ -64,10 +64,24 @@ def adversarial_reads(rng, panel, where):
     return seqs + ["", "A", ad[:7], ad[-7:]]
 
 
+def overlapping(seqs):
+    """seqs plus, per read of >= 12 nt, the read without its first 3 and last 4 nt: packed as a
+    view into the read's own nt (_run), so the batch holds reads that share nt."""
+    return seqs + [s[3:len(s) - 4] for s in seqs if len(s) >= 12]
+
+
 def _run(seqs, panel, where, layout="sorted", env=None, monkeypatch=None):
-    blob, offs, lens = oracle.pack_ascii(seqs)
-    p = lib.pack(blob, offs, lens)
     perm = None
+    if layout == "overlap":   # results for overlapping(seqs): the sub-reads point into their reads
+        blob, offs, lens = oracle.pack_ascii(seqs)
+        p = lib.pack(blob, offs, lens)
+        src = [i for i in range(len(seqs)) if lens[i] >= 12]
+        offs2 = np.concatenate([p.offsets, p.offsets[src] + 3]).astype(p.offsets.dtype)
+        lens2 = np.concatenate([p.lengths, p.lengths[src] - 7]).astype(p.lengths.dtype)
+        p = lib.Packed(p.seq2b, p.nmask, offs2, lens2)
+    else:
+        blob, offs, lens = oracle.pack_ascii(seqs)
+        p = lib.pack(blob, offs, lens)
     if layout == "permuted":
         perm = np.random.default_rng(1).permutation(p.n_reads)
         p = lib.Packed(p.seq2b, p.nmask, p.offsets[perm].copy(), p.lengths[perm].copy())
@@ -89,17 +103,17 @@ def _run(seqs, panel, where, layout="sorted", env=None, monkeypatch=None):
 
 
 @pytest.mark.parametrize("rnd", [0, 1])
-@pytest.mark.parametrize("variant", ["flat", "per_part", "no_flat", "no_pieces"])
+@pytest.mark.parametrize("variant", ["flat", "permuted", "overlap", "no_flat", "no_pieces"])
 def test_one_surviving_piece(rnd, variant, monkeypatch):
     n1, s5, n2, s27 = synth.panels(24, 24)
     panel, where = (s5, oracle.FRONT) if rnd == 0 else (s27, oracle.BACK)
     rng = np.random.default_rng(100 + rnd)
     seqs = adversarial_reads(rng, panel, where)
-    blob, offs, lens = oracle.pack_ascii(seqs)
+    blob, offs, lens = oracle.pack_ascii(overlapping(seqs) if variant == "overlap" else seqs)
     exp = oracle.run_batch(oracle.Panel(panel, where), None, blob, offs, lens, mode=0,
                            use_rc=True, threads=8)
-    assert (exp["bin1"] >= 0).mean() > 0.8
-    layout = "permuted" if variant == "per_part" else "sorted"
+    assert (exp["bin1"] >= 0).mean() > 0.7
+    layout = variant if variant in ("permuted", "overlap") else "sorted"
     env = {"no_flat": {"DMX_NO_FLAT": "1"}, "no_pieces": {"DMX_NO_PIECES": "1"}}.get(variant)
     got, tasks = _run(seqs, panel, where, layout, env, monkeypatch)
     _assert_same(got, exp)
@@ -153,3 +167,35 @@ def test_iupac_panel_falls_back_to_the_full_filter(ctx):
     got = ctx.run(lib.pack(blob, offs, lens))
     _assert_same(got, exp)
     assert ctx.stats()["filter_tasks"][0] == 0
+
+
+@pytest.mark.parametrize("case", ["iupac_round1", "no_flat"])
+def test_two_round_mixed_screens(case, monkeypatch):
+    """Round 1 on the full filter pass (a wildcard panel) while round 2 takes the flat scan (its
+    marks come from the one scan launched ahead of round 1), and both rounds on the per-part
+    screen (DMX_NO_FLAT=1)."""
+    n1, s5, n2, s27 = synth.panels(24, 24)
+    rng = np.random.default_rng(11)
+    p1 = [a[:10] + "N" + a[11:] for a in s5] if case == "iupac_round1" else s5
+    seqs = []
+    for i in range(2000):
+        a = p1[i % 24].replace("N", "ACGT"[int(rng.integers(4))])
+        b = s27[(i * 5) % 24]
+        kb = full_k(len(b), 0.1)
+        cb = mutate(rng, b, pieces_of(len(b), kb), int(rng.integers(kb + 1)))
+        s = _rand(rng, rng.integers(0, 9)) + a + _rand(rng, rng.integers(100, 1200)) + cb
+        seqs.append(revcomp(s) if rng.random() < 0.4 else s)
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    exp = oracle.run_batch(oracle.Panel(p1, oracle.FRONT), oracle.Panel(s27, oracle.BACK), blob,
+                           offs, lens, mode=1, threads=8)
+    assert (exp["bin2"] >= 0).mean() > 0.6
+    if case == "no_flat":
+        monkeypatch.setenv("DMX_NO_FLAT", "1")
+    with lib.Context(0) as c:
+        c.set_panel(0, p1, lib.DMX_FRONT | lib.DMX_RC)
+        c.set_panel(1, s27, lib.DMX_BACK | lib.DMX_RC)
+        c.set_mode(lib.MODE_TWO_ROUND)
+        got = c.run(lib.pack(blob, offs, lens))
+        tasks = c.stats()["filter_tasks"]
+    _assert_same(got, exp)
+    assert tasks[1] > 0 and (tasks[0] == 0) == (case == "iupac_round1")
