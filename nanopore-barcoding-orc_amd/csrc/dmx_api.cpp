@@ -142,6 +142,13 @@ int ensure_pipeline(Ctx* c) {
         c->task_cap = 4 * want_win;
         c->ftask_cap = want_win;
     }
+    // window code slots: verified windows are about one per view and round; later ones gather
+    const size_t want_stage = std::min<size_t>(c->win_cap, 2 * std::max(slots0, n) + 65536);
+    if (c->use_stage && c->stage_cap < want_stage) {
+        int rc;
+        if ((rc = dev_alloc(c, &c->d_stage, want_stage * kStageWords))) return rc;
+        c->stage_cap = want_stage;
+    }
     const size_t nc = counts_size(c);
     if (c->n_counts != nc) {
         int rc;
@@ -306,6 +313,8 @@ int dmx_open(int device, dmx_ctx** out) {
     c->no_pieces = np && np[0] == '1';
     const char* rs = std::getenv("DMX_RESOLVE");
     c->force_ring = rs && std::strcmp(rs, "ring") == 0;
+    const char* stg = std::getenv("DMX_STAGE");   // A/B: window code slots
+    c->use_stage = stg && stg[0] == '1';
     const char* ns = std::getenv("DMX_NO_SCREEN");   // A/B: no index screen before the
     c->no_screen = ns && ns[0] == '1';               // window scan
     const char* s1 = std::getenv("DMX_SCREEN_V1");   // A/B: the unpacked index screen
@@ -336,7 +345,7 @@ void dmx_close(dmx_ctx* c) {
                     c->d_winner[0], c->d_winner[1], c->d_origin[0], c->d_origin[1], c->d_lb[0], c->d_lb[1], c->d_cl[0],
                     c->d_cl[1],     c->d_outc[0],   c->d_outc[1],  c->d_items, c->d_win, c->d_win2, c->d_linked, c->d_tasks, c->d_counters, c->d_shard,
                     c->d_counts,    c->d_panel[0],  c->d_panel[1], c->d_pieces[0], c->d_pieces[1],
-                    c->d_ftask, c->d_pieces_flat, c->d_cells[0], c->d_cells[1], c->d_cells[2],
+                    c->d_ftask, c->d_stage, c->d_pieces_flat, c->d_cells[0], c->d_cells[1], c->d_cells[2],
                     c->d_cells[3]};
     for (void* b : bufs)
         if (b) hipFree(b);
@@ -741,6 +750,16 @@ static int build_panel(Ctx* c, const char* const* seqs, const int* lens, const i
         return DMX_E_UNSUPPORTED;
     }
     for (int a = 0; a < n; ++a) dp.ad[a] = hp.ad[a];
+    // window code slots: from m + k + 1 columns before a window's first hit
+    // column (the window scan's restricted start), never below the band's own warm-up
+    hp.pre_len = dp.pre_len;
+    int mk = 0, m_max = 0;
+    for (int a = 0; a < n; ++a) {
+        mk = std::max(mk, (int)hp.ad[a].m + (int)hp.ad[a].k + 1);
+        m_max = std::max(m_max, (int)hp.ad[a].m);
+    }
+    hp.stage_back = mk;
+    hp.stage_lo = -std::min(kViewReachPre, m_max + 7);
     return DMX_OK;
 }
 
@@ -1128,6 +1147,14 @@ int dmx_debug_fetch(dmx_ctx* c, int what, int round, void* out, size_t cap_bytes
         const size_t take = out ? std::min(nb, cap_bytes > done ? cap_bytes - done : 0) : 0;
         if (take) CK(hipMemcpy((char*)out + done, base + s * scap * rec, take, hipMemcpyDeviceToHost));
         done += nb;
+    }
+    if (out) {   // records name their window code slot in off's top bits: clear them
+        for (size_t r = 0; (r + 1) * rec <= std::min(done, cap_bytes); ++r) {
+            uint64_t off;
+            std::memcpy(&off, (char*)out + r * rec + 32, 8);
+            off &= kOffMask;
+            std::memcpy((char*)out + r * rec + 32, &off, 8);
+        }
     }
     return (int)std::min<size_t>(done, (size_t)1 << 30);
 }

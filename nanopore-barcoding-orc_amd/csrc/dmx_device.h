@@ -105,7 +105,7 @@ struct Window {
     uint32_t n, start, len, info;
     uint64_t off;
 };
-static_assert(sizeof(Window) == 40, "Window layout");
+static_assert(sizeof(Window) == 40 && offsetof(Window, off) == 32, "Window layout");
 constexpr uint8_t kWinClean = 2;   // Window.strand bit 1
 
 constexpr int kStageCap = 256;    // LDS staging of emitted records per block
@@ -273,7 +273,7 @@ struct Cand {
     uint8_t strand, o, a, clean;   // clean: the band reads codes only (Window kWinClean)
     uint64_t off;
 };
-static_assert(sizeof(Cand) == 40, "Cand layout");
+static_assert(sizeof(Cand) == 40 && offsetof(Cand, off) == 32, "Cand layout");
 
 struct Outcome {      // best cell found by the resolve lane of a cluster
     uint64_t key;     // ~0 = none
@@ -367,7 +367,17 @@ struct Packed {
     const uint32_t* seq;
     const uint32_t* nmask;
     Bounds bd;
+    const uint32_t* stage = nullptr;   // window code slots (kStageWords each, wstage_kernel)
 };
+
+// Window code slots: the codes and no-match bits of 128 view columns of one
+// verified window, gathered once by wstage_kernel for the index screen, the window scan and the
+// band.  Words 0..7: codes of columns base + 16 i .. (2 bits each, view orientation), 8..11:
+// no-match bits of columns base + 32 i .., 12: base, 13: columns filled (16 per gathered chunk).
+// A window, task or candidate names its slot in the top bits of its `off` (slot + 1, 0 = none).
+constexpr int kStageWords = 16;
+constexpr int kOffBits = 36;                              // batch nt offsets < 2^36
+constexpr uint64_t kOffMask = (1ull << kOffBits) - 1ull;
 
 __device__ __forceinline__ uint32_t window32(const uint32_t* __restrict__ w, int64_t bitpos,
                                              const Bounds& bd, uint32_t buf) {

@@ -34,6 +34,10 @@ struct HostPanel {
     bool nonpos = false;      // an accepted match may score <= 0 (needs per-orientation winners)
     PanelReach reach;
     DevAdapter ad[kMaxAdapters];
+    int pre_len = 0;          // DevPanel::pre_len (0: no verification, the window scan reads
+                              // the filter's windows)
+    int stage_back = 0;       // window code slots start this many columns before j1 (m + k + 1),
+    int stage_lo = 0;         // and not before this view position
     int piece_step = 0;       // piece screen sampling stride (0 = off: the full filter pass)
     DevPieces pieces;         // its tables
 };
@@ -111,6 +115,9 @@ struct Ctx {
     unsigned long long* d_linked = nullptr;
     Window* d_tasks = nullptr;           // index screen survivors (window piece of one adapter)
     size_t task_cap = 0;
+    uint32_t* d_stage = nullptr;         // window code slots (wstage_kernel), kStageWords each
+    size_t stage_cap = 0;
+    bool use_stage = false;              // DMX_STAGE=1 (A/B, measured slower: DESIGN.md §3.13)
     FTask* d_ftask = nullptr;            // piece screen -> filter tasks
     size_t ftask_cap = 0;
     // flat piece scan (prepare_flat): one scan of the batch against the flat rounds' combined

@@ -62,6 +62,8 @@ struct RoundArgs {
     FTask* ftask;                // piece screen -> filter tasks
     uint32_t* ftask_count;       // [kShards]: shard s at ftask + s * ftask_scap
     uint32_t ftask_scap;
+    uint32_t* stage;             // window code slots (wstage_kernel), stage_cap of them
+    uint32_t stage_cap;
     // flat piece scan: cell bitmaps [2 round + strand], kCellGuardWords words before index 0
     uint32_t n_words;
     uint32_t nsb;                // 4096-nt superblocks of the packed batch
@@ -85,7 +87,49 @@ struct TaskView {
     uint64_t off;
     int o, a;
     bool clean = false;   // the exact stages may skip the no-match mask (Window kWinClean)
+    uint32_t tag = 0;     // window code slot + 1 (0: gather from the packed batch)
+    uint32_t sbl = 0;     // the slot's base column + kViewReachPre (bits 0..23), filled columns
 };
+
+// A record's `off` field -> the view's first nt and its window code slot (kStageWords).
+__device__ __forceinline__ void view_off(const Packed& pk, uint64_t off, TaskView& tv) {
+    tv.off = off & kOffMask;
+    tv.tag = (uint32_t)(off >> kOffBits);
+    tv.sbl = 0;
+    if (tv.tag) {
+        const uint2 h = *reinterpret_cast<const uint2*>(pk.stage + (size_t)(tv.tag - 1) *
+                                                                      kStageWords + 12);
+        tv.sbl = (h.x + kViewReachPre) | (h.y << 24);
+    }
+}
+
+// 16 view positions from p out of the view's window code slot, when it holds them: the same
+// codes and no-match bits as the gather (wstage_kernel filled the slot with fetch16s).
+__device__ __forceinline__ bool staged16(const Packed& pk, const TaskView& tv, int p, bool mask,
+                                         uint32_t& codes, uint32_t& nbits) {
+    if (!tv.tag) return false;
+    const int rel = p + kViewReachPre - (int)(tv.sbl & 0xFFFFFFu);
+    if (rel < 0 || rel + 16 > (int)(tv.sbl >> 24)) return false;
+    const uint32_t* sl = pk.stage + (size_t)(tv.tag - 1) * kStageWords;
+    uint64_t c;
+    __builtin_memcpy(&c, sl + (rel >> 4), 8);
+    codes = (uint32_t)(c >> (2 * (rel & 15)));
+    if (mask) {
+        uint64_t m;
+        __builtin_memcpy(&m, sl + 8 + (rel >> 5), 8);
+        nbits = (uint32_t)(m >> (rel & 31)) & 0xFFFFu;
+    } else {
+        nbits = 0u;
+    }
+    return true;
+}
+
+// fetch16 of a view that may have a window code slot
+__device__ __forceinline__ void fetch16t(const Packed& pk, const TaskView& tv, uint32_t p,
+                                         uint32_t& codes, uint32_t& nbits, bool load_mask = true) {
+    if (staged16(pk, tv, (int)p, load_mask, codes, nbits)) return;
+    fetch16(pk, tv.off, tv.n, tv.strand, tv.start, p, codes, nbits, load_mask);
+}
 
 // An empty view at the first valid offset (DMX_DEBUG_BOUNDS builds: an item or read index out of
 // range; the violation is recorded and the task scans nothing).
@@ -249,15 +293,15 @@ __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster
 
     uint32_t p0 = js;
     uint32_t ncodes, nnb, ncodes2 = 0, nnb2 = 0;   // the next two chunks, in flight
-    fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb);
+    fetch16t(R.pk, tv, p0, ncodes, nnb);
     if (p0 + 16 < jhi)
-        fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes2, nnb2);
+        fetch16t(R.pk, tv, p0 + 16, ncodes2, nnb2);
     for (; p0 + 16 <= jhi; p0 += 16) {
         const uint32_t codes = ncodes, nb = nnb;
         ncodes = ncodes2;
         nnb = nnb2;
         if (p0 + 32 < jhi)
-            fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 32, ncodes2, nnb2);
+            fetch16t(R.pk, tv, p0 + 32, ncodes2, nnb2);
 #pragma unroll
         for (int q = 0; q < 16; ++q) DMX_SCAN_STEP(q)
     }
@@ -409,7 +453,7 @@ __device__ __forceinline__ Cand make_cand(const TaskView& tv, uint32_t item, int
     c.o = (uint8_t)tv.o;
     c.a = (uint8_t)tv.a;
     c.clean = tv.clean ? 1 : 0;
-    c.off = tv.off;
+    c.off = tv.off | ((uint64_t)tv.tag << kOffBits);
     return c;
 }
 
@@ -432,6 +476,7 @@ template <bool MASK = true>
 __device__ __forceinline__ void fetch16s(const Packed& pk, const TaskView& tv, int p,
                                          uint32_t& codes, uint32_t& nbits) {
     p = max(p, -kViewReachPre);
+    if (staged16(pk, tv, p, MASK && !tv.clean, codes, nbits)) return;
     if (tv.strand == 0) {
         const int64_t g = (int64_t)tv.off + (int64_t)tv.start + p;
         codes = code32(pk, g);
@@ -637,15 +682,15 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
     uint32_t p0 = js;
     uint32_t ncodes, nnb, ncodes2 = 0, nnb2 = 0;   // the next two chunks, in flight
     const bool lm = !tv.clean;                      // clean windows: codes only
-    fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0, ncodes, nnb, lm);
+    fetch16t(R.pk, tv, p0, ncodes, nnb, lm);
     if (p0 + 16 < jhi)
-        fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes2, nnb2, lm);
+        fetch16t(R.pk, tv, p0 + 16, ncodes2, nnb2, lm);
     for (; p0 + 16 <= jhi; p0 += 16) {
         const uint32_t codes = ncodes, nb = nnb;
         ncodes = ncodes2;
         nnb = nnb2;
         if (p0 + 32 < jhi)
-            fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 32, ncodes2, nnb2, lm);
+            fetch16t(R.pk, tv, p0 + 32, ncodes2, nnb2, lm);
         if (segset && p0 + 16 >= seg + 64) {   // this chunk could overflow the 64-bit segment
             flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
             segset = false;
@@ -2317,7 +2362,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                 tv.strand = w.strand & 1u;
                 tv.start = w.start;
                 tv.len = w.len;
-                tv.off = w.off;
+                view_off(R.pk, w.off, tv);
                 tv.o = w.o;
                 tv.a = 0;
                 int js = lo - L - kf - 1;              // restricted start: exact from lo on
@@ -2519,7 +2564,7 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
                 tv.strand = w.strand & 1u;
                 tv.start = w.start;
                 tv.len = w.len;
-                tv.off = w.off;
+                view_off(R.pk, w.off, tv);
                 tv.o = w.o;
                 tv.a = a;
                 uint32_t c0 = 0, n0 = 0, c1 = 0, n1 = 0;   // two chunks in flight
@@ -2589,6 +2634,56 @@ __global__ __launch_bounds__(kScanBlock) void iscreen_kernel(RoundArgs R) {
     st.flush();
     __syncthreads();
     if (threadIdx.x == 0 && s_nend) atomicAdd(&R.diag[3], s_nend);     // by 3' cells only
+}
+
+// ---------------------------------------------------------------------------------------------
+// Window code slots: the index screen, the window scan and the band each read
+// the codes around a verified window; without slots each gathers them from the packed batch (a
+// few random 64-B lines per window and stage).  One lane per (window, 16-column chunk) gathers
+// them once, with the same fetch16s, into the window's slot (kStageWords, dense list order), and
+// tags the record's `off` with slot + 1; tasks and candidates inherit the tag.  The slot covers
+// columns [base, base + 128), base = max(j1 - back, lo) with back = the panel's largest m + k + 1
+// and lo = -min(kViewReachPre, m_max + 7) (no gather reaches further before a view than the
+// band's own), chunks starting at or before the view end (later ones keep the gather).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kScanBlock) void wstage_kernel(RoundArgs R, Window* wl,
+                                                            const uint32_t* counts, int back,
+                                                            int lo) {
+    __shared__ uint32_t s_spre[kShards + 1];
+    ShardMap sm{s_spre, 0u};
+    sm.load(counts, R.win_scap);
+    const uint32_t nwin = min(sm.total(), R.stage_cap);
+    const uint32_t k = threadIdx.x & 7u;            // the lane's chunk
+    const uint32_t step = (gridDim.x * blockDim.x) >> 3;
+    for (uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 3; g < nwin; g += step) {
+        const uint32_t phys = sm.phys(g);
+        Window* wp = wl + phys;
+        const Window w = *wp;
+        TaskView tv;
+        tv.read = 0;
+        tv.n = w.n;
+        tv.strand = w.strand & 1u;
+        tv.clean = false;                           // the no-match bits always (exact stages)
+        tv.start = w.start;
+        tv.len = w.len;
+        tv.off = w.off & kOffMask;
+        tv.o = w.o;
+        tv.a = 0;
+        const int base = max((int)w.j1 - back, lo);
+        const int nfill = min(max(((int)w.len - base) / 16 + 1, 0), 8);
+        uint32_t codes = 0, nb = 0;
+        if ((int)k < nfill) fetch16s<true>(R.pk, tv, base + 16 * (int)k, codes, nb);
+        uint32_t* sl = R.stage + (size_t)g * kStageWords;
+        sl[k] = codes;
+        const uint32_t nbn = __shfl_down(nb, 1u, 64);   // (the 8 lanes of a window run together)
+        if (!(k & 1u)) sl[8 + (k >> 1)] = nb | (nbn << 16);
+        if (k == 0) {
+            sl[12] = (uint32_t)base;
+            sl[13] = 16u * (uint32_t)nfill;
+            if (base + kViewReachPre < (1 << 24))
+                wp->off = tv.off | ((uint64_t)(g + 1) << kOffBits);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2832,7 +2927,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                 tv.strand = w.strand & 1u;
                 tv.start = w.start;
                 tv.len = w.len;
-                tv.off = w.off;
+                view_off(R.pk, w.off, tv);
                 tv.o = w.o;
                 tv.a = 0;
                 const char* qb = reinterpret_cast<const char*>(s_q);
@@ -2980,7 +3075,7 @@ __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, 
     tv.clean = (w.strand & kWinClean) != 0;
     tv.start = w.start;
     tv.len = w.len;
-    tv.off = w.off;
+    view_off(R.pk, w.off, tv);
     tv.o = w.o;
     tv.a = a;
     const DevAdapter& ad = R.panel->ad[a];
@@ -3223,7 +3318,7 @@ struct Walker {
             const int p = j - 1;              // view position of column j's character
             if (p < cbase) {
                 cbase = max(p - 15, 0);
-                fetch16(pk, tv.off, tv.n, tv.strand, tv.start, (uint32_t)cbase, codes, nb);
+                fetch16t(pk, tv, (uint32_t)cbase, codes, nb);
             }
             const int sh = p - cbase;
             const uint32_t code = ((codes >> (2 * sh)) & 3u) | (((nb >> sh) & 1u) << 2);
@@ -3368,11 +3463,11 @@ __global__ __launch_bounds__(kResolveBlock) void resolve_kernel(RoundArgs R) {
             since = 0;
         };
         uint32_t ncodes, nnb;             // next chunk, prefetched one chunk ahead
-        fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, (uint32_t)js, ncodes, nnb);
+        fetch16t(R.pk, tv, (uint32_t)js, ncodes, nnb);
         for (uint32_t p0 = (uint32_t)js; p0 < c.j2; p0 += 16) {
             const uint32_t codes = ncodes, nb = nnb;
             if (p0 + 16 < c.j2)
-                fetch16(R.pk, tv.off, tv.n, tv.strand, tv.start, p0 + 16, ncodes, nnb);
+                fetch16t(R.pk, tv, p0 + 16, ncodes, nnb);
             const uint32_t cnt = min(16u, c.j2 - p0);
             for (uint32_t q = 0; q < cnt; ++q) {
                 const uint32_t code = ((codes >> (2 * q)) & 3u) | (((nb >> q) & 1u) << 2);
@@ -3703,7 +3798,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                 tv.clean = c.clean != 0;
                 tv.start = c.start;
                 tv.len = c.len;
-                tv.off = c.off;
+                view_off(R.pk, c.off, tv);
                 tv.o = c.o;
                 tv.a = c.a;
                 int c2, origin, score;
@@ -4394,6 +4489,12 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     R.ftask = c->d_ftask;
     R.ftask_count = c->d_shard + (kShFtask + round) * kShards * kShardStride;
     R.ftask_scap = (uint32_t)(c->ftask_cap / kShards);
+    // window code slots: band-mode window scans of this pipeline, offsets that leave tag bits
+    R.stage = (c->d_stage && !linked && hp.filter && band && c->use_stage &&
+               (uint64_t)c->n_words * 16 < (1ull << kOffBits))
+                  ? c->d_stage : nullptr;
+    R.stage_cap = (uint32_t)c->stage_cap;
+    R.pk.stage = c->d_stage;
     R.n_words = (uint32_t)c->n_words;
     R.nsb = (uint32_t)((c->n_words + kSuperNt / 16 - 1) / (kSuperNt / 16));
     R.round = round;
@@ -4461,6 +4562,14 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         if (hp.verify)
             hipLaunchKernelGGL(verify_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R);
         DMX_DBG_SYNC("verify_kernel");
+        if (R.stage) {   // window code slots for the screen, the window scan and the band
+            set_kid(R.pk.bd, kKerVerify);
+            const bool v = hp.pre_len != 0;   // the window scan's list (wscan_kernel)
+            hipLaunchKernelGGL(wstage_kernel, dim3(256 * 8), dim3(kScanBlock), 0, st, R,
+                               v ? c->d_win2 : c->d_win, v ? R.win2_count : R.win_count,
+                               hp.stage_back, hp.stage_lo);
+            DMX_DBG_SYNC("wstage_kernel");
+        }
         hipEventRecord(c->ev[10 + 2 * round], st);
         if (R.screen) {   // packed quads for panels of <= 32 adapters (DMX_SCREEN_V1: A/B)
             if (hp.n <= 4 * kScreenQuads && !c->screen_v1) {

@@ -149,6 +149,18 @@ def test_error_rates_and_filter_toggle(ctx, e, monkeypatch):
         _assert_same(c2.run(lib.pack(d["blob"], d["offsets"], d["lengths"])), exp)
 
 
+@pytest.mark.parametrize("config,seed", [("c2x24", 3), ("c4", 4)])
+def test_window_code_slots(config, seed, monkeypatch):
+    """DMX_STAGE=1 (A/B): the screen, window scan and band read the codes of a
+    verified window from its slot instead of the packed batch; every byte stays the same."""
+    monkeypatch.setenv("DMX_STAGE", "1")
+    d = synth.generate(config, n=6000, seed=seed)
+    exp = _oracle_two_round(d)
+    with lib.Context(0) as c:
+        _assert_same(_gpu_two_round(c, d), exp)
+        _assert_same(_gpu_two_round(c, d, rc=False), _oracle_two_round(d, rc=False))
+
+
 @pytest.mark.parametrize("mode", ["band", "ring"])
 def test_resolve_kernels_agree(mode, monkeypatch):
     """Both resolve kernels (banded DP / LDS-ring traceback) reproduce the oracle."""
