@@ -265,6 +265,7 @@ def _loop_body(args, argv, infile, outdir, ds, demux_in, pych_dir, base, ads1, a
         level = 1 if args.zlevel1 else args.compression_level
         sink1 = nio.Sink(p1, False, level, threads=args.threads)
         sink2 = nio.Sink(p2, False, level, threads=args.threads)
+        marks.append(("sinks", time.perf_counter() - _T_IMPORT))
     except BaseException:
         for x in (sink1, sink2, reo):
             if x is not None:
@@ -275,6 +276,9 @@ def _loop_body(args, argv, infile, outdir, ds, demux_in, pych_dir, base, ads1, a
         raise
     bp2_out = np.zeros(len(n1), np.int64)
     prof = dict(read_wait=0.0, gpu=0.0, plan_write=0.0, drain=0.0)
+    # parts of plan_write: coordinates, the two sink hand-offs (each waits for that sink's
+    # previous batch to be rendered, compressed and written), the report statistics
+    prof.update(pw_plan=0.0, pw_write1=0.0, pw_write2=0.0, pw_stats=0.0)
     if reo is not None:   # parts of "gpu": pychopper step, view packing
         prof.update(reo=0.0, pack=0.0)
     n2_out = np.zeros(len(n1), np.int64)
@@ -314,12 +318,16 @@ def _loop_body(args, argv, infile, outdir, ds, demux_in, pych_dir, base, ads1, a
                 # unmatched in round 1 is written untrimmed to unknown (--no-cleanup only)
                 s1w = np.where(m1, s1, 0)
                 o1w = o1.astype(np.uint8)   # an unmatched read may still be taken RC'd
+                tq = time.perf_counter()
+                prof["pw_plan"] += tq - tw
                 if views is None:
                     sink1.write(batch, idx1, s1w, e1, o1w, o1w)
                 else:
                     x, y, t = view_coords(views[1], views[2], views[3], s1w, e1, o1w)
                     sink1.write_rows2(batch, views[0], idx1, x, y, t, views[1], views[2],
                                       views[3], o1w)
+                tr = time.perf_counter()
+                prof["pw_write1"] += tr - tq
                 idx2 = np.where(m1, out2[np.maximum(b1, 0), b2 + 1], -1)
                 # round-2 unknown: the round-1 output record, untrimmed by round 2
                 m2 = b2 >= 0
@@ -330,17 +338,25 @@ def _loop_body(args, argv, infile, outdir, ds, demux_in, pych_dir, base, ads1, a
                 e2w = np.where(m2, e2, np.where(u2rc, e1 - s1, e1))
                 o2w = np.where(m2, o2, np.where(u2rc, 1 - o1, o1)).astype(np.uint8)
                 n2w = np.where(m2, nrc2, o1 + u2rc).astype(np.uint8)
+                tq = time.perf_counter()
+                prof["pw_plan"] += tq - tr
                 if views is None:
                     sink2.write(batch, idx2, s2w, e2w, o2w, n2w)
                 else:
                     x, y, t = view_coords(views[1], views[2], views[3], s2w, e2w, o2w)
                     sink2.write_rows2(batch, views[0], idx2, x, y, t, views[1], views[2],
                                       views[3], n2w)
+                tr = time.perf_counter()
+                prof["pw_write2"] += tr - tq
                 _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w,
                              bp2_out, n2_out, packed)
-                prof["plan_write"] += time.perf_counter() - tw
+                tq = time.perf_counter()
+                prof["pw_stats"] += tq - tr
+                prof["plan_write"] += tq - tw
             finally:
+                tf = time.perf_counter()
                 batch.free()
+                prof["free"] = prof.get("free", 0.0) + time.perf_counter() - tf
     finally:
         tw = time.perf_counter()
         marks.append(("loop", tw - _T_IMPORT))
@@ -488,37 +504,50 @@ def _round_stats(st1, st2, res, lens, m1, m2, b1, b2, s1, s2w, e2w, bp2_out, n2_
                                   np.where(two, p, np.where(p >= 0, s1[hit_all] + p, -1)))
         adj = np.full(n, 4, np.int64)
         adj[hit_all] = codes
-    # one stable sort groups the reads of every SP5 bin (ascending read index inside a bin, as
-    # a boolean mask of the bin would select them); per-bin sums are differences of cumsums
+    # every SP5 bin at once: per-bin sums are bincounts over the round-1 bin, the round-2
+    # histograms one unique over (bin1, adapter2, removed, errors) keys, sliced per bin (the
+    # statistics of a bin are those of the reads a boolean mask of the bin would select)
+    nb1, nb2 = len(st2), len(st2[0].adapters) if st2 else 0
     sel = np.nonzero(m1)[0]
-    grp = sel[np.argsort(b1[sel], kind="stable")]
-    edge = np.searchsorted(b1[grp], np.arange(len(st2) + 1))
+    bsel = b1[sel]
 
     def per_bin(v):
-        cs = np.concatenate(([0], np.cumsum(np.asarray(v, np.int64)[grp])))
-        return cs[edge[1:]] - cs[edge[:-1]]
+        w = np.asarray(v, np.int64)[sel]
+        return np.bincount(bsel, weights=w, minlength=nb1).round().astype(np.int64)
 
+    n_in = np.bincount(bsel, minlength=nb1)
     bp_in = per_bin(len1)
     n_rc = per_bin(rc2)
     bp_out = per_bin(np.where(m2, e2w - s2w, len1))
     r2 = res["m2_rstart"].astype(np.int64)
     err2 = res["m2_errors"].astype(np.int64)
+    hit = np.nonzero(m1 & m2)[0]
+    hb1, hb2 = b1[hit], b2[hit]
+    pair = hb1 * nb2 + hb2
+    cnt2 = np.bincount(pair, minlength=nb1 * nb2).reshape(nb1, nb2)
+    rcnt2 = np.bincount(pair[rc2[hit]], minlength=nb1 * nb2).reshape(nb1, nb2)
+    key = (hb1 << 48) | (hb2 << 40) | ((len1 - r2)[hit] << 8) | err2[hit]
+    u, c = np.unique(key, return_counts=True)
+    ue = np.searchsorted(u >> 48, np.arange(nb1 + 1))
+    adjc = None
+    if adj is not None:
+        adjc = np.bincount(pair * 5 + adj[hit], minlength=nb1 * nb2 * 5).reshape(nb1, nb2, 5)
+    low = (1 << 48) - 1
     for i, s in enumerate(st2):
-        g = grp[edge[i]:edge[i + 1]]
-        if not len(g):
+        if not n_in[i]:
             continue
-        s.n_in += len(g)
+        s.n_in += int(n_in[i])
         s.bp_in += int(bp_in[i])
-        hit = g[m2[g]]
-        s.n_with_adapter += len(hit)
+        s.n_with_adapter += int(cnt2[i].sum())
         s.n_rc += int(n_rc[i])
-        s.add_counts(b2[hit], rc2[hit], len(s.adapters))
-        s.add_matches(b2[hit], "back", len1[hit] - r2[hit], err2[hit])
-        if adj is not None:
-            s.add_adjacent(b2[hit], adj[hit])
+        s.add_count_vectors(cnt2[i], rcnt2[i])
+        if ue[i] < ue[i + 1]:
+            s.add_match_counts("back", u[ue[i]:ue[i + 1]] & low, c[ue[i]:ue[i + 1]])
+        if adjc is not None and cnt2[i].any():
+            s.add_adjacent_counts(adjc[i])
         # reads the per-call cutadapt would write (all of them: unknown included), before the
         # script's cleanup deletes files
-        n2_out[i] += len(g)
+        n2_out[i] += int(n_in[i])
         bp2_out[i] += int(bp_out[i])
 
 

@@ -100,13 +100,46 @@ class Stats:
         self.matches = defaultdict(int)
         self.on_rc = defaultdict(int)
         # adapter index -> part ("front"/"back") -> Counter{(removed length, errors): count}
-        self.hist = defaultdict(lambda: defaultdict(Counter))
+        self._hist = defaultdict(lambda: defaultdict(Counter))
         # adapter index -> counts of the base preceding a removed 3' adapter (ADJ_KEYS order)
-        self.adjacent = defaultdict(lambda: np.zeros(5, np.int64))
+        self._adjacent = defaultdict(lambda: np.zeros(5, np.int64))
+        # per-batch additions not folded into the dicts yet: (part, keys, counts) and a dense
+        # [adapter][5] count array (folding once per report instead of once per batch keeps
+        # the fused loop's per-batch statistics in numpy)
+        self._pend = []
+        self._pend_n = 0
+        self._adj_pend = None
         self.min_overlap = 3
 
+    @property
+    def hist(self):
+        self._fold()
+        return self._hist
+
+    @property
+    def adjacent(self):
+        self._fold()
+        return self._adjacent
+
+    def _fold(self):
+        if self._pend:
+            for part in sorted({p for p, _, _ in self._pend}):
+                ks = [k for p, k, _ in self._pend if p == part]
+                cs = [c for p, _, c in self._pend if p == part]
+                u, inv = np.unique(np.concatenate(ks), return_inverse=True)
+                tot = np.zeros(len(u), np.int64)
+                np.add.at(tot, inv, np.concatenate(cs).astype(np.int64))
+                for k, n in zip(u.tolist(), tot.tolist()):
+                    self._hist[k >> 40][part][((k >> 8) & ((1 << 32) - 1), k & 255)] += n
+            self._pend = []
+            self._pend_n = 0
+        if self._adj_pend is not None:
+            for a in np.nonzero(self._adj_pend.sum(axis=1))[0].tolist():
+                self._adjacent[a] += self._adj_pend[a]
+            self._adj_pend = None
+
     def add_match(self, a: int, rc: bool, part: str, removed: int, errors: int):
-        self.hist[a][part][(int(removed), int(errors))] += 1
+        self.add_matches(np.array([a]), part, np.array([removed]), np.array([errors]))
 
     def add_matches(self, a, part: str, removed, errors):
         """Vectorised add_match for arrays of adapter index / removed length / errors."""
@@ -115,8 +148,15 @@ class Stats:
             return
         key = (a << 40) | (np.asarray(removed, np.int64) << 8) | np.asarray(errors, np.int64)
         u, c = np.unique(key, return_counts=True)
-        for k, n in zip(u.tolist(), c.tolist()):
-            self.hist[k >> 40][part][((k >> 8) & ((1 << 32) - 1), k & 255)] += n
+        self.add_match_counts(part, u, c)
+
+    def add_match_counts(self, part: str, keys, counts):
+        """Histogram entries as keys adapter << 40 | removed length << 8 | errors with their
+        counts (folded into `hist` when it is read)."""
+        self._pend.append((part, np.asarray(keys, np.int64), np.asarray(counts, np.int64)))
+        self._pend_n += len(keys)
+        if self._pend_n > (1 << 22):
+            self._fold()
 
     def add_adjacent(self, a, codes):
         """Bases (view_codes) preceding removed 3' adapters of adapters `a`."""
@@ -124,20 +164,32 @@ class Stats:
         if not len(a):
             return
         key = a * 5 + np.asarray(codes, np.int64)
-        u, c = np.unique(key, return_counts=True)
-        for k, n in zip(u.tolist(), c.tolist()):
-            self.adjacent[k // 5][k % 5] += n
+        self.add_adjacent_counts(np.bincount(key, minlength=5 * len(self.adapters))
+                                 .reshape(-1, 5))
+
+    def add_adjacent_counts(self, counts):
+        """A dense [adapter][5] array of preceding-base counts (ADJ_KEYS order)."""
+        counts = np.asarray(counts, np.int64)
+        if self._adj_pend is None:
+            self._adj_pend = np.zeros((max(len(self.adapters), len(counts)), 5), np.int64)
+        if len(counts) > len(self._adj_pend):
+            grown = np.zeros((len(counts), 5), np.int64)
+            grown[:len(self._adj_pend)] = self._adj_pend
+            self._adj_pend = grown
+        self._adj_pend[:len(counts)] += counts
 
     def add_counts(self, bins, rc, n_adapters: int):
         """Per-adapter totals from arrays of matched adapter index and RC flag."""
         bins = np.asarray(bins, np.int64)
-        m = np.bincount(bins, minlength=n_adapters)
-        r = np.bincount(bins[np.asarray(rc, bool)], minlength=n_adapters)
-        for a in range(n_adapters):
-            if m[a]:
-                self.matches[a] += int(m[a])
-            if r[a]:
-                self.on_rc[a] += int(r[a])
+        self.add_count_vectors(np.bincount(bins, minlength=n_adapters),
+                               np.bincount(bins[np.asarray(rc, bool)], minlength=n_adapters))
+
+    def add_count_vectors(self, m, r):
+        """Per-adapter match and reverse-complement totals as count vectors."""
+        for a in np.nonzero(m)[0].tolist():
+            self.matches[a] += int(m[a])
+        for a in np.nonzero(r)[0].tolist():
+            self.on_rc[a] += int(r[a])
 
     def check_totals(self, totals):
         """Per-adapter match totals counted on the GPU(s) (dmx_counts, all-reduced over devices)
