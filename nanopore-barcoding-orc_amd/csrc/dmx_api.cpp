@@ -314,7 +314,7 @@ int dmx_open(int device, dmx_ctx** out) {
     const char* rs = std::getenv("DMX_RESOLVE");
     c->force_ring = rs && std::strcmp(rs, "ring") == 0;
     const char* stg = std::getenv("DMX_STAGE");   // A/B: window code slots
-    c->use_stage = stg && stg[0] == '1';
+    c->use_stage = DMX_STAGE_SLOTS && stg && stg[0] == '1';
     const char* ns = std::getenv("DMX_NO_SCREEN");   // A/B: no index screen before the
     c->no_screen = ns && ns[0] == '1';               // window scan
     const char* s1 = std::getenv("DMX_SCREEN_V1");   // A/B: the unpacked index screen

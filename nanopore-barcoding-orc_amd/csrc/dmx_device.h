@@ -376,6 +376,13 @@ struct Packed {
 // no-match bits of columns base + 32 i .., 12: base, 13: columns filled (16 per gathered chunk).
 // A window, task or candidate names its slot in the top bits of its `off` (slot + 1, 0 = none).
 constexpr int kStageWords = 16;
+// Window code slots are an A/B build (make variant NAME=stage
+// DEFS=-DDMX_STAGE_SLOTS=1, then DMX_STAGE=1 at run time): measured slower, and compiled in they
+// cost every gathering stage registers for the slot test (window scan 43 instead of 31 spilled
+// VGPRs at 4 waves, index screen 7 instead of 2, band list 0 18 instead of 2).
+#ifndef DMX_STAGE_SLOTS
+#define DMX_STAGE_SLOTS 0
+#endif
 constexpr int kOffBits = 36;                              // batch nt offsets < 2^36
 constexpr uint64_t kOffMask = (1ull << kOffBits) - 1ull;
 

@@ -94,9 +94,9 @@ struct TaskView {
 // A record's `off` field -> the view's first nt and its window code slot (kStageWords).
 __device__ __forceinline__ void view_off(const Packed& pk, uint64_t off, TaskView& tv) {
     tv.off = off & kOffMask;
-    tv.tag = (uint32_t)(off >> kOffBits);
+    tv.tag = DMX_STAGE_SLOTS ? (uint32_t)(off >> kOffBits) : 0u;
     tv.sbl = 0;
-    if (tv.tag) {
+    if (DMX_STAGE_SLOTS && tv.tag) {
         const uint2 h = *reinterpret_cast<const uint2*>(pk.stage + (size_t)(tv.tag - 1) *
                                                                       kStageWords + 12);
         tv.sbl = (h.x + kViewReachPre) | (h.y << 24);
@@ -107,7 +107,7 @@ __device__ __forceinline__ void view_off(const Packed& pk, uint64_t off, TaskVie
 // codes and no-match bits as the gather (wstage_kernel filled the slot with fetch16s).
 __device__ __forceinline__ bool staged16(const Packed& pk, const TaskView& tv, int p, bool mask,
                                          uint32_t& codes, uint32_t& nbits) {
-    if (!tv.tag) return false;
+    if (!DMX_STAGE_SLOTS || !tv.tag) return false;
     const int rel = p + kViewReachPre - (int)(tv.sbl & 0xFFFFFFu);
     if (rel < 0 || rel + 16 > (int)(tv.sbl >> 24)) return false;
     const uint32_t* sl = pk.stage + (size_t)(tv.tag - 1) * kStageWords;
@@ -488,6 +488,60 @@ __device__ __forceinline__ void fetch16s(const Packed& pk, const TaskView& tv, i
     }
 }
 
+// fetch16s in two halves (round 6).  fetch16s branches on the lane's strand and finishes the
+// gathered words inside each branch (shift, pair reversal, complement), so the compiler waits
+// for the gather right where it is issued (`s_waitcnt vmcnt(0)` in both branches): the loops'
+// "next chunks in flight" were never in flight, and every chunk cost a full memory round trip.
+// chunk16_load only issues the 8-byte gathers (no branch on the strand, the words unused), and
+// chunk16_codes finishes them when the chunk is consumed, one chunk later.  Same positions,
+// same clamp, same bits as fetch16s.
+struct Chunk16 {
+    uint64_t c = 0, m = 0;   // words q, q + 1 of the codes and of the no-match mask
+};
+// Lowest batch nt of view positions [p, p + 16) (fetch16s' g / b).
+__device__ __forceinline__ int64_t chunk16_pos(const TaskView& tv, int p) {
+    p = max(p, -kViewReachPre);
+    const int64_t f = (int64_t)tv.off + (int64_t)tv.start + p;
+    const int64_t b = (int64_t)tv.off + (int64_t)tv.n - 1 - (int64_t)tv.start - p - 15;
+    return tv.strand ? b : f;
+}
+__device__ __forceinline__ uint64_t load8(const uint32_t* __restrict__ w, int64_t q,
+                                          const Bounds& bd, uint32_t buf) {
+#ifdef DMX_DEBUG_BOUNDS
+    if (!bchk(bd, q, bd.lo, bd.hi - 1, buf)) return 0ull;
+#else
+    (void)bd, (void)buf;
+#endif
+    uint64_t v;
+    __builtin_memcpy(&v, w + q, 8);
+    return v;
+}
+template <bool MASK = true>
+__device__ __forceinline__ Chunk16 chunk16_load(const Packed& pk, const TaskView& tv, int p) {
+    const int64_t g = chunk16_pos(tv, p);
+    Chunk16 r;
+    r.c = load8(pk.seq, (2 * g) >> 5, pk.bd, kBufSeq);
+    if (MASK && !tv.clean) r.m = load8(pk.nmask, g >> 5, pk.bd, kBufMask);
+    return r;
+}
+template <bool MASK = true>
+__device__ __forceinline__ void chunk16_codes(const TaskView& tv, int p, const Chunk16& r,
+                                              uint32_t& codes, uint32_t& nbits) {
+    // only the low 5 bits of the position matter here: 32-bit arithmetic
+    const int pc = max(p, -kViewReachPre);
+    const uint32_t f = (uint32_t)tv.off + tv.start + (uint32_t)pc;
+    const uint32_t b = (uint32_t)tv.off + tv.n - 1u - tv.start - (uint32_t)pc - 15u;
+    const uint32_t g = tv.strand ? b : f;
+    const uint32_t c = (uint32_t)(r.c >> ((2u * g) & 31u));
+    codes = tv.strand ? ~rev_pairs(c) : c;
+    if (MASK) {
+        const uint32_t m = (uint32_t)(r.m >> (g & 31u));
+        nbits = tv.strand ? __brev(m) >> 16 : m & 0xFFFFu;
+    } else {
+        nbits = 0u;
+    }
+}
+
 // The no-match bits of view positions [p, p + 32) (the filter's clean-flag history).
 __device__ __forceinline__ uint32_t mask32s(const Packed& pk, const TaskView& tv, int p) {
     if (tv.strand == 0) return mask32(pk, (int64_t)tv.off + (int64_t)tv.start + p);
@@ -680,17 +734,12 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
     };
 
     uint32_t p0 = js;
-    uint32_t ncodes, nnb, ncodes2 = 0, nnb2 = 0;   // the next two chunks, in flight
-    const bool lm = !tv.clean;                      // clean windows: codes only
-    fetch16t(R.pk, tv, p0, ncodes, nnb, lm);
-    if (p0 + 16 < jhi)
-        fetch16t(R.pk, tv, p0 + 16, ncodes2, nnb2, lm);
+    // the next chunk in flight (clean windows: codes only, chunk16_load skips the mask)
+    Chunk16 nx = chunk16_load(R.pk, tv, (int)p0);
     for (; p0 + 16 <= jhi; p0 += 16) {
-        const uint32_t codes = ncodes, nb = nnb;
-        ncodes = ncodes2;
-        nnb = nnb2;
-        if (p0 + 32 < jhi)
-            fetch16t(R.pk, tv, p0 + 32, ncodes2, nnb2, lm);
+        uint32_t codes, nb;
+        chunk16_codes(tv, (int)p0, nx, codes, nb);
+        if (p0 + 16 < jhi) nx = chunk16_load(R.pk, tv, (int)p0 + 16);
         if (segset && p0 + 16 >= seg + 64) {   // this chunk could overflow the 64-bit segment
             flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
             segset = false;
@@ -704,7 +753,8 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
         DMX_CAND_VISIT(16)
     }
     if (p0 < jhi) {
-        const uint32_t codes = ncodes, nb = nnb;
+        uint32_t codes, nb;
+        chunk16_codes(tv, (int)p0, nx, codes, nb);
         if (segset && p0 + 16 >= seg + 64) {
             flush_cands(sink, tv, item, sub, m, lbk, seg, cm, c0, c1, c2);
             segset = false;
@@ -2932,15 +2982,13 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                 tv.a = 0;
                 const char* qb = reinterpret_cast<const char*>(s_q);
                 const uint32_t q8 = 8u * (uint32_t)q;   // the lane's quad within a code row
-                uint32_t c0 = 0, n0 = 0, c1 = 0, n1 = 0;   // two chunks in flight
-                if (nch > 0) fetch16s<kNecessaryMask>(R.pk, tv, jb, c0, n0);
-                if (nch > 1) fetch16s<kNecessaryMask>(R.pk, tv, jb + 16, c1, n1);
+                Chunk16 nx;                                  // the next chunk, in flight
+                if (nch > 0) nx = chunk16_load<kNecessaryMask>(R.pk, tv, jb);
                 for (int kc = 0; kc < nch && (need & ~pass_m); ++kc) {
                     const int p0 = jb + 16 * kc;
-                    const uint32_t codes = c0, nb = n0;
-                    c0 = c1;
-                    n0 = n1;
-                    if (kc + 2 < nch) fetch16s<kNecessaryMask>(R.pk, tv, p0 + 32, c1, n1);
+                    uint32_t codes, nb;
+                    chunk16_codes<kNecessaryMask>(tv, p0, nx, codes, nb);
+                    if (kc + 1 < nch) nx = chunk16_load<kNecessaryMask>(R.pk, tv, p0 + 16);
                     const bool inR = rows && p0 + 16 >= xr_lo && p0 + 1 <= xrh;
                     const bool inE = lastc && p0 + 16 >= xe_lo;
                     const int qlo = min(inR ? xr_lo : (1 << 30), inE ? xe_lo : (1 << 30)) - p0 - 1;
@@ -3540,21 +3588,23 @@ __device__ __forceinline__ void band_dp2(const uint8_t* rm, const Packed& pk,
     // read codes of row i, cell k: view position i - 1 + dx - H + k; a 48-position window of
     // three 16-code words (w0 current, w1 next, w2 prefetched) advancing 16 rows at a time
     int base = dx - H;
-    uint32_t w0, n0, w1, n1, w2, n2;
-    fetch16s(pk, tv, base, w0, n0);
-    fetch16s(pk, tv, base + 16, w1, n1);
-    fetch16s(pk, tv, base + 32, w2, n2);
+    uint32_t w0, n0, w1, n1;
+    Chunk16 r2 = chunk16_load(pk, tv, base + 32);   // the third chunk stays in flight
+    {
+        const Chunk16 r0 = chunk16_load(pk, tv, base), r1 = chunk16_load(pk, tv, base + 16);
+        chunk16_codes(tv, base, r0, w0, n0);
+        chunk16_codes(tv, base + 16, r1, w1, n1);
+    }
     int o = 0;
     uint32_t rnext = rm[0];           // rm[i * kMaxAdapters]: row i's match mask (row-major table)
     for (int i = 1; i <= ie; ++i) {
         if (o == 16) {                 // uniform: every lane advances one row per iteration
             w0 = w1;
             n0 = n1;
-            w1 = w2;
-            n1 = n2;
+            chunk16_codes(tv, base + 32, r2, w1, n1);
             base += 16;
             // the band's last cell reads view position dx - H + ie + W - 2: no fetch past it
-            if (base + 32 <= dx - H + ie + W - 2) fetch16s(pk, tv, base + 32, w2, n2);
+            if (base + 32 <= dx - H + ie + W - 2) r2 = chunk16_load(pk, tv, base + 32);
             o = 0;
         }
         const uint32_t codes = o ? __builtin_amdgcn_alignbit(w1, w0, 2 * o) : w0;
@@ -3631,10 +3681,13 @@ __device__ __forceinline__ void band_dp_fast(const uint8_t* rm, const Packed& pk
 #pragma unroll
     for (int k = 0; k < W; ++k) S[k] = (uint32_t)k << 3;   // row 0: free start, cost 0
     int base = dx - H;
-    uint32_t w0, n0, w1, n1, w2, n2;
-    fetch16s(pk, tv, base, w0, n0);
-    fetch16s(pk, tv, base + 16, w1, n1);
-    fetch16s(pk, tv, base + 32, w2, n2);
+    uint32_t w0, n0, w1, n1;
+    Chunk16 r2 = chunk16_load(pk, tv, base + 32);   // the third chunk stays in flight
+    {
+        const Chunk16 r0 = chunk16_load(pk, tv, base), r1 = chunk16_load(pk, tv, base + 16);
+        chunk16_codes(tv, base, r0, w0, n0);
+        chunk16_codes(tv, base + 16, r1, w1, n1);
+    }
     n0 = spread_even(n0);
     n1 = spread_even(n1);
     int o = 0;
@@ -3643,10 +3696,11 @@ __device__ __forceinline__ void band_dp_fast(const uint8_t* rm, const Packed& pk
         if (o == 16) {                 // uniform: every lane advances one row per iteration
             w0 = w1;
             n0 = n1;
-            w1 = w2;
+            uint32_t n2;
+            chunk16_codes(tv, base + 32, r2, w1, n2);
             n1 = spread_even(n2);
             base += 16;
-            if (base + 32 <= dx - H + ie + W - 2) fetch16s(pk, tv, base + 32, w2, n2);
+            if (base + 32 <= dx - H + ie + W - 2) r2 = chunk16_load(pk, tv, base + 32);
             o = 0;
         }
         const uint32_t codes = o ? __builtin_amdgcn_alignbit(w1, w0, 2 * o) : w0;
@@ -4490,7 +4544,7 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     R.ftask_count = c->d_shard + (kShFtask + round) * kShards * kShardStride;
     R.ftask_scap = (uint32_t)(c->ftask_cap / kShards);
     // window code slots: band-mode window scans of this pipeline, offsets that leave tag bits
-    R.stage = (c->d_stage && !linked && hp.filter && band && c->use_stage &&
+    R.stage = (DMX_STAGE_SLOTS && c->d_stage && !linked && hp.filter && band && c->use_stage &&
                (uint64_t)c->n_words * 16 < (1ull << kOffBits))
                   ? c->d_stage : nullptr;
     R.stage_cap = (uint32_t)c->stage_cap;

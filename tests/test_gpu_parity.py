@@ -2,10 +2,10 @@
 
 Bit-exact on every field of every read: bins, RC flags, trim coordinates, scores, errors.
 """
+import os
+
 import numpy as np
 import pytest
-
-import os
 
 import oracle
 from dmx import lib, panel, synth
@@ -152,7 +152,11 @@ def test_error_rates_and_filter_toggle(ctx, e, monkeypatch):
 @pytest.mark.parametrize("config,seed", [("c2x24", 3), ("c4", 4)])
 def test_window_code_slots(config, seed, monkeypatch):
     """DMX_STAGE=1 (A/B): the screen, window scan and band read the codes of a
-    verified window from its slot instead of the packed batch; every byte stays the same."""
+    verified window from its slot instead of the packed batch; every byte stays the same.  The
+    slots are compiled only into the A/B build (make variant NAME=stage
+    DEFS=-DDMX_STAGE_SLOTS=1): run with DMX_LIBDMX=.../dmx/libdmx_stage.so DMX_TEST_STAGE_SLOTS=1."""
+    if os.environ.get("DMX_TEST_STAGE_SLOTS") != "1":
+        pytest.skip("window code slots are an A/B build (DMX_STAGE_SLOTS=1)")
     monkeypatch.setenv("DMX_STAGE", "1")
     d = synth.generate(config, n=6000, seed=seed)
     exp = _oracle_two_round(d)
