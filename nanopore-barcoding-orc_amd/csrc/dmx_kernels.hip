@@ -2018,9 +2018,26 @@ constexpr int kSbWords = kSuperNt / 16 + 8;   // LDS copy of a superblock: 4 wor
 // nt x + len - 1 + [dlo, dhi]; a copy of a strand-1 piece (the reverse complement) ends them, in a
 // strand-1 view that walks the batch backwards, at nt x - [dlo, dhi].  Every lane of the wave
 // calls it (valid: the lane holds a hit).
-__device__ __forceinline__ void flat_check(const RoundArgs& R, const PsTables& tb, uint64_t cw,
-                                           uint64_t X, bool valid) {
-    uint32_t* p1 = nullptr;   // the lane's first mark (deduplicated against the left lane's)
+// The four cell bitmaps' pointers held in scalar registers: readfirstlane keeps the compiler from
+// turning a per-lane select between them back into a per-lane load of RoundArgs::cells.
+typedef __attribute__((address_space(1))) uint32_t gu32;   // a global-memory word
+struct CellPtrs {
+    gu32* p[4];   // (global address space: a generic pointer would load through flat)
+    __device__ __forceinline__ explicit CellPtrs(const RoundArgs& R) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t v = reinterpret_cast<uint64_t>(R.cells[i]);
+            const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+            const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+            p[i] = reinterpret_cast<gu32*>(lo | (hi << 32));
+        }
+    }
+};
+
+__device__ __forceinline__ void flat_check(const RoundArgs& R, const CellPtrs& cp,
+                                           const PsTables& tb, uint64_t cw, uint64_t X,
+                                           bool valid) {
+    gu32* p1 = nullptr;       // the lane's first mark (deduplicated against the left lane's)
     uint32_t b1 = 0;
     if (valid) {
         const uint32_t kr = ps_key(tb, (uint32_t)(cw >> 6) & 0xFFFFu);
@@ -2041,7 +2058,10 @@ __device__ __forceinline__ void flat_check(const RoundArgs& R, const PsTables& t
             nlo = nlo < 0 ? 0 : nlo;
             nhi = nhi > last ? last : nhi;
             if (nlo > nhi) continue;
-            uint32_t* cells = R.cells[2 * (int)((ev >> 56) & 1u) + tau];
+            // the entry's round and strand pick one of four uniform pointers (indexing R.cells
+            // by a lane's value is a dependent load of the kernel argument)
+            const int ci = 2 * (int)((ev >> 56) & 1u) + tau;
+            gu32* cells = ci < 2 ? (ci == 0 ? cp.p[0] : cp.p[1]) : (ci == 2 ? cp.p[2] : cp.p[3]);
             for (int64_t c = nlo >> 4; c <= (nhi >> 4);) {   // one atomic per bitmap word
                 const int64_t w = c >> 5;
                 const int64_t cend = min(nhi >> 4, (w << 5) + 31);
@@ -2053,7 +2073,7 @@ __device__ __forceinline__ void flat_check(const RoundArgs& R, const PsTables& t
 #if defined(DMX_PS_AB) && DMX_PS_AB == 3   // timing A/B only: no marks
                     asm volatile("" ::"v"(bits), "v"(cells + w));
 #else
-                    atomicOr(cells + w, bits);
+                    __hip_atomic_fetch_or(cells + w, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
                 }
                 c = cend + 1;
@@ -2069,7 +2089,7 @@ __device__ __forceinline__ void flat_check(const RoundArgs& R, const PsTables& t
 #if defined(DMX_PS_AB) && DMX_PS_AB == 3
         asm volatile("" ::"v"(b1), "v"(p1));
 #else
-        atomicOr(p1, b1);
+        __hip_atomic_fetch_or(p1, b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
     }
 }
@@ -2082,6 +2102,7 @@ __global__ __launch_bounds__(kScanBlock) void pscan_kernel(RoundArgs R) {
     __shared__ uint16_t s_q[kScanBlock / 64][64];
     const PsTables tb = ps_load_tables(R.pieces, s_dyn);
     __syncthreads();
+    const CellPtrs cp(R);
     const int lane = (int)(threadIdx.x & 63u);
     uint32_t* const sbw = s_sb[threadIdx.x >> 6];   // [4 + k]: word k of the superblock
     uint16_t* const q = s_q[threadIdx.x >> 6];
@@ -2127,7 +2148,7 @@ __global__ __launch_bounds__(kScanBlock) void pscan_kernel(RoundArgs R) {
 #if defined(DMX_PS_AB) && DMX_PS_AB == 4   // timing A/B only: queue without checks
             asm volatile("" ::"v"(cw));
 #else
-            flat_check(R, tb, cw, C0 + p, v);
+            flat_check(R, cp, tb, cw, C0 + p, v);
 #endif
             __builtin_amdgcn_wave_barrier();
         }
@@ -2154,47 +2175,82 @@ __global__ __launch_bounds__(kScanBlock) void pcompact_kernel(RoundArgs R) {
     Window* const wbuf = R.win + wsh * R.win_scap;
     uint32_t* const wcnt = R.win_count + wsh * kShardStride;
     const uint32_t stride = gridDim.x * blockDim.x;
+    // Cells [k0, k0 + 64) of a view in view order come from three bitmap words.  They are
+    // loaded with no branch on the strand and finished where they are used, so the loads of
+    // both orientations' first 64 cells, and of a view's next 64 cells, are in flight together
+    // instead of one round trip each.  The bitmap of the lane's strand is a select between
+    // two uniform pointers (indexing R.cells by the lane's strand is a dependent global load).
+    const CellPtrs cp(R);
+    const gu32* const cb0 = cp.p[2 * R.round];
+    const gu32* const cb1 = cp.p[2 * R.round + 1];
+    struct View {
+        TaskView tv;
+        int64_t p0nt = 0;   // nt of view position 0
+        int delta = 0, ncell = 0, l = 0;
+        uint3 w = {0u, 0u, 0u};
+    };
+    const auto words = [&](const View& v, int k0, uint3& wv) __attribute__((always_inline)) {
+        const int64_t c0 = v.p0nt >> 4;
+        const int64_t cs = v.tv.strand ? c0 - k0 - 63 : c0 + k0;   // lowest cell
+        const gu32* cb = v.tv.strand ? cb1 : cb0;
+        // unconditional (word 0 when the cells are not needed: inside the bitmap's guard), so
+        // no merge with a default value waits for the load where it is issued
+        const int64_t w = k0 < v.ncell ? cs >> 5 : 0;              // floor
+        wv.x = cb[w];
+        wv.y = cb[w + 1];
+        wv.z = cb[w + 2];
+    };
+    const auto prep = [&](uint32_t item, bool act, int o, View& v) __attribute__((always_inline)) {
+        if (act) {
+            task_view(R, item, o * A, A, v.tv);
+            v.l = (int)v.tv.len;
+        }
+        // nt of view position 0 and the walk direction through the cells
+        v.p0nt = v.tv.strand ? (int64_t)v.tv.off + v.tv.n - 1 - v.tv.start
+                             : (int64_t)v.tv.off + v.tv.start;
+        v.delta = act ? (v.tv.strand ? 15 - (int)(v.p0nt & 15) : (int)(v.p0nt & 15)) : 0;
+        v.ncell = act && v.l > 0 ? (v.l + v.delta + 15) >> 4 : 0;   // cells of the view
+        words(v, 0, v.w);
+    };
+    const auto run = [&](uint32_t item, bool act, int o, const View& v) __attribute__((always_inline)) {
+        bool reached = false;
+        uint3 cur = v.w;
+        for (int k0 = 0; __ballot(k0 < v.ncell); k0 += 64) {
+            uint3 nx = {0u, 0u, 0u};
+            words(v, k0 + 64, nx);                                 // the next 64 cells, in flight
+            uint64_t m = 0;
+            if (k0 < v.ncell) {
+                // cells k0 .. k0 + 63 in view order = bitmap cells c0 + u (strand 0) or
+                // c0 - u (strand 1), c0 = the cell of view position 0
+                const int64_t c0 = v.p0nt >> 4;
+                const int64_t cs = v.tv.strand ? c0 - k0 - 63 : c0 + k0;   // lowest cell
+                const uint32_t sh = (uint32_t)(cs & 31);
+                const uint64_t lo = ((uint64_t)cur.y << 32) | cur.x;
+                const uint64_t x = sh ? (lo >> sh) | ((uint64_t)cur.z << (64 - sh)) : lo;
+                m = v.tv.strand ? __builtin_bitreverse64(x) : x;
+                if (front && k0 == 0)               // partial alignments from column 0
+                    m |= (fr + v.delta + 15) >> 4 >= 64 ? ~0ull
+                                                        : ((1ull << ((fr + v.delta + 15) >> 4)) - 1ull);
+                const int left = v.ncell - k0;
+                if (left < 64) m &= (1ull << left) - 1ull;
+                m |= ((m << 1) & (m >> 1)) | ((m << 1) & (m >> 2)) | ((m << 2) & (m >> 1));
+            }
+            PsRuns rr{m, k0, v.delta, v.l, W, SEG, 0, 0};
+            reached |= ps_emit(R, fbuf, fcnt, rr, item, o, v.tv);
+            cur = nx;
+        }
+        ps_lastcol(R, wbuf, wcnt, act && !front && !reached, item, o, v.tv, rb);
+    };
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n_items; i0 += stride) {   // wave-uniform
         const uint32_t item = i0 + threadIdx.x;
         const bool act = item < n_items;
-        for (int o = 0; o < no; ++o) {
-            TaskView tv;
-            int l = 0;
-            if (act) {
-                task_view(R, item, o * A, A, tv);
-                l = (int)tv.len;
-            }
-            // nt of view position 0 and the walk direction through the cells
-            const int64_t p0nt = tv.strand ? (int64_t)tv.off + tv.n - 1 - tv.start
-                                           : (int64_t)tv.off + tv.start;
-            const int delta = act ? (tv.strand ? 15 - (int)(p0nt & 15) : (int)(p0nt & 15)) : 0;
-            const int ncell = act && l > 0 ? (l + delta + 15) >> 4 : 0;   // cells of the view
-            bool reached = false;
-            for (int k0 = 0; __ballot(k0 < ncell); k0 += 64) {
-                uint64_t m = 0;
-                if (k0 < ncell) {
-                    // cells k0 .. k0 + 63 in view order = bitmap cells c0 + u (strand 0) or
-                    // c0 - u (strand 1), c0 = the cell of view position 0
-                    const int64_t c0 = p0nt >> 4;
-                    const int64_t cs = tv.strand ? c0 - k0 - 63 : c0 + k0;   // lowest cell
-                    const uint32_t* cb = R.cells[2 * R.round + (int)tv.strand];
-                    const int64_t w = cs >> 5;                               // floor
-                    const uint32_t sh = (uint32_t)(cs & 31);
-                    const uint64_t lo = ((uint64_t)cb[w + 1] << 32) | cb[w];
-                    const uint64_t v = sh ? (lo >> sh) | ((uint64_t)cb[w + 2] << (64 - sh)) : lo;
-                    m = tv.strand ? __builtin_bitreverse64(v) : v;
-                    if (front && k0 == 0)               // partial alignments from column 0
-                        m |= (fr + delta + 15) >> 4 >= 64 ? ~0ull
-                                                          : ((1ull << ((fr + delta + 15) >> 4)) - 1ull);
-                    const int left = ncell - k0;
-                    if (left < 64) m &= (1ull << left) - 1ull;
-                    m |= ((m << 1) & (m >> 1)) | ((m << 1) & (m >> 2)) | ((m << 2) & (m >> 1));
-                }
-                PsRuns rr{m, k0, delta, l, W, SEG, 0, 0};
-                reached |= ps_emit(R, fbuf, fcnt, rr, item, o, tv);
-            }
-            ps_lastcol(R, wbuf, wcnt, act && !front && !reached, item, o, tv, rb);
-        }
+        View v0, v1;   // (no branch on `no`: a merge there made the first loads wait)
+        v0.tv.strand = v1.tv.strand = 0;
+        const bool act1 = act && no > 1;
+        prep(item, act, 0, v0);
+        prep(item, act1, 1, v1);
+        run(item, act, 0, v0);
+        run(item, act1, 1, v1);
     }
 }
 
