@@ -91,6 +91,34 @@ struct TaskView {
     uint32_t sbl = 0;     // the slot's base column + kViewReachPre (bits 0..23), filled columns
 };
 
+// A pointer moved into SGPRs (readfirstlane) in the global address space: a per-lane select
+// between such pointers stays a select, where the compiler turns a per-lane index into a
+// RoundArgs pointer array into a dependent load of the kernel argument.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* sgpr_ptr(T* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<__attribute__((address_space(1))) T*>(lo | (hi << 32));
+}
+
+// cd into p[i] through a global-address-space pointer (two 16-B and one 8-B store).
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void store_cand(__attribute__((address_space(1))) Cand* p, uint32_t i,
+                                           const Cand& cd) {
+    static_assert(sizeof(Cand) == 40, "Cand layout");
+    u32x4_t a, b;
+    u32x2_t c;
+    __builtin_memcpy(&a, reinterpret_cast<const char*>(&cd), 16);
+    __builtin_memcpy(&b, reinterpret_cast<const char*>(&cd) + 16, 16);
+    __builtin_memcpy(&c, reinterpret_cast<const char*>(&cd) + 32, 8);
+    auto* d = reinterpret_cast<__attribute__((address_space(1))) char*>(p + i);
+    *reinterpret_cast<__attribute__((address_space(1))) u32x4_t*>(d) = a;
+    *reinterpret_cast<__attribute__((address_space(1))) u32x4_t*>(d + 16) = b;
+    *reinterpret_cast<__attribute__((address_space(1))) u32x2_t*>(d + 32) = c;
+}
+
 // A record's `off` field -> the view's first nt and its window code slot (kStageWords).
 __device__ __forceinline__ void view_off(const Packed& pk, uint64_t off, TaskView& tv) {
     tv.off = off & kOffMask;
@@ -190,9 +218,27 @@ __device__ __forceinline__ uint32_t slot_of(const RoundArgs& R, uint32_t item, i
 constexpr int kPeqStride = kMaxAdapters + 24;
 constexpr int kIpeqStride = 9;   // index screen: words per adapter (4 codes + bank padding)
 
+// An adapter's length, k, end and kk (DevAdapter's four bytes m, k, where, kk): what the scans
+// need per task, held in LDS by the kernels (a per-lane read of DevAdapter is a global load the
+// task's first gather waits behind).
+struct AdLite {
+    int m, k, kk;
+    bool front;
+};
+__device__ __forceinline__ uint32_t ad_word(const DevAdapter& ad) {
+    return (uint32_t)ad.m | ((uint32_t)ad.k << 8) | ((uint32_t)ad.where << 16) |
+           ((uint32_t)(uint8_t)ad.kk << 24);
+}
+__device__ __forceinline__ AdLite ad_lite(uint32_t w) {
+    return AdLite{(int)(w & 255u), (int)((w >> 8) & 255u), (int)(int8_t)(w >> 24),
+                  ((w >> 16) & 255u) == kFront};
+}
+__device__ __forceinline__ AdLite ad_lite(const DevAdapter& ad) { return ad_lite(ad_word(ad)); }
+
 __device__ __forceinline__ void load_panel_lds(const DevPanel* P, uint64_t* s_peq, int8_t* s_acc,
-                                               int8_t* s_pacc) {
+                                               int8_t* s_pacc, uint32_t* s_amk) {
     const int A = P->n_adapters;
+    for (int a = threadIdx.x; a < A; a += blockDim.x) s_amk[a] = ad_word(P->ad[a]);
     for (int x = threadIdx.x; x < 8 * A; x += blockDim.x) {
         const int c = x / A, a = x % A;   // code-major, power-of-two row stride (no multiply)
         s_peq[c * kPeqStride + a] = P->ad[a].peq[c];   // lanes of one read: consecutive words
@@ -250,12 +296,12 @@ __device__ __forceinline__ bool beats_lb(int lbk, int ub, int o, int cost) {
 // >= js + m + k + 1.  Emits clusters; returns this task's score lower bound.
 __device__ __forceinline__ int scan_task(const RoundArgs& R, const Stage<Cluster>& st,
                                          const TaskView& tv, uint32_t item, int sub,
-                                         const uint64_t* peq, int A, const DevAdapter& ad,
+                                         const uint64_t* peq, int A, AdLite ad,
                                          const int8_t* acc, const int8_t* pacc, uint32_t js,
                                          bool real, uint32_t jlo, uint32_t jhi, bool lastcol) {
     const int m = ad.m;
     const int kk = ad.kk;
-    const bool front = ad.where == kFront;
+    const bool front = ad.front;
     const uint32_t hbit = (uint32_t)(m - 1);
     const uint32_t gap = (uint32_t)(m + ad.k + 1);
 
@@ -637,9 +683,13 @@ __device__ __forceinline__ void emit_cands(const RoundArgs& R, const CandOut& co
     }
     b0 = __builtin_amdgcn_readfirstlane(b0) + (pre & 0xFFFFu);
     b1 = __builtin_amdgcn_readfirstlane(b1) + (pre >> 16);
+    // the lane's list picks one of two pointers held in SGPRs (R.cand[l] with a per-lane l is a
+    // dependent load of the kernel argument before every store)
+    __attribute__((address_space(1))) Cand* const cl0 = sgpr_ptr(R.cand[0] + sh * R.cand_scap);
+    __attribute__((address_space(1))) Cand* const cl1 = sgpr_ptr(R.cand[1] + sh * R.cand_scap);
     const auto put = [&](int l, const Cand& cd) __attribute__((always_inline)) {
         const uint32_t i = l ? b1++ : b0++;
-        if (i < R.cand_scap) R.cand[l][sh * R.cand_scap + i] = cd;
+        if (i < R.cand_scap) store_cand(l ? cl1 : cl0, i, cd);
         else atomicOr(R.flags, 8u);
     };
     uint64_t x = co.cells;
@@ -667,14 +717,14 @@ __device__ __forceinline__ void emit_cands(const RoundArgs& R, const CandOut& co
 template <int HB, class Sink, int PSTRIDE = kPeqStride, bool ZROW = false>
 __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink& sink,
                                                  const TaskView& tv, uint32_t item, int sub,
-                                                 const uint64_t* peq, int A, const DevAdapter& ad,
+                                                 const uint64_t* peq, int A, AdLite ad,
                                                  const int8_t* acc, const int8_t* pacc,
                                                  uint32_t js, bool real, uint32_t jlo,
                                                  uint32_t jhi, bool lastcol,
                                                  CandOut* out = nullptr) {
     const int m = ad.m;
     const int kk = ad.kk;   // <= 7 in band mode (three cost planes)
-    const bool front = ad.where == kFront;
+    const bool front = ad.front;
     const uint32_t hbit = (uint32_t)(m - 1);
 
     uint64_t pv = (front && real) ? 0ull : ~0ull, mv = 0ull;
@@ -854,7 +904,7 @@ __device__ __forceinline__ int scan_task_cand_hb(const RoundArgs& R, const Sink&
 template <class Sink, int PSTRIDE = kPeqStride, bool ZROW = false>
 __device__ __forceinline__ int scan_task_cand(const RoundArgs& R, const Sink& sink,
                                               const TaskView& tv, uint32_t item, int sub,
-                                              const uint64_t* peq, int A, const DevAdapter& ad,
+                                              const uint64_t* peq, int A, AdLite ad,
                                               const int8_t* acc, const int8_t* pacc,
                                               uint32_t js, bool real, uint32_t jlo,
                                               uint32_t jhi, bool lastcol,
@@ -917,8 +967,9 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
     __shared__ uint64_t s_peq[8 * kPeqStride];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
     __shared__ int8_t s_pacc[72 * kMaxAdapters];
+    __shared__ uint32_t s_amk[kMaxAdapters];
     DMX_STAGES
-    load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
+    load_panel_lds(R.panel, s_peq, s_acc, s_pacc, s_amk);
     __syncthreads();
 
     const int A = R.panel->n_adapters;
@@ -933,10 +984,10 @@ __global__ __launch_bounds__(kScanBlock) void scan_kernel(RoundArgs R) {
         task_view(R, item, sub, A, tv);
         int lb;
         if constexpr (BAND)
-            lb = scan_task_cand(R, sink, tv, item, sub, s_peq + tv.a, A, R.panel->ad[tv.a],
+            lb = scan_task_cand(R, sink, tv, item, sub, s_peq + tv.a, A, ad_lite(s_amk[tv.a]),
                                 s_acc + 72 * tv.a, s_pacc + 72 * tv.a, 0, true, 1, tv.len, true);
         else
-            lb = scan_task(R, st, tv, item, sub, s_peq + tv.a, A, R.panel->ad[tv.a],
+            lb = scan_task(R, st, tv, item, sub, s_peq + tv.a, A, ad_lite(s_amk[tv.a]),
                            s_acc + 72 * tv.a, s_pacc + 72 * tv.a, 0, true, 1, tv.len, true);
         const uint32_t slot = slot_of(R, item, sub);
         if (lb > 0 && DMX_BOUND(R.pk.bd, slots, slot, kBufSlot)) atomicMax(&R.lb[slot], lb);
@@ -2025,12 +2076,7 @@ struct CellPtrs {
     gu32* p[4];   // (global address space: a generic pointer would load through flat)
     __device__ __forceinline__ explicit CellPtrs(const RoundArgs& R) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint64_t v = reinterpret_cast<uint64_t>(R.cells[i]);
-            const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-            const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-            p[i] = reinterpret_cast<gu32*>(lo | (hi << 32));
-        }
+        for (int i = 0; i < 4; ++i) p[i] = sgpr_ptr(R.cells[i]);
     }
 };
 
@@ -2400,17 +2446,18 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
         __syncthreads();                           // (also: the last group's s_ord)
         constexpr int PER = kSortGroup / kScanBlock;
         uint32_t key[PER], pos[PER];
+        // every record's fields first (unconditional loads, clamped index: all in flight at
+        // once), then the bin counts
 #pragma unroll
         for (int e = 0; e < PER; ++e) {
             const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
-            key[e] = 0;
-            if (li < gn) {
-                const Window* w = R.win + sm.phys(gb + li);
-                const int span = (int)w->j2 - (int)w->j1;   // the rows range grows with it
-                key[e] = (uint32_t)min(max(span, 0) >> kSortShift, kSortBins - 1);
-                pos[e] = atomicAdd(&s_bin[key[e]], 1u);
-            }
+            const Window* w = R.win + sm.phys(gb + min(li, gn - 1u));
+            const int span = (int)w->j2 - (int)w->j1;   // the rows range grows with it
+            key[e] = (uint32_t)min(max(span, 0) >> kSortShift, kSortBins - 1);
         }
+#pragma unroll
+        for (int e = 0; e < PER; ++e)
+            if (threadIdx.x + (uint32_t)e * kScanBlock < gn) pos[e] = atomicAdd(&s_bin[key[e]], 1u);
         __syncthreads();
         if (threadIdx.x == 0) {                    // exclusive scan over the bins
             uint32_t acc = 0;
@@ -2923,18 +2970,19 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
         __syncthreads();                           // (also: the last group's s_ord)
         constexpr int PER = kSortGroup / kScanBlock;
         uint32_t key[PER], pos[PER];
+        // every record's fields first (unconditional loads, clamped index: all in flight at
+        // once), then the bin counts
 #pragma unroll
         for (int e = 0; e < PER; ++e) {
             const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
-            key[e] = 0;
-            if (li < gn) {
-                const Window* w = wl + sm.phys((gb + li) / (uint32_t)Q);
-                const int j1 = (int)w->j1, j2 = (int)w->j2;
-                const int span = w->bmin != 255 ? j2 - max(j1, jsplit) : -1;
-                key[e] = span < 0 ? 0u : 1u + (uint32_t)min(span >> kSortShift, kSortBins - 2);
-                pos[e] = atomicAdd(&s_bin[key[e]], 1u);
-            }
+            const Window* w = wl + sm.phys((gb + min(li, gn - 1u)) / (uint32_t)Q);
+            const int j1 = (int)w->j1, j2 = (int)w->j2;
+            const int span = w->bmin != 255 ? j2 - max(j1, jsplit) : -1;
+            key[e] = span < 0 ? 0u : 1u + (uint32_t)min(span >> kSortShift, kSortBins - 2);
         }
+#pragma unroll
+        for (int e = 0; e < PER; ++e)
+            if (threadIdx.x + (uint32_t)e * kScanBlock < gn) pos[e] = atomicAdd(&s_bin[key[e]], 1u);
         __syncthreads();
         if (threadIdx.x == 0) {                    // exclusive scan over the bins
             uint32_t acc = 0;
@@ -3169,9 +3217,9 @@ constexpr int kLaneRows = 5;
 template <bool BAND, class ClStage, class Sink>
 __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, int a, int A,
                                            const uint64_t* s_peq, const int8_t* s_acc,
-                                           const int8_t* s_pacc, const ClStage& st,
-                                           const Sink& sink, CandOut& co, TaskView& tv,
-                                           int& sub, uint64_t* lrow) {
+                                           const int8_t* s_pacc, const uint32_t* s_amk,
+                                           const ClStage& st, const Sink& sink, CandOut& co,
+                                           TaskView& tv, int& sub, uint64_t* lrow) {
     sub = w.o * A + a;
     tv.read = 0;
     tv.n = w.n;
@@ -3182,8 +3230,8 @@ __device__ __forceinline__ void wscan_task(const RoundArgs& R, const Window& w, 
     view_off(R.pk, w.off, tv);
     tv.o = w.o;
     tv.a = a;
-    const DevAdapter& ad = R.panel->ad[a];
-    int js = (int)w.j1 - (int)ad.m - (int)ad.k - 1;
+    const AdLite ad = ad_lite(s_amk[a]);
+    int js = (int)w.j1 - ad.m - ad.k - 1;
     const bool real = js <= 0;
     if (real) js = 0;
     int lb;
@@ -3217,6 +3265,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
     __shared__ uint64_t s_peq[8 * kPeqStride];
     __shared__ int8_t s_acc[72 * kMaxAdapters];
     __shared__ int8_t s_pacc[72 * kMaxAdapters];
+    __shared__ uint32_t s_amk[kMaxAdapters];
     __shared__ Cluster s_cl[BAND ? 1 : kStageCap];
     __shared__ uint32_t s_clcnt, s_clbase;
     __shared__ Cand s_wcand[BAND ? kScanBlock / 64 : 1][2][kWaveCandCap];
@@ -3243,7 +3292,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                                                            R.cand[1] + wsh * R.cand_scap,
                                                            R.cand_count + (kShards + wsh) * kShardStride,
                                                            R.cand_scap, R.flags, 8u}}};
-    load_panel_lds(R.panel, s_peq, s_acc, s_pacc);
+    load_panel_lds(R.panel, s_peq, s_acc, s_pacc, s_amk);
     __shared__ uint32_t s_spre[kShards + 1];
     ShardMap sm{s_spre, 0u};
     const Window* wl = R.panel->pre_len ? R.win2 : R.win;
@@ -3275,18 +3324,20 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             __syncthreads();                       // (also: s_mk, and the last group's s_ord)
             constexpr int PER = kSortGroup / kScanBlock;
             uint32_t key[PER], pos[PER];
+            // every record's fields first (unconditional loads, clamped index: all in flight at
+            // once), then the bin counts
 #pragma unroll
             for (int e = 0; e < PER; ++e) {
                 const uint32_t li = threadIdx.x + (uint32_t)e * kScanBlock;
-                key[e] = 0;
-                if (li < gn) {
-                    const Window* w = tl + sm.phys(gb + li);
-                    const int j1 = (int)w->j1, j2 = (int)w->j2, a = (int)w->info;
-                    const int cols = j2 - max(j1 - (int)s_mk[a], 0);
-                    key[e] = (uint32_t)min(max(cols, 0) >> kSortShift, kSortBins - 1);
-                    pos[e] = atomicAdd(&s_bin[key[e]], 1u);
-                }
+                const Window* w = tl + sm.phys(gb + min(li, gn - 1u));
+                const int j1 = (int)w->j1, j2 = (int)w->j2, a = (int)w->info;
+                const int cols = j2 - max(j1 - (int)s_mk[a], 0);
+                key[e] = (uint32_t)min(max(cols, 0) >> kSortShift, kSortBins - 1);
             }
+#pragma unroll
+            for (int e = 0; e < PER; ++e)
+                if (threadIdx.x + (uint32_t)e * kScanBlock < gn)
+                    pos[e] = atomicAdd(&s_bin[key[e]], 1u);
             __syncthreads();
             if (threadIdx.x == 0) {                // exclusive scan over the bins
                 uint32_t acc = 0;
@@ -3313,11 +3364,11 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
                 if (li < gn) {
                     const Window w = tl[sm.phys(gb + (sorted ? s_ord[li] : li))];
                     item = w.item;
-                    wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, st, sink, co,
+                    wscan_task<BAND>(R, w, (int)w.info, A, s_peq, s_acc, s_pacc, s_amk, st, sink, co,
                                      tv, sub, lrow);
                 }
                 if constexpr (BAND) {
-                    emit_cands(R, co, tv, item, sub, R.panel->ad[tv.a].m);
+                    emit_cands(R, co, tv, item, sub, (int)(s_amk[tv.a] & 255u));
                     __builtin_amdgcn_wave_barrier();
                     if (sink.st[0].count() > DMX_WAVE_CAND_FLUSH) sink.st[0].flush();
                     if (sink.st[1].count() > DMX_WAVE_CAND_FLUSH) sink.st[1].flush();
@@ -3348,10 +3399,11 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(DMX_
             const Window w = wl[sm.phys((uint32_t)(t / A))];
             const int a = (int)(t % A);
             item = w.item;
-            wscan_task<BAND>(R, w, a, A, s_peq, s_acc, s_pacc, st, sink, co, tv, sub, lrow);
+            wscan_task<BAND>(R, w, a, A, s_peq, s_acc, s_pacc, s_amk, st, sink, co, tv, sub,
+                             lrow);
         }
         if constexpr (BAND) {                        // wave-uniform: no block barrier
-            emit_cands(R, co, tv, item, sub, R.panel->ad[tv.a].m);
+            emit_cands(R, co, tv, item, sub, (int)(s_amk[tv.a] & 255u));
             __builtin_amdgcn_wave_barrier();
             if (sink.st[0].count() > DMX_WAVE_CAND_FLUSH) sink.st[0].flush();
             if (sink.st[1].count() > DMX_WAVE_CAND_FLUSH) sink.st[1].flush();
@@ -3836,8 +3888,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     __shared__ uint32_t s_sorted[256];
     __shared__ uint8_t s_sc[256];
     __shared__ uint32_t s_hist[8], s_nq[2], s_n;
+    __shared__ uint32_t s_amk[kMaxAdapters];         // ad_word per adapter
+    __shared__ int8_t s_bacc[72 * kMaxAdapters];     // acc tables
     const DevPanel* P = R.panel;
     const int A = P->n_adapters;
+    for (int a = threadIdx.x; a < A; a += blockDim.x) s_amk[a] = ad_word(P->ad[a]);
+    for (int x = threadIdx.x; x < 72 * A; x += blockDim.x) s_bacc[x] = P->ad[x / 72].acc[x % 72];
     // bits 0-3: codes adapter char i matches; bits 4-5: that code when it is exactly one
     __shared__ uint32_t s_multi;   // some adapter char matches more or fewer than one code
     if (threadIdx.x == 0) s_multi = 0;
@@ -3899,7 +3955,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                 const bool slot_in = DMX_BOUND(R.pk.bd, slots, slot, kBufSlot);
                 const int cst = c.cost, iend = c.iend;
                 const int j = (int)c.j;
-                const DevAdapter& ad = P->ad[c.a];
+                const AdLite ad = ad_lite(s_amk[c.a]);
+                const int8_t* const acc = s_bacc + 72 * c.a;
                 const uint64_t t = iend == ad.m ? (uint64_t)j : (uint64_t)c.len + 1 + iend;
                 TaskView tv;
                 tv.read = 0;
@@ -3920,15 +3977,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #endif
                 if (e == 0)
                     band_dp_cost<CMIN == 0 ? 1 : CMIN, CMAX, false>(
-                        wc, fast, s_rm + c.a, R.pk, tv, ad.where == kFront, iend, j, c2,
+                        wc, fast, s_rm + c.a, R.pk, tv, ad.front, iend, j, c2,
                         origin, score);
                 else
                     band_dp_cost<CMIN == 0 ? 1 : CMIN, CMAX, true>(
-                        wc, fast, s_rm + c.a, R.pk, tv, ad.where == kFront, iend, j, c2,
+                        wc, fast, s_rm + c.a, R.pk, tv, ad.front, iend, j, c2,
                         origin, score);
                 if (c2 != cst) atomicOr(R.flags, 2u);    // band / scan disagreement: bug
                 const int lr = iend + (origin < 0 ? origin : 0);
-                if (slot_in && lr >= 0 && cst <= (int)ad.acc[lr]) {
+                if (slot_in && lr >= 0 && cst <= (int)acc[lr]) {
                     Outcome out;
                     out.key = make_key(score, c.o, cst, c.a, t);
                     out.origin = origin;
@@ -3950,7 +4007,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             const bool slot_in = DMX_BOUND(R.pk.bd, slots, slot, kBufSlot);
             const int cost = c.cost, iend = c.iend;
             const int j = (int)c.j;
-            const uint64_t t = iend == P->ad[c.a].m ? (uint64_t)j : (uint64_t)c.len + 1 + iend;
+            const uint64_t t = iend == (int)(s_amk[c.a] & 255u) ? (uint64_t)j
+                                                               : (uint64_t)c.len + 1 + iend;
             Outcome out;
             out.key = ~0ull;
             out.origin = 0;
@@ -3963,7 +4021,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                     const int origin = j - iend;
                     const int score = j >= iend ? iend : j;
                     const int lr = iend + (origin < 0 ? origin : 0);
-                    if (lr >= 0 && 0 <= (int)P->ad[c.a].acc[lr]) {
+                    if (lr >= 0 && 0 <= (int)s_bacc[72 * c.a + lr]) {
                         out.key = make_key(score, c.o, 0, c.a, t);
                         out.origin = origin;
                         out.pad = (int32_t)slot;
