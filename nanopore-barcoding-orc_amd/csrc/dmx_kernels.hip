@@ -3865,6 +3865,10 @@ __device__ __forceinline__ void band_dp_cost(int wc, bool fast, const uint8_t* r
 // so the DP waves are full whatever the prune rate; a pass first sorts its cells by cost, so each
 // wave runs the narrowest band its cells allow (band_dp_cost).  The slot's best is the minimum
 // key over all its candidates (key order = locate's / best_match's / ReverseComplementer's order).
+#ifndef DMX_BAND_SPLIT   // list 1 in two launches, cost 4 then cost 5 (0: one launch)
+#define DMX_BAND_SPLIT 1
+#endif
+constexpr bool kBandSplit = DMX_BAND_SPLIT != 0;
 template <int CMIN, int CMAX>
 // Occupancy floors of list 0 (costs 1..3) and list 1 with kk <= 5: the DP passes wait on their
 // cells' loads, and 8 / 6 waves per SIMD (64 / 80 VGPRs) measured 8.44 -> 8.28 ms
@@ -3878,7 +3882,7 @@ template <int CMIN, int CMAX>
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     CMAX <= 3 ? DMX_BAND_WAVES0 : (CMAX <= 5 ? DMX_BAND_WAVES1 : 1)))) void band_cand_kernel(
-    RoundArgs R, int list) {
+    RoundArgs R, int list, int cmask) {
     // s_rm[i * kMaxAdapters + a]: bit c = adapter a's char i matches read code c.  Row-major, so
     // the lanes of a wave (one row i, different adapters) read neighbouring bytes: no bank
     // conflicts (an adapter-major table put every adapter's row i in one of 4 banks).
@@ -4000,9 +4004,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
         const uint32_t ti = base + threadIdx.x;
-        if (ti < total) {
-            const uint32_t ci = sm.phys(ti);
-            const Cand c = cl[ci];
+        const uint32_t ci = ti < total ? sm.phys(ti) : 0u;
+        Cand c{};
+        if (ti < total) c = cl[ci];
+        // cmask != 0: this launch takes the list's cells whose cost has its bit set (the others'
+        // outcomes are written by the launch that takes them)
+        if (ti < total && (cmask == 0 || ((cmask >> c.cost) & 1))) {
             const uint32_t slot = slot_of(R, c.item, c.sub);
             const bool slot_in = DMX_BOUND(R.pk.bd, slots, slot, kBufSlot);
             const int cost = c.cost, iend = c.iend;
@@ -4751,6 +4758,8 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
         DMX_DBG_SYNC("iscreen");
         hipEventRecord(c->ev[13 + round], st);
         set_kid(R.pk.bd, kKerWscan);
+        // (near-start tasks in a second launch, pruned against the slot lower bounds of the
+        // first: measured no faster, profiles/r6_ab_wscan_near_phase_*.txt)
         if (band) hipLaunchKernelGGL(wscan_kernel<true>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         else hipLaunchKernelGGL(wscan_kernel<false>, dim3(256 * 16), dim3(kScanBlock), 0, st, R);
         DMX_DBG_SYNC("wscan_kernel");
@@ -4766,13 +4775,28 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     hipEventRecord(c->ev[round * 3 + 1], st);
     if (band) {
         set_kid(R.pk.bd, kKerBand0);
-        hipLaunchKernelGGL((band_cand_kernel<0, 3>), dim3(256 * 8), dim3(256), 0, st, R, 0);
+        // (list 0 in two launches, costs 0..2 then 3, measured slower: round 2's band 2.15 ->
+        // 2.30 ms, profiles/r6_ab_band_list0_split.txt)
+        hipLaunchKernelGGL((band_cand_kernel<0, 3>), dim3(256 * 8), dim3(256), 0, st, R, 0, 0);
         DMX_DBG_SYNC("band_cand_kernel<0, 3>");
         set_kid(R.pk.bd, kKerBand1);
-        if (c->band_wide[round])
-            hipLaunchKernelGGL((band_cand_kernel<4, 7>), dim3(256 * 4), dim3(256), 0, st, R, 1);
-        else   // every cost in list 1 is <= 5: a band of 2 * 5 + 1 diagonals is exact
-            hipLaunchKernelGGL((band_cand_kernel<4, 5>), dim3(256 * 4), dim3(256), 0, st, R, 1);
+        if (c->band_wide[round] && kBandSplit) {   // costs 4, 5, then 6..7 (as below)
+            hipLaunchKernelGGL((band_cand_kernel<4, 7>), dim3(256 * 4), dim3(256), 0, st, R, 1, 16);
+            hipLaunchKernelGGL((band_cand_kernel<4, 7>), dim3(256 * 4), dim3(256), 0, st, R, 1, 32);
+            hipLaunchKernelGGL((band_cand_kernel<4, 7>), dim3(256 * 4), dim3(256), 0, st, R, 1, 192);
+        } else if (c->band_wide[round]) {
+            hipLaunchKernelGGL((band_cand_kernel<4, 7>), dim3(256 * 4), dim3(256), 0, st, R, 1, 0);
+        } else if (kBandSplit) {
+            // every cost in list 1 is <= 5 (a band of 2 * 5 + 1 diagonals is exact).  The cost-4
+            // cells first: their exact keys are in the winner slots when the cost-5 launch
+            // screens its cells (a cost-5 cell's score is at most 49 of 59, below a cost-4
+            // winner's unless that has 2+ deletions), so fewer cost-5 DPs run (band 3.74 / 2.81
+            // -> 2.98 / 2.15 ms per round, profiles/r6_ab_band_list1_split.txt).
+            hipLaunchKernelGGL((band_cand_kernel<4, 5>), dim3(256 * 4), dim3(256), 0, st, R, 1, 16);
+            hipLaunchKernelGGL((band_cand_kernel<4, 5>), dim3(256 * 4), dim3(256), 0, st, R, 1, 32);
+        } else {
+            hipLaunchKernelGGL((band_cand_kernel<4, 5>), dim3(256 * 4), dim3(256), 0, st, R, 1, 0);
+        }
         DMX_DBG_SYNC("band_cand_kernel<4, 5|7>");
         set_kid(R.pk.bd, kKerSelectCand);
         hipLaunchKernelGGL(select_cand_kernel, dim3(1024), dim3(256), 0, st, R);
