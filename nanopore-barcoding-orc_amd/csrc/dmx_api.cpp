@@ -481,7 +481,9 @@ static void build_pieces(const Ctx* c, const char* const* seqs, const int* lens,
     // Sampled offsets: any `step` consecutive offsets j0 .. j0+step-1 of a piece cover every copy
     // (one of its 8-mers sits at a sampled position).  Per piece take the window whose 8-mers the
     // fewest other pieces share (pieces of different adapters that overlap a shared constant
-    // block share 8-mers, and every entry of a key is checked on each sampled hit of it).
+    // block share 8-mers, and every entry of a key is checked on each sampled hit of it).  The
+    // offset is a 2-bit field that both screens read the copy back with (the flat scan holds the
+    // codes of nt [X - 3, X + 29) per sampled nt X), so the window ends at offset kPieceMaxOff.
     std::map<uint32_t, int> mult;
     for (const Pc& x : uq)
         for (int off = 0; off + kPieceK <= x.len; ++off) ++mult[(x.val >> (2 * off)) & 0xFFFFu];
@@ -490,7 +492,7 @@ static void build_pieces(const Ctx* c, const char* const* seqs, const int* lens,
     bool any1 = false;
     for (const Pc& x : uq) {
         int best = 0, bcost = 1 << 30;
-        for (int j0 = 0; j0 + step - 1 + kPieceK <= x.len; ++j0) {
+        for (int j0 = 0; j0 + step - 1 <= kPieceMaxOff && j0 + step - 1 + kPieceK <= x.len; ++j0) {
             int cost = 0;
             for (int off = j0; off < j0 + step; ++off) cost += mult[(x.val >> (2 * off)) & 0xFFFFu];
             if (cost < bcost) bcost = cost, best = j0;

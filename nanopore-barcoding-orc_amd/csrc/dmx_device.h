@@ -139,6 +139,7 @@ constexpr int kPieceBitmapWords = 1 << (2 * kPieceK - 5);
 // its length, orientation, the sampled 8-mer's offset inside it, and the range of alignment end
 // columns after the copy (dlo, dhi; + 128); the flat scan's combined table tags each entry with
 // its round (bit 56).
+constexpr int kPieceMaxOff = 3;            // an entry's 8-mer offset in its piece: 2 bits
 __host__ __device__ inline uint64_t piece_entry(uint32_t val, int len, int o, int off, int dlo,
                                                 int dhi, int round = 0) {
     return (uint64_t)val | ((uint64_t)len << 32) | ((uint64_t)o << 37) | ((uint64_t)off << 38) |

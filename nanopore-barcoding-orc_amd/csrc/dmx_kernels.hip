@@ -4776,7 +4776,8 @@ int launch_round(Ctx* c, int round, hipStream_t st) {
     if (band) {
         set_kid(R.pk.bd, kKerBand0);
         // (list 0 in two launches, costs 0..2 then 3, measured slower: round 2's band 2.15 ->
-        // 2.30 ms, profiles/r6_ab_band_list0_split.txt)
+        // 2.30 ms, profiles/r6_ab_band_list0_split.txt; the exact cost-0 cells first, then costs 1..3,
+        // 2.98 -> 3.21 ms, profiles/r6_ab_band_zero_first.txt)
         hipLaunchKernelGGL((band_cand_kernel<0, 3>), dim3(256 * 8), dim3(256), 0, st, R, 0, 0);
         DMX_DBG_SYNC("band_cand_kernel<0, 3>");
         set_kid(R.pk.bd, kKerBand1);

@@ -12,7 +12,7 @@ import pytest
 
 import oracle
 from dmx import lib, synth
-from test_pieces_host import full_k, mutate, pieces_of, revcomp
+from test_pieces_host import _flank_cases, full_k, mutate, pieces_of, revcomp
 
 pytestmark = pytest.mark.gpu
 
@@ -28,12 +28,12 @@ def _rand(rng, n, alphabet="ACGT", p=None):
     return "".join(rng.choice(list(alphabet), size=int(n), p=p))
 
 
-def adversarial_reads(rng, panel, where):
+def adversarial_reads(rng, panel, where, rate=0.1):
     """Reads holding one adapter copy with K edits (one surviving piece), plus partial copies at
     the read ends (a FRONT adapter's suffix at the start, a BACK adapter's prefix at the end)."""
     seqs = []
     for ad in panel:
-        K = full_k(len(ad), 0.1)
+        K = full_k(len(ad), rate)
         pcs = pieces_of(len(ad), K)
         for survive in range(K + 1):
             for place in ("start", "middle", "end"):
@@ -199,3 +199,31 @@ def test_two_round_mixed_screens(case, monkeypatch):
         tasks = c.stats()["filter_tasks"]
     _assert_same(got, exp)
     assert tasks[1] > 0 and (tasks[0] == 0) == (case == "iupac_round1")
+
+
+@pytest.mark.parametrize("variant", ["flat", "no_flat"])
+@pytest.mark.parametrize("name,panel,where,rate", _flank_cases())
+def test_shared_flank_panels(name, panel, where, rate, variant, monkeypatch):
+    """Panels whose adapters share a constant prefix and suffix: pieces that straddle a shared
+    block sample a window past offset 0 (the tools/parity_sweep.py seed-56 mismatches, when
+    offsets 4 .. 8 overflowed the entries' 2-bit field)."""
+    w = oracle.FRONT if where == lib.DMX_FRONT else oracle.BACK
+    rng = np.random.default_rng(200 + len(name))
+    seqs = adversarial_reads(rng, panel, w, rate)
+    for ad in panel:   # exact copies at every start modulo the sampling stride
+        for shift in range(4):
+            s = _rand(rng, 40 + shift) + ad + _rand(rng, 60)
+            seqs.append(revcomp(s) if rng.random() < 0.5 else s)
+    blob, offs, lens = oracle.pack_ascii(seqs)
+    exp = oracle.run_batch(oracle.Panel(panel, w, max_errors=rate), None, blob, offs, lens,
+                           mode=0, use_rc=True, threads=8)
+    assert (exp["bin1"] >= 0).mean() > 0.5
+    if variant == "no_flat":
+        monkeypatch.setenv("DMX_NO_FLAT", "1")
+    with lib.Context(0) as c:
+        c.set_panel(0, panel, where | lib.DMX_RC, rate)
+        c.set_mode(lib.MODE_SINGLE)
+        got = c.run(lib.pack(blob, offs, lens))
+        tasks = c.stats()["filter_tasks"]
+    _assert_same(got, exp)
+    assert tasks[0] > 0

@@ -176,3 +176,74 @@ def test_reads_with_n_only_add_marks():
         read = left + copy
         marks = model_marks(read, ents, info["step"], 2)
         assert len(read) in marks[0]
+
+
+def _shared_flank_panel(rng, n, pre, suf, lo, hi):
+    """Adapters that share a constant prefix and suffix (as in the sweep's random panels): the
+    pieces that straddle a shared block are the ones whose sampled window starts past offset 0."""
+    p = "".join(rng.choice(list("ACGT"), size=pre))
+    s = "".join(rng.choice(list("ACGT"), size=suf))
+    return [p + "".join(rng.choice(list("ACGT"), size=int(L))) + s
+            for L in rng.integers(lo, hi, size=n)]
+
+
+# a panel of tools/parity_sweep.py seed 56 whose pieces took sampled windows at offsets 4 .. 8,
+# beyond the entries' 2-bit offset field (read back as offsets 0 .. 3 with a shifted end range)
+SWEEP56_PANEL = [
+    "CGAAGACTCGCTCCTAGGTTTCGGACGGCCCGTGTTTACAACCCCTACGCC", "CGAAGACTCTAACCACAACCCCTACGCC",
+    "CGAAGACTCCAACGGAACGGTCCCACAACCCCTACGCC", "CGAAGACTCGCTATCATTTTTTGCTAAACAACCCCTACGCC",
+    "CGAAGACTCTCTCGCCAGTAGTTGGGGAATCCCCTTAACAACCCCTACGCC",
+    "CGAAGACTCCCGACGGTTCTAAACTTCCTTACAACCCCTACGCC", "CGAAGACTCCCTATGGCGAATTTAGACAACCCCTACGCC",
+    "CGAAGACTCCAGCCTGTTGAGTAAATTACAACCCCTACGCC", "CGAAGACTCGAATCCGCCAACAACCCCTACGCC",
+    "CGAAGACTCAAGCCAGTACAACCCCTACGCC", "CGAAGACTCCGCGATACAACCCCTACGCC",
+    "CGAAGACTCTAACGGCCGTGAAGAGGGGGTACACAACCCCTACGCC",
+]
+
+
+def _flank_cases():
+    rng = np.random.default_rng(56)
+    out = [("sweep56", SWEEP56_PANEL, lib.DMX_FRONT, 0.0)]
+    for i, (where, rate) in enumerate([(lib.DMX_FRONT, 0.05), (lib.DMX_BACK, 0.0),
+                                       (lib.DMX_BACK, 0.05), (lib.DMX_FRONT, 0.1)]):
+        out.append((f"flank{i}", _shared_flank_panel(rng, 12, int(rng.integers(5, 14)),
+                                                     int(rng.integers(8, 20)), 8, 35), where, rate))
+    return out
+
+
+@pytest.mark.parametrize("name,seqs,where,rate", _flank_cases())
+def test_entries_keep_their_piece_end_range(name, seqs, where, rate):
+    """Every entry of a piece carries the piece's own end range and an offset the screens can read
+    back: the `step` sampled offsets of a piece are consecutive and start at 0 .. 4 - step."""
+    rc, info, ents = lib.panel_pieces(seqs, where | lib.DMX_RC, rate)
+    assert rc == 0 and info["step"] > 0, name
+    by_piece = {}
+    for e in ents:
+        by_piece.setdefault((e["val"], e["len"], e["o"]), []).append(e)
+    assert len(by_piece) == info["pieces"]
+    for key, es in by_piece.items():
+        assert len({(e["dlo"], e["dhi"]) for e in es}) == 1, (name, key)
+        assert es[0]["dlo"] <= es[0]["dhi"]
+        offs = sorted(e["off"] for e in es)
+        assert offs == list(range(offs[0], offs[0] + info["step"])) and offs[-1] <= 3, (name, key)
+
+
+@pytest.mark.parametrize("name,seqs,where,rate", _flank_cases())
+def test_shared_flank_copies_end_in_marked_columns(name, seqs, where, rate):
+    """Exact copies and K-edit copies (one surviving piece) of every adapter of a shared-flank
+    panel, at every start modulo the sampling stride, end in a marked column."""
+    rc, info, ents = lib.panel_pieces(seqs, where | lib.DMX_RC, rate)
+    step = info["step"]
+    rng = np.random.default_rng(len(name))
+    for ad in seqs:
+        K = full_k(len(ad), rate)
+        pcs = pieces_of(len(ad), K)
+        for survive in range(K + 1):
+            for shift in range(step):
+                copy = mutate(rng, ad, pcs, survive) if K else ad
+                left = "".join(rng.choice(list("ACGT"), size=20 + shift))
+                view0 = left + copy + "".join(rng.choice(list("ACGT"), size=30))
+                for rc_read in (False, True):
+                    read = revcomp(view0) if rc_read else view0
+                    marks = model_marks(read, ents, step, 2)
+                    assert len(left) + len(copy) in marks[1 if rc_read else 0], \
+                        (name, ad, survive, shift, rc_read)
