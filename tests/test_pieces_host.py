@@ -247,3 +247,34 @@ def test_shared_flank_copies_end_in_marked_columns(name, seqs, where, rate):
                     marks = model_marks(read, ents, step, 2)
                     assert len(left) + len(copy) in marks[1 if rc_read else 0], \
                         (name, ad, survive, shift, rc_read)
+
+
+def test_entry_fields_on_random_panels():
+    """The packed entry fields read back as built on 60 random panels (lengths 8..64, shared
+    flanks or none, -e 0..0.3): per piece one end range, dlo <= dhi, `step` consecutive offsets
+    <= 3, lengths 8..16; every key's 8-mer is the piece's codes at the entry's offset."""
+    rng = np.random.default_rng(123)
+    seen = 0
+    for _ in range(60):
+        n = int(rng.integers(1, 25))
+        pre, suf = int(rng.integers(0, 16)), int(rng.integers(0, 24))
+        lo = int(rng.integers(4, 30))
+        seqs = [s[:64] for s in _shared_flank_panel(rng, n, pre, suf, lo, lo + 30)]
+        seqs = [s for s in seqs if len(s) >= 8] or ["ACGTACGTACGTACGTAC"]
+        where = lib.DMX_FRONT if rng.random() < 0.5 else lib.DMX_BACK
+        rate = float(rng.choice([0.0, 0.05, 0.1, 0.1, 0.2, 0.3]))
+        rc, info, ents = lib.panel_pieces(seqs, where | lib.DMX_RC, rate)
+        assert rc == 0
+        if not info["step"]:
+            continue
+        seen += 1
+        by_piece = {}
+        for e in ents:
+            by_piece.setdefault((e["val"], e["len"], e["o"]), []).append(e)
+        for es in by_piece.values():
+            assert len({(e["dlo"], e["dhi"]) for e in es}) == 1
+            assert es[0]["dlo"] <= es[0]["dhi"] and 8 <= es[0]["len"] <= 16
+            offs = sorted(e["off"] for e in es)
+            assert offs == list(range(offs[0], offs[0] + info["step"])) and offs[-1] <= 3
+            assert offs[-1] + 8 <= es[0]["len"]
+    assert seen >= 10
