@@ -12,7 +12,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "nanopore-barcoding-orc_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
+import oracle  # noqa: E402  (its Where constants only)
 from dmx import lib  # noqa: E402
 
 
@@ -22,7 +24,7 @@ def run(p, seqs, item, tag):
     offs = np.zeros(len(seqs), dtype=np.uint64)
     offs[1:] = np.cumsum(lens[:-1])
     with lib.Context(0) as ctx:
-        ctx.set_panel_mixed(0, p["panel"], [lib.DMX_FRONT if w == 11 else lib.DMX_BACK
+        ctx.set_panel_mixed(0, p["panel"], [lib.DMX_FRONT if w == oracle.FRONT else lib.DMX_BACK
                                             for w in p["wheres"]], p["rc"], p["e"],
                             p["min_overlap"])
         ctx.set_mode(lib.MODE_SINGLE)
